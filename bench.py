@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Roundtable benchmark: wall-clock per round + aggregate knight tokens/s (BASELINE.json metric).
+
+Workload (one "step" = one complete discussion round):
+  * knights are Llama-3-8B (bf16, random-init weights: there are no checkpoints), 3 per
+    table, a table = one 3-knight ``discuss`` (BASELINE config 2 / metric "3-knight discuss");
+  * N GPUs host N tables (3N knights). Knight j of table t lives on rank (3t + j) mod N,
+    so every GPU hosts exactly 3 knights (batched in one decode hipGraph) and every table
+    spans min(3, N) GPUs — each round's responses cross xGMI in the RCCL all-gather (C1).
+    Per-GPU work is fixed as N grows: ``scaling: weak``;
+  * ``parallel`` round mode, ``append`` prompt layout, the real orchestrator
+    (prompt assembly, consensus parse, discussion.md/metrics writes) inside the timed region;
+  * fixed ``--new-tokens`` per turn with EOS ignored (random weights never emit a
+    consensus block; BASELINE.md measurement protocol).
+
+The reference publishes no numbers (BASELINE.json "published": {}), so ``vs_baseline`` is
+null; ``reference_bound_ms_per_round`` records its implied upper bound (3 knights x the
+120 s per-turn timeout, sequential) for context.
+
+Launch: ``python bench.py --gpus 1`` or, for N > 1,
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+TOPIC = ("Hoe structureren we de resident KV-cache van elke knight zodat een discussie van vijf rondes "
+         "volledig in HBM blijft, en welke consistentie-garanties geven we bij een crash midden in een ronde?")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3, help="timed rounds")
+    p.add_argument("--warmup", type=int, default=1, help="untimed rounds (round 1 includes the initial prefill)")
+    p.add_argument("--model", default="llama3-8b")
+    p.add_argument("--knights-per-gpu", type=int, default=3)
+    p.add_argument("--knights-per-table", type=int, default=3)
+    p.add_argument("--new-tokens", type=int, default=512, help="decode tokens per knight turn")
+    p.add_argument("--temperature", type=float, default=0.7)
+    p.add_argument("--top-p", type=float, default=0.95)
+    p.add_argument("--round-mode", default="parallel", choices=["parallel"])
+    p.add_argument("--layout", default="append", choices=["append", "reference"])
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--device", default=None, help="override device (cpu for a plumbing run)")
+    p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return p.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    import torch
+    from theroundtaible_amd.engine.engine import Engine, EngineConfig
+    from theroundtaible_amd.engine.sampler import SamplingParams
+    from theroundtaible_amd.knights.distributed import DistributedPool, RemoteKnight
+    from theroundtaible_amd.knights.engine_backend import EngineBackend
+    from theroundtaible_amd.orchestrator import Orchestrator, RunOptions, run_tables_parallel
+    from theroundtaible_amd.parallel.cluster import init_cluster
+    from theroundtaible_amd.types import RoundtableConfig
+
+    cl = init_cluster(prefer_gpu=args.device != "cpu")
+    N = cl.world
+    device = args.device or cl.device
+    kpt = args.knights_per_table
+    total_knights = args.knights_per_gpu * N
+    n_tables = max(1, total_knights // kpt)
+    base_names = ["Claude", "Gemini", "GPT", "Mistral", "Llama", "Qwen", "Phi", "Falcon"]
+    placement = {}
+    tables = []
+    for t in range(n_tables):
+        knights = []
+        for j in range(kpt):
+            name = f"{base_names[j % len(base_names)]}-{t}"
+            placement[name] = [(kpt * t + j) % N]
+            knights.append({"name": name, "adapter": f"local-llm-{name.lower()}", "capabilities": ["architecture"],
+                            "priority": j + 1})
+        tables.append(knights)
+    local_names = [n for n, ranks in placement.items() if cl.rank in ranks]
+
+    t_load = time.perf_counter()
+    engine = Engine(EngineConfig(model=args.model, weights=f"random:{1234}", device=device,
+                                 use_graphs=not args.no_graphs and device != "cpu",
+                                 dtype="bf16" if device != "cpu" else "fp32"))
+    params = SamplingParams(temperature=args.temperature, top_p=args.top_p, max_new_tokens=args.new_tokens,
+                            ignore_eos=True, stop_on_consensus=False, seed=7)
+    import threading
+    lock = threading.Lock()
+    local = {n: EngineBackend(n, f"local-llm-{n.lower()}", engine, params, lock) for n in local_names}
+    pool = DistributedPool(cl, placement, local, engine.tokenizer)
+    load_s = time.perf_counter() - t_load
+
+    rounds = args.warmup + args.steps
+    workdir = tempfile.mkdtemp(prefix=f"rt-bench-r{cl.rank}-")
+    orchs = []
+    for t, knights in enumerate(tables):
+        cfg = RoundtableConfig.from_dict({
+            "version": "1.0", "project": "bench", "language": "nl", "knights": knights,
+            "rules": {"max_rounds": rounds, "consensus_threshold": 9, "timeout_per_turn_seconds": 3600,
+                      "escalate_to_user_after": rounds + 1, "auto_execute": False, "ignore": [".git"],
+                      "round_mode": args.round_mode, "prompt_layout": args.layout},
+            "chronicle": ".roundtable/chronicle.md", "adapter_config": {}})
+        backends = {k["adapter"]: RemoteKnight(pool, k["name"], k["name"], k["adapter"]) for k in knights}
+        orchs.append(Orchestrator(cfg, backends, workdir, options=RunOptions(shuffle_seed=1000 + t,
+                                                                             max_new_tokens=args.new_tokens),
+                                  store_root=workdir))
+
+    timing = {}
+
+    def on_round(rnd: int, ms: float):
+        if rnd == args.warmup:
+            if device.startswith("cuda"):
+                torch.cuda.synchronize()
+            cl.barrier()
+            timing["t0"] = time.perf_counter()
+        if rnd == rounds:
+            if device.startswith("cuda"):
+                torch.cuda.synchronize()
+            cl.barrier()
+            timing["t1"] = time.perf_counter()
+
+    if args.warmup == 0:
+        cl.barrier()
+        timing["t0"] = time.perf_counter()
+    run_tables_parallel(orchs, [f"{TOPIC} (tafel {t})" for t in range(n_tables)], on_round=on_round)
+    elapsed = cl.max_scalar(timing["t1"] - timing["t0"])
+    timed = range(args.warmup + 1, rounds + 1)
+    dec = pre = reused = 0
+    for o in orchs:
+        for e in o.all_rounds:
+            if e.round in timed:
+                dec += int(e.metrics.get("decode_tokens", 0))
+                pre += int(e.metrics.get("prefill_tokens", 0))
+                reused += int(e.metrics.get("reused_tokens", 0))
+    exch = sum(pool.exchange_ms[-args.steps:]) / max(1, args.steps) if pool.exchange_ms else 0.0
+    ms_round = elapsed / max(1, args.steps) * 1e3
+    value = dec / elapsed if elapsed > 0 else 0.0
+    ref_bound_ms = kpt * 120_000.0
+    out = {
+        "metric": "aggregate knight tokens/sec (3-knight discuss tables, parallel rounds)",
+        "value": round(value, 2), "unit": "tokens/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_round, 2), "ms_per_round": round(ms_round, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "reference_bound_ms_per_round": ref_bound_ms, "speedup_vs_reference_bound": round(ref_bound_ms / ms_round, 1),
+        "dtype": "bf16" if device != "cpu" else "fp32", "data": "synthetic prompts, random-init weights",
+        "config": {"model": args.model, "knights_per_table": kpt, "tables": n_tables, "knights": kpt * n_tables,
+                   "knights_per_gpu": args.knights_per_gpu, "new_tokens_per_turn": args.new_tokens,
+                   "global_batch": kpt * n_tables, "seq_len": args.new_tokens,
+                   "round_mode": args.round_mode, "prompt_layout": args.layout,
+                   "parallelism": f"knight-placement x{N} (tables striped over GPUs), C1 all-gather"},
+        "detail": {"decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
+                   "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
+                   "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
+                   "kv_capacity_tokens": engine.kv_capacity_tokens},
+    }
+    if cl.rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    cl.barrier()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

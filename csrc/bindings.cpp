@@ -1,0 +1,206 @@
+// pybind11 bindings: torch tensors -> raw HIP launchers on the current HIP stream
+// (so every kernel is captured by torch.cuda.graph / hipGraph like any torch op).
+// Every entry point validates dtype / device / contiguity / shape BEFORE launching:
+// a hand-written kernel must never see operands its grid does not assume.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+void launch_norm(void* out, const void* x, void* res, const void* w, const void* b, int rows, int H, float eps,
+                 bool add, bool ln, hipStream_t stream);
+void launch_rope_cache(void* q_out, const void* qkv, const int64_t* positions, const float* cos_sin, void* k_cache,
+                       void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int BS, int64_t qkv_stride,
+                       bool rope, hipStream_t stream);
+void launch_silu_mul(void* out, const void* x, int rows, int I, hipStream_t stream);
+void launch_gelu(void* out, const void* x, int64_t n, hipStream_t stream);
+int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                        const int* ctx_lens, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D,
+                        int max_blocks, float scale, int num_splits, hipStream_t stream);
+int prefill_rows_per_tile(int G);
+int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                   const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv, int D,
+                   int max_blocks, float scale, hipStream_t stream);
+int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
+                  const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
+                  const int64_t* offsets, hipStream_t stream);
+
+namespace {
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_bf16(const torch::Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bfloat16");
+}
+void check_type(const torch::Tensor& t, torch::ScalarType st, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == st, name, " has wrong dtype");
+}
+
+void norm_common(torch::Tensor& out, const torch::Tensor& x, torch::Tensor* res, const torch::Tensor& w,
+                 const torch::Tensor* b, double eps, bool ln) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  const int64_t H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0 && H <= 32768, "hidden size must be a multiple of 8 and <= 32768");
+  TORCH_CHECK(w.numel() == H && out.sizes() == x.sizes(), "norm shape mismatch");
+  if (res) {
+    check_bf16(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch");
+  }
+  if (b) {
+    check_bf16(*b, "bias");
+    TORCH_CHECK(b->numel() == H, "bias shape mismatch");
+  }
+  const int rows = (int)(x.numel() / H);
+  if (rows == 0) return;
+  launch_norm(out.data_ptr(), x.data_ptr(), res ? res->data_ptr() : nullptr, w.data_ptr(), b ? b->data_ptr() : nullptr,
+              rows, (int)H, (float)eps, res != nullptr, ln, cur_stream());
+}
+
+void rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, double eps) {
+  norm_common(out, x, nullptr, w, nullptr, eps, false);
+}
+void fused_add_rms_norm(torch::Tensor out, torch::Tensor x, torch::Tensor res, torch::Tensor w, double eps) {
+  norm_common(out, x, &res, w, nullptr, eps, false);
+}
+void layer_norm(torch::Tensor out, torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps) {
+  norm_common(out, x, nullptr, w, &b, eps, true);
+}
+void fused_add_layer_norm(torch::Tensor out, torch::Tensor x, torch::Tensor res, torch::Tensor w, torch::Tensor b,
+                          double eps) {
+  norm_common(out, x, &res, w, &b, eps, true);
+}
+
+void check_caches(const torch::Tensor& kc, const torch::Tensor& vc, int64_t Hkv, int64_t D) {
+  check_bf16(kc, "k_cache");
+  check_bf16(vc, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && vc.dim() == 4, "caches must be 4-D");
+  TORCH_CHECK(kc.size(1) == Hkv && kc.size(3) == D, "k_cache must be [NB, Hkv, BS, D]");
+  TORCH_CHECK(vc.size(0) == kc.size(0) && vc.size(1) == Hkv && vc.size(2) == D && vc.size(3) == kc.size(2),
+              "v_cache must be [NB, Hkv, D, BS]");
+}
+
+void rope_and_cache(torch::Tensor q_out, torch::Tensor qkv, torch::Tensor positions, torch::Tensor cos_sin,
+                    torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots, int64_t Hq, int64_t Hkv,
+                    int64_t D) {
+  check_bf16(q_out, "q_out");
+  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == torch::kBFloat16 && qkv.stride(-1) == 1, "qkv must be bf16 rows");
+  check_type(positions, torch::kInt64, "positions");
+  check_type(slots, torch::kInt64, "slot_mapping");
+  check_caches(k_cache, v_cache, Hkv, D);
+  const int64_t T = qkv.size(0);
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
+  TORCH_CHECK(positions.numel() == T && slots.numel() == T && q_out.numel() == T * Hq * D, "token count mismatch");
+  TORCH_CHECK(D % 8 == 0, "head_dim must be a multiple of 8");
+  const bool rope = cos_sin.numel() > 0;
+  if (rope) {
+    check_type(cos_sin, torch::kFloat32, "cos_sin");
+    TORCH_CHECK(cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  }
+  launch_rope_cache(q_out.data_ptr(), qkv.data_ptr(), positions.data_ptr<int64_t>(),
+                    rope ? cos_sin.data_ptr<float>() : nullptr, k_cache.data_ptr(), v_cache.data_ptr(),
+                    slots.data_ptr<int64_t>(), (int)T, (int)Hq, (int)Hkv, (int)D, (int)k_cache.size(2), qkv.stride(0),
+                    rope, cur_stream());
+}
+
+void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
+                            torch::Tensor block_tables, torch::Tensor ctx_lens, double scale, int64_t num_splits,
+                            torch::Tensor part_o, torch::Tensor part_ml) {
+  check_bf16(out, "out");
+  check_bf16(q, "q");
+  TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
+  const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
+  check_caches(k_cache, v_cache, k_cache.size(1), D);
+  TORCH_CHECK(k_cache.size(2) == 32, "decode kernel requires kv block_size == 32");
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_type(ctx_lens, torch::kInt32, "ctx_lens");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && ctx_lens.numel() >= B, "metadata shape");
+  check_type(part_o, torch::kFloat32, "partial_o");
+  check_type(part_ml, torch::kFloat32, "partial_ml");
+  TORCH_CHECK(num_splits >= 1 && part_o.numel() >= B * Hq * num_splits * D && part_ml.numel() >= B * Hq * num_splits * 2,
+              "split workspace too small");
+  const int rc = launch_paged_decode(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                     block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), part_o.data_ptr<float>(),
+                                     part_ml.data_ptr<float>(), (int)B, (int)Hq, (int)k_cache.size(1), (int)D,
+                                     (int)block_tables.size(1), (float)scale, (int)num_splits, cur_stream());
+  TORCH_CHECK(rc == 0, "paged_attention_decode: unsupported configuration (rc=", rc, ")");
+}
+
+void prefill_attention(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
+                       torch::Tensor block_tables, torch::Tensor cu_q, torch::Tensor start_pos, torch::Tensor tile_map,
+                       double scale) {
+  check_bf16(out, "out");
+  check_bf16(q, "q");
+  TORCH_CHECK(q.dim() == 3, "q must be [T, Hq, D]");
+  const int64_t Hq = q.size(1), D = q.size(2);
+  check_caches(k_cache, v_cache, k_cache.size(1), D);
+  TORCH_CHECK(k_cache.size(2) == 32, "prefill kernel requires kv block_size == 32");
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_type(cu_q, torch::kInt32, "cu_q");
+  check_type(start_pos, torch::kInt32, "start_pos");
+  check_type(tile_map, torch::kInt32, "tile_map");
+  TORCH_CHECK(block_tables.size(0) == cu_q.numel() - 1 && start_pos.numel() == cu_q.numel() - 1, "varlen metadata");
+  TORCH_CHECK(tile_map.dim() == 2 && tile_map.size(1) == 2, "tile_map must be [n, 2]");
+  const int rc = launch_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                block_tables.data_ptr<int>(), cu_q.data_ptr<int>(), start_pos.data_ptr<int>(),
+                                tile_map.data_ptr<int>(), (int)tile_map.size(0), (int)Hq, (int)k_cache.size(1), (int)D,
+                                (int)block_tables.size(1), (float)scale, cur_stream());
+  TORCH_CHECK(rc == 0, "prefill_attention: unsupported configuration (rc=", rc, ")");
+}
+
+void silu_and_mul(torch::Tensor out, torch::Tensor x) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  const int64_t I = x.size(-1) / 2;
+  TORCH_CHECK(x.size(-1) % 16 == 0 && out.size(-1) == I && out.numel() * 2 == x.numel(), "silu_and_mul shape");
+  launch_silu_mul(out.data_ptr(), x.data_ptr(), (int)(x.numel() / x.size(-1)), (int)I, cur_stream());
+}
+
+void gelu_tanh(torch::Tensor out, torch::Tensor x) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  TORCH_CHECK(x.numel() % 8 == 0 && out.numel() == x.numel(), "gelu shape");
+  launch_gelu(out.data_ptr(), x.data_ptr(), x.numel(), cur_stream());
+}
+
+void sample(torch::Tensor out, torch::Tensor logits, torch::Tensor temperature, torch::Tensor top_p,
+            torch::Tensor top_k, torch::Tensor seeds, torch::Tensor offsets) {
+  check_type(out, torch::kInt64, "out");
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V] row-major");
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "logits must be bf16 or fp32");
+  const int64_t B = logits.size(0);
+  check_type(temperature, torch::kFloat32, "temperature");
+  check_type(top_p, torch::kFloat32, "top_p");
+  check_type(top_k, torch::kInt32, "top_k");
+  check_type(seeds, torch::kInt64, "seeds");
+  check_type(offsets, torch::kInt64, "offsets");
+  TORCH_CHECK(out.numel() >= B && temperature.numel() >= B && top_p.numel() >= B && top_k.numel() >= B &&
+                  seeds.numel() >= B && offsets.numel() >= B,
+              "sampling parameter vectors shorter than the batch");
+  launch_sample(out.data_ptr<int64_t>(), logits.data_ptr(), bf, (int)B, (int)logits.size(1), logits.stride(0),
+                temperature.data_ptr<float>(), top_p.data_ptr<float>(), top_k.data_ptr<int>(),
+                seeds.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), cur_stream());
+}
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
+  m.def("rms_norm", &rms_norm);
+  m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("layer_norm", &layer_norm);
+  m.def("fused_add_layer_norm", &fused_add_layer_norm);
+  m.def("rope_and_cache", &rope_and_cache);
+  m.def("paged_attention_decode", &paged_attention_decode);
+  m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
+  m.def("prefill_attention", &prefill_attention);
+  m.def("silu_and_mul", &silu_and_mul);
+  m.def("gelu_tanh", &gelu_tanh);
+  m.def("sample", &sample);
+  m.attr("arch") = "gfx950";
+}

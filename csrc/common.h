@@ -1,0 +1,79 @@
+// Shared device helpers for the roundtable CDNA4 (gfx950) kernels.
+// wave64 everywhere: reductions use __shfl_xor over 64 lanes; block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define RT_DEVICE __device__ __forceinline__
+
+namespace rt {
+
+constexpr int kWave = 64;
+
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef short short4 __attribute__((ext_vector_type(4)));
+typedef float float4_ __attribute__((ext_vector_type(4)));
+typedef float float16_ __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// bf16 <-> f32 by bit manipulation (round-to-nearest-even on the way down; NaN kept NaN).
+RT_DEVICE float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+RT_DEVICE uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+RT_DEVICE uint32_t pack2(float lo, float hi) { return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16); }
+
+template <typename T> struct DT;
+template <> struct DT<uint16_t> {  // bf16 storage
+  static RT_DEVICE float load(const uint16_t* p) { return bf2f(*p); }
+  static RT_DEVICE void store(uint16_t* p, float v) { *p = f2bf(v); }
+};
+template <> struct DT<float> {
+  static RT_DEVICE float load(const float* p) { return *p; }
+  static RT_DEVICE void store(float* p, float v) { *p = v; }
+};
+
+RT_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+RT_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (multiple of 64). `scratch` >= 16 floats of LDS.
+RT_DEVICE float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = (lane < nw) ? scratch[lane] : 0.f;
+  return wave_sum(t);
+}
+RT_DEVICE float block_max(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = (lane < nw) ? scratch[lane] : -INFINITY;
+  return wave_max(t);
+}
+
+}  // namespace rt
+
+#define RT_HIP_CHECK(expr)                                                              \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+    }                                                                                   \
+  } while (0)

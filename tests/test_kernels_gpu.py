@@ -1,0 +1,190 @@
+"""Numerics of every HIP kernel vs the plain-PyTorch fp32 reference (ops/reference.py)."""
+import math
+
+import pytest
+import torch
+
+from theroundtaible_amd import ops
+from theroundtaible_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=DEV) * scale).to(torch.bfloat16)
+
+
+def close(a, b, atol, rtol=0.0):
+    d = (a.float() - b.float()).abs()
+    tol = atol + rtol * b.float().abs()
+    assert bool((d <= tol).all()), f"max err {d.max().item():.4g}"
+
+
+def test_native_loaded():
+    assert ops.native_available()
+    assert ops.native().arch == "gfx950"
+
+
+@pytest.mark.parametrize("H", [256, 768, 4096, 8192])
+@pytest.mark.parametrize("rows", [1, 3, 17])
+def test_rmsnorm(H, rows):
+    x, w = bf(rows, H, seed=1), bf(H, seed=2)
+    close(ops.rms_norm(x, w, 1e-5), ref.rms_norm(x.cpu(), w.cpu(), 1e-5).to(DEV), 0.02, 0.01)
+    r = bf(rows, H, seed=3)
+    exp_o, exp_r = ref.fused_add_rms_norm(x.cpu(), r.cpu(), w.cpu(), 1e-5)
+    o, r2 = ops.fused_add_rms_norm(x, r, w, 1e-5)
+    close(r2, exp_r.to(DEV), 0.0)
+    close(o, exp_o.to(DEV), 0.02, 0.01)
+
+
+@pytest.mark.parametrize("H", [128, 768])
+def test_layernorm(H):
+    x, w, b = bf(5, H, seed=1), bf(H, seed=2), bf(H, seed=4)
+    close(ops.layer_norm(x, w, b, 1e-5), ref.layer_norm(x.cpu(), w.cpu(), b.cpu(), 1e-5).to(DEV), 0.03, 0.01)
+    r = bf(5, H, seed=3)
+    eo, er = ref.fused_add_layer_norm(x.cpu(), r.cpu(), w.cpu(), b.cpu(), 1e-5)
+    o, r2 = ops.fused_add_layer_norm(x, r, w, b, 1e-5)
+    close(r2, er.to(DEV), 0.0)
+    close(o, eo.to(DEV), 0.03, 0.01)
+
+
+def test_activations():
+    x = bf(7, 2 * 1024, seed=5)
+    close(ops.silu_and_mul(x), ref.silu_and_mul(x.cpu()).to(DEV), 0.02, 0.01)
+    close(ops.gelu_tanh(x), ref.gelu_tanh(x.cpu()).to(DEV), 0.02, 0.01)
+
+
+def make_cache(nb, hkv, d, seed=0):
+    kc = bf(nb, hkv, 32, d, seed=seed)
+    vc = bf(nb, hkv, d, 32, seed=seed + 1)
+    return kc, vc
+
+
+@pytest.mark.parametrize("hq,hkv,d,rope", [(32, 8, 128, True), (12, 12, 64, False), (8, 1, 128, True)])
+def test_rope_and_cache(hq, hkv, d, rope):
+    T, nb = 37, 16
+    qkv = bf(T, (hq + 2 * hkv) * d, seed=7)
+    pos = torch.randint(0, 4000, (T,), device=DEV)
+    perm = torch.randperm(nb * 32, device=DEV)[:T]
+    cs = ref.rope_cos_sin(4096, d, 500000.0, DEV) if rope else None
+    kc, vc = make_cache(nb, hkv, d)
+    kc2, vc2 = kc.cpu().clone(), vc.cpu().clone()
+    q = ops.rope_and_cache(qkv, pos, cs, kc, vc, perm, hq, hkv, d)
+    qr = ref.rope_and_cache(qkv.cpu(), pos.cpu(), cs.cpu() if cs is not None else None, kc2, vc2, perm.cpu(),
+                            hq, hkv, d)
+    close(q, qr.to(DEV), 0.02, 0.01)
+    close(kc, kc2.to(DEV), 0.02, 0.01)
+    close(vc, vc2.to(DEV), 0.0)
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 2, 128)])
+@pytest.mark.parametrize("splits", [1, 3, 8])
+def test_paged_decode(hq, hkv, d, splits):
+    lens = [1, 31, 32, 33, 257, 1500]
+    B = len(lens)
+    nb = sum((l + 31) // 32 for l in lens) + 4
+    kc, vc = make_cache(nb, hkv, d, seed=11)
+    perm = torch.randperm(nb).tolist()
+    maxb = max((l + 31) // 32 for l in lens)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    i = 0
+    for b, l in enumerate(lens):
+        n = (l + 31) // 32
+        bt[b, :n] = torch.tensor(perm[i:i + n], dtype=torch.int32)
+        i += n
+    q = bf(B, hq, d, seed=12)
+    cl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(d)
+    ws = ops.DecodeWorkspace(B, hq, d, splits, DEV)
+    out = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws)
+    exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, cl, scale)
+    close(out, exp.to(DEV), 0.02, 0.02)
+
+
+def test_paged_decode_spike():
+    """Force the online-softmax rescale path: a key that dominates late in the sequence."""
+    hq, hkv, d, L = 32, 8, 128, 700
+    nb = 32
+    kc, vc = make_cache(nb, hkv, d, seed=3)
+    q = bf(1, hq, d, seed=4)
+    # make key 650 align strongly with every query of kv head 0
+    blk, off = 650 // 32, 650 % 32
+    kc[blk, 0, off] = (q[0, :4].float().mean(0) * 8).to(torch.bfloat16)
+    bt = torch.arange(nb, dtype=torch.int32)[None]
+    cl = torch.tensor([L], dtype=torch.int32)
+    for splits in (1, 4):
+        out = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), 1 / math.sqrt(d), splits)
+        exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, cl, 1 / math.sqrt(d))
+        close(out, exp.to(DEV), 0.03, 0.02)
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 128), (16, 1, 128)])
+def test_prefill_varlen(hq, hkv, d):
+    # (start_pos, new tokens): prefix already cached + delta chunk
+    specs = [(0, 1), (0, 45), (100, 70), (31, 33), (500, 17)]
+    S = len(specs)
+    nb_each = [(sp + n + 31) // 32 for sp, n in specs]
+    nb = sum(nb_each) + 2
+    kc, vc = make_cache(nb, hkv, d, seed=21)
+    perm = torch.randperm(nb).tolist()
+    maxb = max(nb_each)
+    bt = torch.zeros(S, maxb, dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(nb_each):
+        bt[s, :n] = torch.tensor(perm[i:i + n], dtype=torch.int32)
+        i += n
+    cu = [0]
+    for _, n in specs:
+        cu.append(cu[-1] + n)
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    st = torch.tensor([sp for sp, _ in specs], dtype=torch.int32)
+    q = bf(cu[-1], hq, d, seed=22)
+    scale = 1 / math.sqrt(d)
+    out = ops.prefill_attention(q, kc, vc, bt.to(DEV), cu_t.to(DEV), st.to(DEV), scale)
+    exp = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt, cu_t, st, scale)
+    close(out, exp.to(DEV), 0.02, 0.02)
+
+
+def test_sample_greedy_and_topk1():
+    B, V = 5, 128256
+    logits = bf(B, V, scale=3.0, seed=31)
+    z = torch.zeros(B, device=DEV)
+    one = torch.ones(B, device=DEV)
+    k0 = torch.zeros(B, dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV)
+    offs = torch.arange(B, dtype=torch.int64, device=DEV) + 7
+    am = logits.float().argmax(-1)
+    assert torch.equal(ops.sample(logits, z, one, k0, seeds, offs), am)
+    k1 = torch.ones(B, dtype=torch.int32, device=DEV)
+    assert torch.equal(ops.sample(logits, one * 0.8, one, k1, seeds, offs), am)
+
+
+def test_sample_matches_reference():
+    B, V = 8, 32000
+    logits = bf(B, V, scale=2.0, seed=41).float()
+    temp = torch.full((B,), 0.7, device=DEV)
+    top_p = torch.tensor([1.0, 0.9, 0.5, 0.95, 1.0, 0.8, 0.99, 0.3], device=DEV)
+    top_k = torch.tensor([0, 0, 0, 50, 10, 0, 1000, 0], dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 1000 + 1
+    offs = torch.arange(B, dtype=torch.int64, device=DEV) + 123
+    got = ops.sample(logits, temp, top_p, top_k, seeds, offs).cpu()
+    exp = ref.sample(logits.cpu(), temp.cpu(), top_p.cpu(), top_k.cpu(), seeds.cpu(), offs.cpu())
+    assert (got == exp).sum() >= B - 1, (got, exp)
+    # determinism
+    again = ops.sample(logits, temp, top_p, top_k, seeds, offs).cpu()
+    assert torch.equal(got, again)
+
+
+def test_sample_top_p_nucleus():
+    V = 1000
+    logits = torch.full((1, V), -10.0, device=DEV)
+    logits[0, :3] = torch.tensor([5.0, 4.9, 4.8], device=DEV)
+    hits = set()
+    for s in range(64):
+        tok = ops.sample(logits, torch.ones(1, device=DEV), torch.tensor([0.5], device=DEV),
+                         torch.zeros(1, dtype=torch.int32, device=DEV), torch.tensor([s], device=DEV),
+                         torch.tensor([s], device=DEV))
+        hits.add(int(tok))
+    assert hits <= {0, 1} and len(hits) == 2

@@ -1,0 +1,531 @@
+"""``roundtable`` CLI (reference `src/index.ts:48-182` + `src/commands/*.ts`).
+
+Commands: init, discuss, summon, apply, status, list, chronicle, decrees,
+manifest {list,add,deprecate,check}, code-red, bench. ``main`` is the single error
+sink: every command raises, ``main`` formats and returns the exit code (index.ts:25-46).
+Interactive questions read stdin; every one also has a flag so scripts and CI can
+run non-interactively (EOF on stdin = the default answer).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+from typing import List, Optional
+
+from . import __version__, store
+from .config import DEFAULT_CAPABILITIES, generate_config, load_config, write_config
+from .errors import ConfigError, RoundtableError, format_error, get_exit_code
+from .types import ContinueOptions
+from .utils.ui import UI
+
+
+# ---- prompts ------------------------------------------------------------------------------------
+def ask(ui: UI, question: str, default: str = "") -> str:
+    ui.print(question)
+    try:
+        line = sys.stdin.readline()
+    except (EOFError, OSError):
+        return default
+    if not line:
+        return default
+    return line.strip() or default
+
+
+def confirm(ui: UI, question: str, default_yes: bool = True) -> bool:
+    hint = "[Y/n]" if default_yes else "[y/N]"
+    ans = ask(ui, f"{question} {hint}", "y" if default_yes else "n").lower()
+    return ans in ("y", "yes", "ja")
+
+
+# ---- init ---------------------------------------------------------------------------------------
+def gpu_inventory() -> List[dict]:
+    """GPUs without initializing HIP in this process (device_count only; rocm-smi for HBM)."""
+    try:
+        import torch
+        n = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        n = 0
+    return [{"index": i} for i in range(n)]
+
+
+def cmd_init(args, ui: UI) -> int:
+    root = os.getcwd()
+    rt = os.path.join(root, ".roundtable")
+    if os.path.exists(rt) and not args.yes:
+        ui.warn("\n  The roundtable already exists in this project.")
+        if not confirm(ui, "  Reinitialize? This will overwrite your config.", False):
+            ui.dim("  Wise choice. The table stands.")
+            return 0
+    ui.print("\n  Welcome to TheRoundtAIble (MI355X engine)\n", "bold")
+    ui.dim(f"  Version: v{__version__}")
+    project = args.project or (os.path.basename(root) if args.yes else ask(ui, f"  Project name? ({os.path.basename(root)})", os.path.basename(root)))
+    language = args.language or ("nl" if args.yes else ask(ui, "  Discussion language? (nl)", "nl"))
+    gpus = gpu_inventory()
+    ui.ok(f"  Scouting complete: {len(gpus)} GPU(s) visible" + ("" if gpus else " — knights will run on CPU"))
+    seats = [("Claude", "claude-cli"), ("Gemini", "gemini-cli"), ("GPT", "openai-cli")][:max(1, min(3, args.knights))]
+    extra = max(0, args.knights - 3)
+    knights = []
+    adapter_engine = {}
+    for i, (name, adapter) in enumerate(seats):
+        if args.yes or confirm(ui, f"  Seat {name} at the table?", True):
+            knights.append({"name": name, "adapter": adapter})
+    for j in range(extra):
+        knights.append({"name": f"Knight{j + 4}", "adapter": f"local-llm-knight{j + 4}",
+                        "capabilities": ["code", "logic"]})
+    if not knights:
+        ui.error("\n  A roundtable with no knights is just a table.")
+        return 0
+    for i, k in enumerate(knights):
+        eng = {"model": args.model, "tp": args.tp}
+        if gpus:
+            g0 = (i * args.tp) % len(gpus)
+            eng["gpus"] = [(g0 + t) % len(gpus) for t in range(args.tp)]
+        else:
+            eng["device"] = "cpu"
+        adapter_engine[k["adapter"]] = eng
+    cfg = generate_config(project, language, knights,
+                          engine={"default_model": args.model, "weights": args.weights, "dtype": "bf16",
+                                  "max_new_tokens": args.max_new_tokens},
+                          adapter_engine=adapter_engine)
+    for k in knights:
+        if k["adapter"].startswith("local-llm"):
+            cfg["adapter_config"][k["adapter"]].update({"endpoint": "engine://local", "model": args.model,
+                                                        "name": k["name"]})
+    os.makedirs(os.path.join(rt, "sessions"), exist_ok=True)
+    write_config(root, cfg)
+    from .utils.atomic import atomic_write_text
+    from .store.chronicle import INIT_HEADER
+    from .types import dumps_js
+    from .utils.clock import iso_now
+    atomic_write_text(os.path.join(rt, "chronicle.md"), INIT_HEADER)
+    atomic_write_text(os.path.join(rt, "manifest.json"),
+                      dumps_js({"version": "1.0", "last_updated": iso_now(), "features": []}))
+    ui.ok("\n  TheRoundtAIble is ready.\n")
+    ui.print(f"    Project:   {project}")
+    ui.print(f"    Language:  {language}")
+    ui.print(f"    Knights:   {', '.join(k['name'] for k in knights)} ({args.model}, tp={args.tp})")
+    ui.dim('\n  The table is set. Run `roundtable discuss "your question"` to begin.\n')
+    return 0
+
+
+# ---- discuss / summon ---------------------------------------------------------------------------
+def _make_backends(config, ui: UI, device: Optional[str] = None):
+    from .knights.registry import BackendFactory, initialize_backends
+    factory = BackendFactory(config, device_override=device)
+    return initialize_backends(config, ui, factory), factory
+
+
+def last_proposals(all_rounds):
+    """(discuss.ts:229-260) last entry per knight with a one-line summary."""
+    import re
+    last = {}
+    for e in all_rounds:
+        last[e.knight] = e
+    out = []
+    for e in last.values():
+        score = e.consensus.consensus_score if e.consensus else 0
+        cleaned = re.sub(r"```json[\s\S]*?```", "", e.response)
+        cleaned = re.sub(r'\{[^{}]*"consensus_score"[^{}]*\}', "", cleaned).strip()
+        lines = [l for l in cleaned.split("\n") if len(l.strip()) > 10]
+        summary = lines[0].strip() if lines else "No summary available"
+        if len(summary) > 80:
+            summary = summary[:77] + "..."
+        out.append({"knight": e.knight, "score": score, "summary": summary, "full": e.response})
+    return out
+
+
+def discuss(topic: str, args, ui: UI) -> int:
+    from .orchestrator import Orchestrator, RunOptions
+    root = os.getcwd()
+    config = load_config(root)
+    ui.print(f'\n  Topic: "{topic}"\n', "bold")
+    ui.dim("  Summoning the knights to the table...\n")
+    backends, factory = _make_backends(config, ui, getattr(args, "device", None))
+    if not backends:
+        raise ConfigError("A roundtable with no knights is just a table.",
+                          hint="Configure at least one knight adapter with an engine model.")
+    names = [next((k.name for k in config.knights if k.adapter == a), a) for a in backends]
+    ui.dim(f"  {', '.join(names)} {'takes' if len(names) == 1 else 'take'} their seat{'' if len(names) == 1 else 's'}.\n")
+    if args.read_codebase is None:
+        ans = ask(ui, "  Shall the knights read the codebase first? Read codebase? [Y/N]", "n").lower()
+        read_src = ans in ("y", "yes")
+    else:
+        read_src = args.read_codebase
+    opts = RunOptions(read_source=read_src, shuffle_seed=args.seed, round_mode=args.round_mode,
+                      prompt_layout=args.layout, max_new_tokens=args.max_new_tokens)
+    orch = Orchestrator(config, backends, root, ui, opts, backend_factory=factory)
+    cont = None
+    if args.resume:
+        cont = _resume_state(root, args.resume)
+    result = orch.run(topic, cont)
+    while True:
+        ui.print("\n" + "=" * 50, "bold")
+        if result.consensus:
+            if result.unanimous_rejection:
+                ui.print("  The knights unanimously reject this proposal.", "bold", "red")
+                ui.dim(f"  Rounds: {result.rounds}\n  Session: {result.session_path}")
+            else:
+                ui.print("  A miracle has occurred. The knights actually agree.", "bold", "green")
+                ui.dim(f"  Rounds: {result.rounds}\n  Session: {result.session_path}")
+                ui.dim(f"  Read the decision: {result.session_path}/decisions.md\n")
+                _kings_decree(root, topic, result, args, ui)
+            break
+        action = _no_consensus(root, topic, result, args, ui)
+        if action != "send_back":
+            break
+        ui.print("=" * 50, "bold")
+        cont = ContinueOptions(result.session_path, result.all_rounds, result.rounds + 1,
+                               result.resolved_files, result.resolved_commands)
+        args.choice = None  # a scripted choice applies once
+        result = orch.run(topic, cont)
+    ui.print("=" * 50 + "\n", "bold")
+    return 0
+
+
+def _resume_state(root: str, session: str) -> ContinueOptions:
+    """``--resume <session>``: continue a crashed/escalated discussion from rounds.jsonl."""
+    from .errors import SessionError
+    path = session if os.path.isabs(session) else os.path.join(root, ".roundtable", "sessions", session)
+    if session == "latest":
+        info = store.find_latest_session(root)
+        if info is None:
+            raise SessionError("No session to resume.")
+        path = info.path
+    entries = store.load_round_entries(path)
+    if not os.path.isdir(path):
+        raise SessionError(f"Session not found: {session}")
+    last = max((e.round for e in entries), default=0)
+    return ContinueOptions(path, entries, last + 1)
+
+
+def _kings_decree(root, topic, result, args, ui: UI) -> None:
+    """Decree after consensus (decree.ts:11-23 + TODO.md:95-100): self / later / reject."""
+    choice = args.decree
+    if choice is None:
+        return
+    name = os.path.basename(result.session_path)
+    if choice == "later":
+        e = store.add_decree_entry(root, "deferred", name, topic, args.decree_reason)
+        ui.dim(f"  Decree {e['id']}: deferred.")
+    elif choice == "reject":
+        e = store.add_decree_entry(root, "rejected_no_apply", name, topic, args.decree_reason)
+        ui.dim(f"  Decree {e['id']}: rejected, no apply.")
+
+
+def _no_consensus(root, topic, result, args, ui: UI) -> str:
+    ui.print("  The knights have agreed to disagree. As usual.", "bold", "yellow")
+    ui.dim(f"  Rounds: {result.rounds}\n  Session: {result.session_path}")
+    props = last_proposals(result.all_rounds)
+    if not props:
+        ui.dim("\n  No proposals to choose from. The knights were useless today.")
+        return "done"
+    ui.print("\n  But YOU are the King. The final word is yours.\n", "bold")
+    for i, p in enumerate(props, start=1):
+        ui.print(f"  {i}. {p['knight']} ({p['score']}/10) — {p['summary']}")
+    ui.print(f"  {len(props) + 1}. Send them back — they must reach unanimity!")
+    raw = str(args.choice) if args.choice is not None else ask(ui, f"  What say you, Your Majesty? [1-{len(props) + 1}]", "")
+    try:
+        choice = int(raw)
+    except ValueError:
+        choice = -1
+    if choice < 1 or choice > len(props) + 1:
+        ui.dim("  The King waves dismissively. Perhaps another time.")
+        return "done"
+    if choice == len(props) + 1:
+        return "send_back"
+    chosen = props[choice - 1]
+    ui.print(f"\n  The King has chosen {chosen['knight']}'s advice. So it shall be.", "bold")
+    store.write_decisions(result.session_path, topic, chosen["full"], result.all_rounds)
+    store.update_status(result.session_path, phase="consensus_reached", consensus_reached=True,
+                        lead_knight=chosen["knight"])
+    ui.dim(f"  Read the decision: {result.session_path}/decisions.md\n")
+    return "done"
+
+
+def cmd_discuss(args, ui: UI) -> int:
+    return discuss(args.topic, args, ui)
+
+
+def cmd_summon(args, ui: UI) -> int:
+    from .gitutil import git_branch, git_diff, recent_commits
+    root = os.getcwd()
+    load_config(root)
+    ui.dim("\n  Reading the git scrolls...\n")
+    diff, branch, commits = git_diff(root), git_branch(root), recent_commits(3, root)
+    if not diff:
+        ui.warn("  Nothing to review. The code rests in peace.")
+        ui.dim("  Make some changes first, then summon again.\n")
+        return 0
+    import re
+    n_files = len(re.findall(r"^diff --git", diff, re.M))
+    ui.dim(f"  Branch: {branch or 'unknown'}\n  Changed files: {n_files}")
+    preview = diff[:500].replace("\n", " ").strip()
+    topic = (f'Review de huidige wijzigingen op branch "{branch or "unknown"}". {n_files} bestand(en) gewijzigd. '
+             f"Diff preview: {preview}")
+    ui.print("\n  The knights shall review your changes...\n", "bold")
+    return discuss(topic, args, ui)
+
+
+# ---- read-only views ----------------------------------------------------------------------------
+PHASES = {"discussing": ("⚔️", "debating", "Discussing — swords are drawn"),
+          "consensus_reached": ("✅", "consensus", "Consensus — ready to apply"),
+          "escalated": ("⚠️", "escalated", "Escalated — the knights need your wisdom"),
+          "applying": ("⚙️", "executing", "Applying — the knight is writing..."),
+          "completed": ("✨", "done", "Completed — the deed is done")}
+
+
+def cmd_status(args, ui: UI) -> int:
+    s = store.find_latest_session(os.getcwd())
+    if s is None:
+        ui.warn("\n  The table is empty. No sessions yet.")
+        ui.dim('  Run `roundtable discuss "topic"` to summon the knights.\n')
+        return 0
+    st = s.status or {}
+    phase = st.get("phase", "unknown")
+    ui.print("\n  Latest Session\n", "bold")
+    ui.print(f"  Name:      {s.name}")
+    ui.print(f"  Topic:     {s.topic or '—'}")
+    ui.print(f"  Phase:     {PHASES.get(phase, ('', '', phase))[2]}")
+    ui.print(f"  Round:     {st.get('round') or 0}")
+    ui.print(f"  Consensus: {'Yes — miracles happen' if st.get('consensus_reached') else 'No — still arguing'}")
+    for key, label in (("current_knight", "Knight:   "), ("lead_knight", "Lead:     "),
+                       ("started_at", "Started:  "), ("updated_at", "Updated:  ")):
+        if st.get(key):
+            ui.print(f"  {label} {st[key]}")
+    dp = os.path.join(s.path, "decisions.md")
+    if os.path.exists(dp):
+        with open(dp, encoding="utf-8") as f:
+            content = f.read()
+        ui.print("\n  The verdict:\n", "bold")
+        ui.dim("\n".join(f"  {l}" for l in content.split("\n")[:10]))
+        if len(content.split("\n")) > 10:
+            ui.dim("  ...(the rest is in decisions.md)")
+    ui.dim(f"\n  Path: {s.path}\n")
+    return 0
+
+
+def cmd_list(args, ui: UI) -> int:
+    sessions = store.list_sessions(os.getcwd())
+    if not sessions:
+        ui.warn("\n  No battles fought yet.")
+        ui.dim('  Run `roundtable discuss "topic"` to start one.\n')
+        return 0
+    ui.print(f"\n  The Archives — {len(sessions)} session(s)\n", "bold")
+    for s in sessions:
+        phase = (s.status or {}).get("phase", "unknown")
+        icon, label, _ = PHASES.get(phase, ("?", phase, phase))
+        rnd = (s.status or {}).get("round") or 0
+        topic = s.topic or "—"
+        if len(topic) > 60:
+            topic = topic[:57] + "..."
+        ui.print(f"  {icon} {label:<12} {s.name}")
+        ui.print(f"    {topic} ({rnd} round{'' if rnd == 1 else 's'})\n")
+    return 0
+
+
+def cmd_chronicle(args, ui: UI) -> int:
+    import re
+    root = os.getcwd()
+    path = ".roundtable/chronicle.md"
+    try:
+        path = load_config(root).chronicle
+    except ConfigError as e:
+        if "No .roundtable/config.json found" not in e.message:
+            raise
+    content = store.read_chronicle(root, path)
+    if not content.strip():
+        ui.warn("\n  The chronicle is blank. No decisions recorded yet.")
+        ui.dim("  Win some debates first, then come back.\n")
+        return 0
+    n = len(re.findall(r"^## \d{4}", content, re.M))
+    ui.print(f"\n  The Chronicle — {n} decision(s) etched in stone\n", "bold")
+    ui.dim("  " + "=" * 56)
+    for line in content.split("\n"):
+        if line.startswith("# "):
+            ui.print(f"  {line}", "bold", "cyan")
+        elif line.startswith("## "):
+            ui.print(f"\n  {line}", "bold")
+        elif line.startswith("---"):
+            ui.dim("  " + "~" * 40)
+        else:
+            ui.print(f"  {line}")
+    return 0
+
+
+def cmd_decrees(args, ui: UI) -> int:
+    log = store.read_decree_log(os.getcwd())
+    if not log["entries"]:
+        ui.dim("\n  No decrees yet. The King has spoken on nothing.\n")
+        return 0
+    ui.print("\n  King's Decree Log\n", "bold")
+    for e in log["entries"]:
+        rev = " [REVOKED]" if e.get("revoked") else ""
+        ui.print(f"  {e['id']} {e['type'].upper()}{rev}")
+        ui.dim(f"    Topic:   {e['topic']}\n    Reason:  {e['reason']}\n    Session: {e['session']}\n"
+               f"    Date:    {e['date'][:10]}\n")
+    active = sum(1 for e in log["entries"] if not e.get("revoked"))
+    ui.dim(f"  Total: {len(log['entries'])} ({active} active, {len(log['entries']) - active} revoked)\n")
+    return 0
+
+
+def cmd_manifest(args, ui: UI) -> int:
+    root = os.getcwd()
+    if args.mcmd == "list":
+        m = store.read_manifest(root)
+        if not m["features"]:
+            ui.dim("\n  The manifest is empty. No features tracked yet.")
+            ui.dim("  Features are added automatically after `roundtable apply`.\n")
+            return 0
+        ui.print(f"\n  Implementation Manifest ({len(m['features'])} features)\n", "bold")
+        from .store.manifest import status_icon
+        for f in m["features"]:
+            ui.print(f"  [{status_icon(f['status'])}] {f['id']} — {f.get('summary', '')}")
+            ui.dim(f"      Status: {f['status']} | Knight: {f.get('lead_knight')} | {str(f.get('applied_at', ''))[:10]}")
+            ui.dim(f"      Files: {', '.join(f.get('files', []))}")
+            if f.get("files_skipped"):
+                ui.warn(f"      Skipped: {', '.join(f['files_skipped'])}")
+            if f.get("replaced_by"):
+                ui.dim(f"      Replaced by: {f['replaced_by']}")
+            ui.print("")
+    elif args.mcmd == "add":
+        if not args.feature_id or not args.files:
+            ui.error("\n  Usage: roundtable manifest add <feature-id> --files file1.ts file2.ts\n")
+            return 0
+        summary = args.summary if args.summary is not None else ask(ui, "  Summary: ", "")
+        from .utils.clock import iso_now
+        store.add_manifest_entry(root, {"id": args.feature_id, "session": "manual", "status": "implemented",
+                                        "files": args.files, "summary": summary.strip() or args.feature_id,
+                                        "applied_at": iso_now(), "lead_knight": "manual"})
+        ui.ok(f'\n  Added "{args.feature_id}" to manifest with {len(args.files)} file(s).\n')
+    elif args.mcmd == "deprecate":
+        if store.deprecate_feature(root, args.feature_id, args.replaced_by):
+            ui.warn(f'\n  Deprecated "{args.feature_id}".')
+            if args.replaced_by:
+                ui.dim(f"  Replaced by: {args.replaced_by}")
+        else:
+            ui.error(f'\n  Feature "{args.feature_id}" not found in manifest.\n')
+    elif args.mcmd == "check":
+        w = store.check_manifest(root)
+        if not w:
+            ui.ok("\n  Manifest is consistent. All tracked files exist on disk.\n")
+        else:
+            ui.warn(f"\n  {len(w)} warning(s) found:\n")
+            for x in w:
+                ui.warn(f"    {x}")
+    return 0
+
+
+def cmd_apply(args, ui: UI) -> int:
+    from .apply.apply import apply_command
+    return apply_command(args, ui)
+
+
+def cmd_code_red(args, ui: UI) -> int:
+    from .codered import code_red_command
+    return code_red_command(args, ui)
+
+
+def cmd_bench(args, ui: UI) -> int:
+    import subprocess
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(here, "bench.py")] + args.bench_args
+    return subprocess.call(cmd)
+
+
+# ---- parser -------------------------------------------------------------------------------------
+def _discuss_flags(p):
+    g = p.add_mutually_exclusive_group()
+    g.add_argument("--read-codebase", dest="read_codebase", action="store_true", default=None)
+    g.add_argument("--no-read-codebase", dest="read_codebase", action="store_false")
+    p.add_argument("--round-mode", choices=["sequential", "parallel"])
+    p.add_argument("--layout", choices=["reference", "append"])
+    p.add_argument("--max-new-tokens", type=int)
+    p.add_argument("--seed", type=int, help="seed the speaking-order shuffle (default: unseeded)")
+    p.add_argument("--choice", type=int, help="non-interactive King's choice when no consensus")
+    p.add_argument("--decree", choices=["self", "later", "reject"], help="King's decree after consensus")
+    p.add_argument("--decree-reason", default=None)
+    p.add_argument("--resume", help="continue a session from its rounds.jsonl ('latest' or a session name)")
+    p.add_argument("--device", help="force every knight onto this device (e.g. cpu, cuda:0)")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="roundtable", description="TheRoundtAIble — Where no AI is King, but all serve the Code. (MI355X engine)")
+    p.add_argument("--version", action="version", version=__version__)
+    p.add_argument("--quiet", action="store_true")
+    sub = p.add_subparsers(dest="cmd", required=True)
+    i = sub.add_parser("init", help="Initialize TheRoundtAIble in the current project")
+    i.add_argument("--yes", "-y", action="store_true", help="accept defaults non-interactively")
+    i.add_argument("--project")
+    i.add_argument("--language")
+    i.add_argument("--model", default="llama3-8b")
+    i.add_argument("--weights", default="random:0")
+    i.add_argument("--knights", type=int, default=3)
+    i.add_argument("--tp", type=int, default=1)
+    i.add_argument("--max-new-tokens", type=int, default=512)
+    i.set_defaults(fn=cmd_init)
+    d = sub.add_parser("discuss", help="Start a discussion between knights")
+    d.add_argument("topic")
+    _discuss_flags(d)
+    d.set_defaults(fn=cmd_discuss)
+    s = sub.add_parser("summon", help="Start a discussion based on current git diff")
+    _discuss_flags(s)
+    s.set_defaults(fn=cmd_summon)
+    a = sub.add_parser("apply", help="Execute the consensus decision (lead knight writes code)")
+    a.add_argument("--noparley", action="store_true", help="write without file-by-file review")
+    a.add_argument("--dry-run", action="store_true", help="run the full pipeline without writing files")
+    a.add_argument("--override-scope", action="store_true", help="bypass scope enforcement (requires a reason)")
+    a.add_argument("--reason", help="override-scope reason (non-interactive)")
+    a.add_argument("--yes", action="store_true", help="accept every parley prompt")
+    a.add_argument("--session", help="session name (default: latest)")
+    a.add_argument("--max-new-tokens", type=int)
+    a.add_argument("--device")
+    a.add_argument("--response-file", help="use this file as the lead knight's edit output (testing)")
+    a.set_defaults(fn=cmd_apply)
+    for name, fn, h in (("status", cmd_status, "Show the status of the latest discussion"),
+                        ("list", cmd_list, "List all discussion sessions"),
+                        ("chronicle", cmd_chronicle, "View the decision log"),
+                        ("decrees", cmd_decrees, "View the King's Decree Log")):
+        sub.add_parser(name, help=h).set_defaults(fn=fn)
+    cr = sub.add_parser("code-red", help="Emergency diagnostic mode (triage, blind round, convergence)")
+    cr.add_argument("symptoms")
+    _discuss_flags(cr)
+    cr.set_defaults(fn=cmd_code_red)
+    m = sub.add_parser("manifest", help="Manage the implementation manifest")
+    msub = m.add_subparsers(dest="mcmd", required=True)
+    msub.add_parser("list")
+    ma = msub.add_parser("add")
+    ma.add_argument("feature_id")
+    ma.add_argument("--files", nargs="+", default=[])
+    ma.add_argument("--summary")
+    md = msub.add_parser("deprecate")
+    md.add_argument("feature_id")
+    md.add_argument("--replaced-by")
+    msub.add_parser("check")
+    m.set_defaults(fn=cmd_manifest)
+    b = sub.add_parser("bench", help="Run the roundtable benchmark (wraps bench.py)")
+    b.add_argument("bench_args", nargs=argparse.REMAINDER)
+    b.set_defaults(fn=cmd_bench)
+    return p
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = build_parser().parse_args(argv)
+    ui = UI(quiet=args.quiet)
+    try:
+        return int(args.fn(args, ui) or 0)
+    except RoundtableError as e:
+        print(format_error(e), file=sys.stderr)
+        return int(e.exit_code)
+    except KeyboardInterrupt:
+        return 130
+    except Exception as e:  # noqa: BLE001 - the single error sink
+        print(f"\n  Unexpected error: {e}", file=sys.stderr)
+        if os.environ.get("DEBUG"):
+            import traceback
+            traceback.print_exc()
+        return get_exit_code(e)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,424 @@
+"""The per-GPU(-group) inference engine that hosts one or more knights.
+
+A knight turn on the engine:
+
+1. tokenize the prompt segment-by-segment (stable prefixes; response segments keep ids);
+2. longest-common-prefix match against the knight's *resident* KV sequence, roll the
+   sequence back to the LCP (paged: drop tail blocks) and prefill only the delta —
+   chunked, varlen-batched across all knights of this call (K4 prefill attention);
+3. pre-allocate KV blocks for ``max_new_tokens`` and run the decode loop fully
+   device-side: one hipGraph replay per token for the whole batch (embed -> 32 layers
+   with K1/K2/K3/K5 -> lm_head -> K6 sampling -> next-input/slot/position update);
+   the host only replays and, every ``sync_every`` steps, reads back tokens for
+   EOS / consensus-JSON / wall-clock checks;
+4. detokenize; the generated ids are returned too (C1 token-id path), and the KV of
+   the response stays resident for the knight's next turn.
+
+The same class runs on CPU (reference ops, no graphs) for the GPT-2 plumbing config.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from ..consensus import parse_consensus
+from ..errors import AdapterError, EngineTimeout
+from ..models.config import ModelConfig, get_config
+from ..models.gpt2 import build_model
+from ..models.llama import AttnMeta
+from ..models.weights import materialize
+from ..parallel.tp import TPInfo
+from ..prompt import Prompt, PromptLike, Segment
+from ..utils import trace
+from .kv_cache import KVCacheOOM, PagedKVCache, SeqState
+from .sampler import SamplingParams
+from .tokenizer import EngineTokenizer, get_tokenizer
+
+BATCH_BUCKETS = (1, 2, 4, 8, 16, 32)
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    weights: str = "random:0"
+    dtype: str = "bf16"
+    device: str = "cuda:0"
+    block_size: int = 32
+    num_blocks: Optional[int] = None        # None = size from free memory
+    kv_cache_fraction: float = 0.85
+    max_kv_tokens: Optional[int] = None     # optional cap on resident tokens
+    prefill_chunk: int = 8192               # tokens per prefill forward (summed over sequences)
+    use_graphs: bool = True
+    sync_every: int = 32                    # decode steps between host token readbacks
+    max_batch: int = 16
+    model_overrides: Dict[str, object] = field(default_factory=dict)
+
+
+@dataclass
+class Turn:
+    seq_key: str
+    prompt: PromptLike
+    params: SamplingParams
+    timeout_s: float = 1e9
+
+
+@dataclass
+class TurnOutput:
+    text: str
+    ids: List[int]
+    metrics: Dict[str, float]
+    error: Optional[BaseException] = None
+
+
+def _dtype(s: str) -> torch.dtype:
+    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16,
+            "float16": torch.float16, "fp32": torch.float32, "float32": torch.float32}[s]
+
+
+class Engine:
+    def __init__(self, ecfg: EngineConfig, tp: Optional[TPInfo] = None):
+        self.ecfg = ecfg
+        self.tp = tp or TPInfo()
+        self.cfg: ModelConfig = get_config(ecfg.model, **ecfg.model_overrides)
+        self.device = torch.device(ecfg.device)
+        self.on_gpu = self.device.type == "cuda"
+        self.dtype = _dtype(ecfg.dtype)
+        if not self.on_gpu and self.dtype == torch.float16:
+            self.dtype = torch.float32
+        self.tokenizer: EngineTokenizer = get_tokenizer(self.cfg.vocab)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            weights = materialize(self.cfg, ecfg.weights, self.device, self.dtype, self.tp)
+            self.model = build_model(self.cfg, weights, self.device, self.dtype, self.tp)
+        self.load_s = time.perf_counter() - t0
+        self.kv = self._alloc_kv()
+        self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}
+        self._seg_cache: Dict[Tuple[str, str], List[int]] = {}
+        self.healthy = True
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0}
+
+    # ---- memory ----------------------------------------------------------------------------
+    def _alloc_kv(self) -> PagedKVCache:
+        m = self.model
+        bs = self.ecfg.block_size
+        per_block = PagedKVCache.bytes_per_block(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, bs,
+                                                 torch.finfo(self.dtype).bits // 8)
+        nb = self.ecfg.num_blocks
+        if nb is None:
+            if self.on_gpu:
+                free, _total = torch.cuda.mem_get_info(self.device)
+                budget = int(free * self.ecfg.kv_cache_fraction) - (2 << 30)  # leave 2 GiB for activations
+                nb = max(64, budget // per_block)
+            else:
+                nb = 2048
+        if self.ecfg.max_kv_tokens:
+            nb = min(nb, (self.ecfg.max_kv_tokens + bs - 1) // bs + self.ecfg.max_batch)
+        return PagedKVCache(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, int(nb), bs,
+                            self.device, self.dtype)
+
+    @property
+    def kv_capacity_tokens(self) -> int:
+        return self.kv.num_blocks * self.kv.block_size
+
+    def max_source_chars(self) -> int:
+        """Source budget in chars: positional limit minus response/overhead reserve (local-llm.ts:58-70)."""
+        ctx = min(self.cfg.max_pos, self.kv_capacity_tokens)
+        avail = max(ctx - 4096 - 3000, 2000)
+        return int(avail * 4)
+
+    # ---- tokenization ------------------------------------------------------------------------
+    def encode_prompt(self, prompt: PromptLike) -> List[int]:
+        segs = [Segment(prompt)] if isinstance(prompt, str) else prompt.segments
+        out: List[int] = []
+        fam = self.tokenizer.family
+        for s in segs:
+            if s.ids is not None and s.tokenizer == fam:
+                out.extend(int(i) for i in s.ids)
+                continue
+            key = (fam, s.text)
+            ids = self._seg_cache.get(key)
+            if ids is None:
+                ids = self.tokenizer.encode(s.text)
+                if len(self._seg_cache) > 4096:
+                    self._seg_cache.clear()
+                self._seg_cache[key] = ids
+            out.extend(ids)
+        if not out:
+            out = [self.tokenizer.bos_id]
+        return out
+
+    # ---- prefix reuse ------------------------------------------------------------------------
+    def sync_prefix(self, key: str, target: List[int]) -> Tuple[SeqState, int]:
+        """Roll the resident sequence back to its LCP with ``target``; return (seq, reused tokens)."""
+        s = self.kv.seq(key)
+        n = 0
+        lim = min(len(s.tokens), len(target) - 1)   # always recompute >= 1 token (need its logits)
+        toks = s.tokens
+        while n < lim and toks[n] == target[n]:
+            n += 1
+        self.kv.truncate(s, n)
+        return s, n
+
+    def release(self, key: str) -> None:
+        self.kv.free_seq(key)
+
+    def fork(self, src: str, dst: str) -> None:
+        self.kv.fork(src, dst)
+
+    # ---- forward helpers -----------------------------------------------------------------------
+    def _max_blocks(self) -> int:
+        return (self.cfg.max_pos + self.kv.block_size - 1) // self.kv.block_size
+
+    @torch.no_grad()
+    def prefill(self, items: Sequence[Tuple[SeqState, List[int]]]) -> torch.Tensor:
+        """Append ``ids`` to each sequence's KV (chunked, varlen-batched). Returns last-token logits [S, V]."""
+        dev = self.device
+        pending = [(s, list(ids)) for s, ids in items]
+        last_logits: List[Optional[torch.Tensor]] = [None] * len(pending)
+        offs = [0] * len(pending)
+        budget = self.ecfg.prefill_chunk
+        while True:
+            batch = []
+            used = 0
+            for i, (s, ids) in enumerate(pending):
+                rem = len(ids) - offs[i]
+                if rem <= 0:
+                    continue
+                take = min(rem, max(1, budget - used))
+                if used and used + take > budget:
+                    break
+                batch.append((i, take))
+                used += take
+                if used >= budget:
+                    break
+            if not batch:
+                break
+            seqs = []
+            tok, pos, slots, cu, starts, last = [], [], [], [0], [], []
+            for i, take in batch:
+                s, ids = pending[i]
+                st = s.length
+                chunk = ids[offs[i]:offs[i] + take]
+                self.kv.ensure_capacity(s, st + take)
+                tok += chunk
+                pos += list(range(st, st + take))
+                slots += self.kv.slots(s, st, st + take)
+                s.tokens.extend(chunk)
+                starts.append(st)
+                cu.append(cu[-1] + take)
+                last.append(cu[-1] - 1)
+                offs[i] += take
+                seqs.append(s)
+            maxb = max(len(s.blocks) for s in seqs)
+            bt = torch.zeros(len(seqs), maxb, dtype=torch.int32)
+            for j, s in enumerate(seqs):
+                bt[j, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+            cu_t = torch.tensor(cu, dtype=torch.int32)
+            meta = AttnMeta(kind="prefill",
+                            slot_mapping=torch.tensor(slots, dtype=torch.int64).to(dev, non_blocking=True),
+                            block_tables=bt.to(dev, non_blocking=True),
+                            cu_q=cu_t.to(dev, non_blocking=True),
+                            start_pos=torch.tensor(starts, dtype=torch.int32).to(dev, non_blocking=True),
+                            last_rows=torch.tensor(last, dtype=torch.int64).to(dev, non_blocking=True))
+            if self.on_gpu:
+                rows = ops.native().prefill_rows_per_tile(self.model.n_heads // self.model.n_kv_heads)
+                meta.tile_map = ops.prefill_tile_map(cu_t, rows).to(dev, non_blocking=True)
+            with trace.range("prefill"):
+                logits = self.model.forward(torch.tensor(tok, dtype=torch.int64).to(dev, non_blocking=True),
+                                            torch.tensor(pos, dtype=torch.int64).to(dev, non_blocking=True),
+                                            self.kv, meta)
+            for j, (i, take) in enumerate(batch):
+                if offs[i] >= len(pending[i][1]):
+                    last_logits[i] = logits[j]
+        return torch.stack([l for l in last_logits])  # type: ignore[misc]
+
+    # ---- the turn API ----------------------------------------------------------------------------
+    @torch.no_grad()
+    def run_turns(self, turns: Sequence[Turn]) -> List[TurnOutput]:
+        """Run one turn for each entry (distinct seq_keys), batched; per-turn errors are returned."""
+        if not turns:
+            return []
+        if not self.healthy:
+            err = AdapterError("engine", "engine unhealthy after a previous device error", kind="device")
+            return [TurnOutput("", [], {}, err) for _ in turns]
+        try:
+            return self._run_turns(turns)
+        except KVCacheOOM as e:
+            for t in turns:  # drop partial state; the knight re-prefills next time
+                self.release(t.seq_key)
+            return [TurnOutput("", [], {}, AdapterError("engine", f"out of memory: {e}", kind="oom")) for _ in turns]
+        except EngineTimeout as e:
+            return [TurnOutput("", [], {}, e) for _ in turns]
+        except RuntimeError as e:
+            msg = str(e)
+            if "HIP" in msg or "hip" in msg or "CUDA" in msg or "device" in msg:
+                self.healthy = False
+                return [TurnOutput("", [], {}, AdapterError("engine", f"HIP error: {msg}", kind="device"))
+                        for _ in turns]
+            raise
+
+    def _run_turns(self, turns: Sequence[Turn]) -> List[TurnOutput]:
+        t_start = time.perf_counter()
+        targets = [self.encode_prompt(t.prompt) for t in turns]
+        seqs, reused = [], []
+        for t, ids in zip(turns, targets):
+            s, n = self.sync_prefix(t.seq_key, ids)
+            seqs.append(s)
+            reused.append(n)
+        deltas = [ids[n:] for ids, n in zip(targets, reused)]
+        self._sync()
+        t0 = time.perf_counter()
+        logits = self.prefill(list(zip(seqs, deltas)))
+        first = self._sample_host(logits, seqs, turns)
+        self._sync()
+        t1 = time.perf_counter()
+        gen, decode_steps = self.decode(seqs, turns, first, deadline=t_start + min(t.timeout_s for t in turns))
+        self._sync()
+        t2 = time.perf_counter()
+        outs = []
+        for t, s, g, n, d in zip(turns, seqs, gen, reused, deltas):
+            text = self.tokenizer.decode(g)
+            outs.append(TurnOutput(text, g, {
+                "prompt_tokens": len(d) + n, "prefill_tokens": len(d), "reused_tokens": n,
+                "decode_tokens": len(g), "prefill_ms": (t1 - t0) * 1e3, "decode_ms": (t2 - t1) * 1e3,
+                "decode_tok_s": len(g) / max(t2 - t1, 1e-9), "batch": len(turns),
+                "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3}))
+        self.stats["prefill_tokens"] += sum(len(d) for d in deltas)
+        self.stats["decode_tokens"] += sum(len(g) for g in gen)
+        self.stats["prefill_s"] += t1 - t0
+        self.stats["decode_s"] += t2 - t1
+        return outs
+
+    def _sync(self):
+        if self.on_gpu:
+            torch.cuda.synchronize(self.device)
+
+    def _sample_host(self, logits: torch.Tensor, seqs: Sequence[SeqState], turns: Sequence[Turn]) -> torch.Tensor:
+        B = logits.shape[0]
+        dev = logits.device
+        temp = torch.tensor([t.params.temperature for t in turns], dtype=torch.float32, device=dev)
+        top_p = torch.tensor([t.params.top_p for t in turns], dtype=torch.float32, device=dev)
+        top_k = torch.tensor([t.params.top_k for t in turns], dtype=torch.int32, device=dev)
+        seeds = torch.tensor([t.params.seq_seed(t.seq_key) for t in turns], dtype=torch.int64, device=dev)
+        offs = torch.tensor([s.length for s in seqs], dtype=torch.int64, device=dev)
+        return ops.sample(logits.contiguous(), temp, top_p, top_k, seeds, offs)
+
+    # ---- decode -------------------------------------------------------------------------------------
+    def decode(self, seqs: Sequence[SeqState], turns: Sequence[Turn], first: torch.Tensor,
+               deadline: float) -> Tuple[List[List[int]], int]:
+        B = len(seqs)
+        max_new = [max(1, t.params.max_new_tokens) for t in turns]
+        steps = max(max_new)
+        # every sequence: the first sampled token is "generated", then steps-1 decode forwards
+        for s, n in zip(seqs, max_new):
+            self.kv.ensure_capacity(s, s.length + steps)
+        eos = self.tokenizer.eos_id
+        if self.on_gpu and self.ecfg.use_graphs:
+            runner = self._graph_for(B, max(s.length for s in seqs) + steps)
+            toks = runner.run(self, seqs, turns, first, steps, deadline, eos)
+        else:
+            toks = self._decode_eager(seqs, turns, first, steps, deadline, eos)
+        gen: List[List[int]] = []
+        for b, (s, t) in enumerate(zip(seqs, turns)):
+            g = toks[b][:max_new[b]]
+            if not t.params.ignore_eos and eos in g:
+                g = g[:g.index(eos) + 1]
+            if t.params.stop_on_consensus:
+                g = _cut_at_consensus(self.tokenizer, g)
+            gen.append(g)
+            # resident KV = prompt + the tokens actually kept (the last one's K/V is not computed yet)
+            # resident = prompt + kept tokens except the last (its K/V was never computed)
+            s.tokens.extend(g)
+            self.kv.truncate(s, s.length - 1 if g else s.length)
+        return gen, steps
+
+    def _decode_eager(self, seqs, turns, first, steps, deadline, eos) -> List[List[int]]:
+        dev = self.device
+        B = len(seqs)
+        cur = first.clone()
+        out: List[List[int]] = [[int(x)] for x in cur.tolist()]
+        lens = [s.length for s in seqs]
+        temp = torch.tensor([t.params.temperature for t in turns], dtype=torch.float32, device=dev)
+        top_p = torch.tensor([t.params.top_p for t in turns], dtype=torch.float32, device=dev)
+        top_k = torch.tensor([t.params.top_k for t in turns], dtype=torch.int32, device=dev)
+        seeds = torch.tensor([t.params.seq_seed(t.seq_key) for t in turns], dtype=torch.int64, device=dev)
+        done = [False] * B
+        bt = torch.zeros(B, max(len(s.blocks) for s in seqs), dtype=torch.int32)
+        for j, s in enumerate(seqs):
+            bt[j, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+        bt = bt.to(dev)
+        bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
+        splits = ops.decode_splits(bucket, self.model.n_kv_heads) if self.on_gpu else 1
+        ws = ops.DecodeWorkspace(B, self.model.n_heads, self.cfg.head_dim, splits, dev) if self.on_gpu else None
+        for step in range(1, steps):
+            pos = list(lens)
+            slots = [s.blocks[p // self.kv.block_size] * self.kv.block_size + p % self.kv.block_size
+                     for s, p in zip(seqs, pos)]
+            meta = AttnMeta(kind="decode", slot_mapping=torch.tensor(slots, dtype=torch.int64, device=dev),
+                            block_tables=bt, ctx_lens=torch.tensor([p + 1 for p in pos], dtype=torch.int32, device=dev),
+                            num_splits=splits, workspace=ws)
+            logits = self.model.forward(cur.to(dev), torch.tensor(pos, dtype=torch.int64, device=dev), self.kv, meta)
+            offs = torch.tensor([p + 1 for p in pos], dtype=torch.int64, device=dev)
+            cur = ops.sample(logits.contiguous(), temp, top_p, top_k, seeds, offs)
+            for b, x in enumerate(cur.tolist()):
+                out[b].append(int(x))
+            lens = [l + 1 for l in lens]
+            if step % self.ecfg.sync_every == 0:
+                if time.perf_counter() > deadline:
+                    self._unwind(seqs)
+                    raise EngineTimeout("engine", "turn exceeded timeout_per_turn_seconds")
+                done = [d or _finished(o, t.params, eos, self.tokenizer) for d, o, t in zip(done, out, turns)]
+                if all(done):
+                    break
+        return out
+
+    def _unwind(self, seqs):
+        # the knights' tokens were not extended; drop the blocks pre-allocated for generation
+        for s in seqs:
+            self.kv.truncate(s, s.length)
+
+    def _graph_for(self, B: int, max_ctx: int) -> "DecodeGraph":
+        from .graphs import DecodeGraph
+        bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
+        splits = ops.decode_splits(bucket, self.model.n_kv_heads)
+        key = (bucket, splits)
+        g = self.graphs.get(key)
+        if g is None:
+            g = DecodeGraph(self, bucket, splits)
+            self.graphs[key] = g
+        return g
+
+
+def _finished(out: List[int], params: SamplingParams, eos: int, tok: EngineTokenizer) -> bool:
+    if len(out) >= params.max_new_tokens:
+        return True
+    if not params.ignore_eos and eos in out:
+        return True
+    if params.stop_on_consensus and len(out) > 8:
+        return _consensus_closed(tok, out)
+    return False
+
+
+def _consensus_closed(tok: EngineTokenizer, ids: List[int]) -> bool:
+    text = tok.decode(ids)
+    return "consensus_score" in text and parse_consensus(text, "", 0) is not None
+
+
+def _cut_at_consensus(tok: EngineTokenizer, ids: List[int]) -> List[int]:
+    """Truncate right after the first complete consensus block (decode may overshoot by < sync_every)."""
+    text = tok.decode(ids)
+    if "consensus_score" not in text or parse_consensus(text, "", 0) is None:
+        return ids
+    lo, hi = 1, len(ids)
+    while lo < hi:  # smallest prefix that still parses
+        mid = (lo + hi) // 2
+        if parse_consensus(tok.decode(ids[:mid]), "", 0) is not None:
+            hi = mid
+        else:
+            lo = mid + 1
+    return ids[:lo]

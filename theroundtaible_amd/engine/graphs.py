@@ -1,0 +1,129 @@
+"""hipGraph-captured decode step (one replay = one token for every knight in the batch).
+
+The captured region is the whole step: embedding, all layers (K1/K2/K3/K5 + GEMMs
++ TP all-reduces), lm_head, K6 sampling, then device-side bookkeeping so the next
+replay needs no host input: the sampled ids become the next inputs, positions /
+context lengths / the step counter advance, and the next slot mapping is derived
+from the (pre-allocated) block tables. Static buffers are refreshed once per turn.
+
+Graphs are cached per (batch bucket, split-KV count); padded batch rows decode a
+dummy sequence living in a reserved scratch block and are discarded.
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Sequence
+
+import torch
+
+from .. import ops
+from ..errors import EngineTimeout
+from ..models.llama import AttnMeta
+
+MAX_STEPS = 8192
+
+
+class DecodeGraph:
+    def __init__(self, engine, bucket: int, splits: int):
+        self.engine = engine
+        self.B = bucket
+        self.splits = splits
+        dev = engine.device
+        kv = engine.kv
+        self.bs = kv.block_size
+        self.maxb = engine._max_blocks()
+        if not hasattr(engine, "_scratch_block"):
+            engine._scratch_block = kv.alloc.alloc()
+        self.scratch = engine._scratch_block
+        B = bucket
+        self.input_ids = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.positions = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.ctx_lens = torch.ones(B, dtype=torch.int32, device=dev)
+        self.block_tables = torch.full((B, self.maxb), self.scratch, dtype=torch.int32, device=dev)
+        self.temp = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.top_p = torch.ones(B, dtype=torch.float32, device=dev)
+        self.top_k = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.seeds = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.out = torch.zeros(MAX_STEPS, B, dtype=torch.int64, device=dev)
+        self.ws = ops.DecodeWorkspace(B, engine.model.n_heads, engine.cfg.head_dim, max(1, splits), dev)
+        self.graph = None
+        self._capture()
+
+    def _body(self):
+        e = self.engine
+        bs = self.bs
+        blk = self.block_tables.gather(1, (self.positions // bs).unsqueeze(1)).squeeze(1).long()
+        slots = blk * bs + self.positions % bs
+        meta = AttnMeta(kind="decode", slot_mapping=slots, block_tables=self.block_tables, ctx_lens=self.ctx_lens,
+                        num_splits=self.splits, workspace=self.ws)
+        logits = e.model.forward(self.input_ids, self.positions, e.kv, meta)
+        nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, self.positions + 1)
+        self.out.index_copy_(0, self.step, nxt.unsqueeze(0))
+        self.input_ids.copy_(nxt)
+        self.positions.add_(1)
+        self.ctx_lens.add_(1)
+        self.step.add_(1)
+
+    def _reset_dummy(self):
+        self.positions.zero_()
+        self.ctx_lens.fill_(1)
+        self.step.zero_()
+        self.block_tables.fill_(self.scratch)
+
+    def _capture(self):
+        dev = self.engine.device
+        self._reset_dummy()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s), torch.no_grad():
+            for _ in range(2):  # warm up kernels / allocator / hipBLASLt heuristics outside capture
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        self._reset_dummy()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g), torch.no_grad():
+            self._body()
+        self.graph = g
+        self._reset_dummy()
+
+    def run(self, engine, seqs: Sequence, turns: Sequence, first: torch.Tensor, steps: int, deadline: float,
+            eos: int) -> List[List[int]]:
+        from .engine import _finished
+        B = len(seqs)
+        dev = engine.device
+        steps = min(steps, MAX_STEPS)
+        self._reset_dummy()
+        bt = torch.full((self.B, self.maxb), self.scratch, dtype=torch.int32)
+        for j, s in enumerate(seqs):
+            bt[j, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+        self.block_tables.copy_(bt.to(dev, non_blocking=True))
+        lens = torch.tensor([s.length for s in seqs] + [0] * (self.B - B), dtype=torch.int64)
+        self.positions.copy_(lens.to(dev, non_blocking=True))
+        self.ctx_lens.copy_((lens + 1).to(torch.int32).to(dev, non_blocking=True))
+        pad = self.B - B
+        self.input_ids.zero_()
+        self.input_ids[:B].copy_(first[:B])
+        self.temp.copy_(torch.tensor([t.params.temperature for t in turns] + [0.0] * pad, dtype=torch.float32))
+        self.top_p.copy_(torch.tensor([t.params.top_p for t in turns] + [1.0] * pad, dtype=torch.float32))
+        self.top_k.copy_(torch.tensor([t.params.top_k for t in turns] + [0] * pad, dtype=torch.int32))
+        self.seeds.copy_(torch.tensor([t.params.seq_seed(t.seq_key) for t in turns] + [0] * pad, dtype=torch.int64))
+        need_tokens = any((not t.params.ignore_eos) or t.params.stop_on_consensus for t in turns)
+        sync_every = engine.ecfg.sync_every
+        first_host = first[:B].tolist()
+        done_at = steps
+        for i in range(1, steps):
+            self.graph.replay()
+            if i % sync_every == 0:
+                if time.perf_counter() > deadline:
+                    engine._sync()
+                    raise EngineTimeout("engine", "turn exceeded timeout_per_turn_seconds")
+                if need_tokens:
+                    got = self.out[:i, :B].t().tolist()
+                    outs = [[f] + g for f, g in zip(first_host, got)]
+                    if all(_finished(o, t.params, eos, engine.tokenizer) for o, t in zip(outs, turns)):
+                        done_at = i + 1
+                        break
+        n = done_at - 1
+        got = self.out[:n, :B].t().tolist() if n > 0 else [[] for _ in range(B)]
+        return [[f] + g for f, g in zip(first_host, got)]

@@ -1,0 +1,116 @@
+"""SPMD knight pool: every rank runs the same orchestrator; knights run where they are placed.
+
+All ranks execute the identical host program (same config, same broadcast shuffle
+seed), so they build identical prompts and reach identical consensus decisions.
+For each batch of turns the pool
+
+1. runs the knights placed on this rank on the local engine (one batched decode; for a
+   TP knight all ranks of its group run it in lockstep — RCCL all-reduce inside);
+2. exchanges the results (C1, :mod:`theroundtaible_amd.parallel.exchange`): token
+   ids via an RCCL all-gather, metadata via the gloo control group;
+3. returns every knight's result on every rank.
+
+Sequential (reference) round mode calls this with one turn at a time: only the
+speaker's group computes while the others wait in the collective.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+from ..errors import AdapterError
+from ..parallel.cluster import Cluster
+from ..parallel.exchange import exchange_token_ids
+from .base import KnightBackend, TurnRequest, TurnResult
+
+
+class DistributedPool:
+    def __init__(self, cluster: Cluster, placement: Dict[str, List[int]], local: Dict[str, KnightBackend],
+                 tokenizer=None):
+        """``placement``: knight name -> ranks hosting it (first = leader). ``local``: name -> backend here."""
+        self.cluster = cluster
+        self.placement = placement
+        self.local = local
+        self.tokenizer = tokenizer
+        self.exchange_ms: List[float] = []
+        budgets = [b.max_source_chars() for b in local.values()]
+        mine = min([b for b in budgets if b is not None], default=200_000)
+        self._src_budget = int(-cluster.max_scalar(-float(mine))) if cluster.distributed else mine
+
+    def leader(self, name: str) -> int:
+        return self.placement[name][0]
+
+    def execute_round(self, pairs: Sequence[Tuple["RemoteKnight", TurnRequest]],
+                      timeout_s: float) -> List[Union[TurnResult, BaseException]]:
+        rank = self.cluster.rank
+        mine_idx = [i for i, (k, _) in enumerate(pairs) if rank in self.placement[k.knight_name]]
+        local_res: Dict[int, Union[TurnResult, BaseException]] = {}
+        # group local work by underlying backend group (one batched decode per engine)
+        groups: Dict[object, List[int]] = {}
+        for i in mine_idx:
+            b = self.local[pairs[i][0].knight_name]
+            groups.setdefault(b.group_key(), []).append(i)
+        for idxs in groups.values():
+            first = self.local[pairs[idxs[0]][0].knight_name]
+            outs = first.execute_group([(self.local[pairs[i][0].knight_name], pairs[i][1]) for i in idxs], timeout_s)
+            for i, o in zip(idxs, outs):
+                local_res[i] = o
+        # contributions from the knights this rank leads
+        led = [i for i in mine_idx if self.leader(pairs[i][0].knight_name) == rank]
+        t0 = time.perf_counter()
+        meta = {}
+        ids_contrib = []
+        for i in led:
+            o = local_res[i]
+            if isinstance(o, BaseException):
+                meta[i] = ("err", getattr(o, "kind", "unknown"), str(o))
+            else:
+                has_ids = o.ids is not None
+                meta[i] = ("ok", None if has_ids else o.text, o.tokenizer, o.metrics)
+                if has_ids:
+                    ids_contrib.append((i, list(o.ids)))
+        all_meta = self.cluster.all_gather_object(meta)
+        all_ids = exchange_token_ids(self.cluster, ids_contrib, self.cluster.device)
+        self.exchange_ms.append((time.perf_counter() - t0) * 1e3)
+        merged: Dict[int, tuple] = {}
+        for m in all_meta:
+            merged.update(m)
+        results: List[Union[TurnResult, BaseException]] = []
+        for i, (k, _) in enumerate(pairs):
+            m = merged.get(i)
+            if m is None:
+                results.append(AdapterError(k.name, "no rank hosted this knight", kind="device"))
+            elif m[0] == "err":
+                results.append(AdapterError(k.name, m[2], kind=m[1]))
+            else:
+                _, text, tok, metrics = m
+                ids = all_ids.get(i)
+                if text is None:
+                    if i in local_res and not isinstance(local_res[i], BaseException):
+                        text = local_res[i].text   # leader/local copy: exact text
+                    else:
+                        text = self.tokenizer.decode(ids) if self.tokenizer is not None else ""
+                results.append(TurnResult(text, ids, tok, dict(metrics or {})))
+        return results
+
+
+class RemoteKnight(KnightBackend):
+    """Orchestrator-facing backend for one knight of a :class:`DistributedPool`."""
+
+    def __init__(self, pool: DistributedPool, knight_name: str, name: str, adapter_id: str):
+        self.pool = pool
+        self.knight_name = knight_name
+        self.name = name
+        self.adapter_id = adapter_id
+
+    def group_key(self):
+        return id(self.pool)
+
+    def max_source_chars(self) -> Optional[int]:
+        return self.pool._src_budget
+
+    def execute_group(self, pairs, timeout_s):
+        return self.pool.execute_round(pairs, timeout_s)
+
+    def execute_many(self, reqs, timeout_s):
+        return self.pool.execute_round([(self, r) for r in reqs], timeout_s)

@@ -1,0 +1,180 @@
+"""Op dispatch: hand-written HIP/CDNA4 kernels on GPU tensors, PyTorch reference on CPU.
+
+GPU tensors ALWAYS go to the native extension ``theroundtaible_amd._C`` (built
+in-tree by ``csrc/build.py``); if it is missing on a GPU box the op raises instead
+of silently falling back, so a test can never pass on eager PyTorch while claiming
+to exercise the kernels. (``ROUNDTABLE_ALLOW_TORCH_FALLBACK=1`` exists only for
+debugging a broken build.)
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+
+_NATIVE = None
+_NATIVE_ERR: Optional[BaseException] = None
+
+
+def native():
+    """The compiled extension module (raises if it cannot be imported)."""
+    global _NATIVE, _NATIVE_ERR
+    if _NATIVE is None and _NATIVE_ERR is None:
+        try:
+            from .. import _C  # type: ignore
+            _NATIVE = _C
+        except BaseException as e:  # noqa: BLE001
+            _NATIVE_ERR = e
+    if _NATIVE is None:
+        raise RuntimeError(f"theroundtaible_amd._C (HIP kernels) is not built/importable: {_NATIVE_ERR}. "
+                           f"Run `python csrc/build.py` (or __graft_entry__.build()).")
+    return _NATIVE
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _use_native(t: torch.Tensor) -> bool:
+    if not t.is_cuda:
+        return False
+    if os.environ.get("ROUNDTABLE_ALLOW_TORCH_FALLBACK") == "1" and not native_available():
+        return False
+    return True
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    if _use_native(x):
+        out = torch.empty_like(x)
+        native().rms_norm(out, x, w, eps)
+        return out
+    return ref.rms_norm(x, w, eps)
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                       eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Returns (rmsnorm(x + residual), x + residual). On GPU ``residual`` is updated in place."""
+    if _use_native(x):
+        out = torch.empty_like(x)
+        native().fused_add_rms_norm(out, x, residual, w, eps)
+        return out, residual
+    return ref.fused_add_rms_norm(x, residual, w, eps)
+
+
+def layer_norm(x, w, b, eps):
+    if _use_native(x):
+        out = torch.empty_like(x)
+        native().layer_norm(out, x, w, b, eps)
+        return out
+    return ref.layer_norm(x, w, b, eps)
+
+
+def fused_add_layer_norm(x, residual, w, b, eps):
+    if _use_native(x):
+        out = torch.empty_like(x)
+        native().fused_add_layer_norm(out, x, residual, w, b, eps)
+        return out, residual
+    return ref.fused_add_layer_norm(x, residual, w, b, eps)
+
+
+def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor],
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, slot_mapping: torch.Tensor,
+                   n_heads: int, n_kv_heads: int, head_dim: int) -> torch.Tensor:
+    if _use_native(qkv):
+        q = torch.empty(qkv.shape[0], n_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+        native().rope_and_cache(q, qkv, positions, cos_sin if cos_sin is not None else torch.empty(0, device=qkv.device),
+                                k_cache, v_cache, slot_mapping, n_heads, n_kv_heads, head_dim)
+        return q
+    return ref.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n_heads, n_kv_heads, head_dim)
+
+
+class DecodeWorkspace:
+    """Split-KV scratch for paged decode (static: allocated once, reused inside hipGraphs)."""
+
+    def __init__(self, max_batch: int, n_heads: int, head_dim: int, max_splits: int, device):
+        self.max_splits = max_splits
+        self.partial_o = torch.empty(max_batch * n_heads * max_splits * head_dim, dtype=torch.float32, device=device)
+        self.partial_ml = torch.empty(max_batch * n_heads * max_splits * 2, dtype=torch.float32, device=device)
+
+
+def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 32) -> int:
+    """Split-KV count fixed per (batch bucket, kv heads): ~2 workgroups per CU at any context length.
+
+    The kernel derives each split's key range from the *runtime* context length, so one
+    captured hipGraph serves every length (splits past the end are empty and skipped by the
+    reduce) — no re-capture as a knight's discussion grows."""
+    want = max(1, (2 * num_cus) // max(1, batch * n_kv_heads))
+    return int(max(1, min(max_splits, want)))
+
+
+def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           block_tables: torch.Tensor, ctx_lens: torch.Tensor, scale: float,
+                           num_splits: int = 1, workspace: Optional[DecodeWorkspace] = None,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _use_native(q):
+        if out is None:
+            out = torch.empty_like(q)
+        if workspace is None:
+            workspace = DecodeWorkspace(q.shape[0], q.shape[1], q.shape[2], max(1, num_splits), q.device)
+        native().paged_attention_decode(out, q, k_cache, v_cache, block_tables, ctx_lens, scale,
+                                        int(num_splits), workspace.partial_o, workspace.partial_ml)
+        return out
+    return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+
+
+def prefill_tile_map(cu_q: torch.Tensor, rows_per_tile: int) -> torch.Tensor:
+    """[n_tiles, 2] int32 (sequence, first row) work list for the varlen prefill kernel."""
+    items = []
+    cq = cu_q.tolist()
+    for s in range(len(cq) - 1):
+        for r in range(cq[s], cq[s + 1], rows_per_tile):
+            items.append((s, r))
+    return torch.tensor(items, dtype=torch.int32).reshape(-1, 2)
+
+
+def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                      cu_q: torch.Tensor, start_pos: torch.Tensor, scale: float,
+                      tile_map: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _use_native(q):
+        nat = native()
+        rows = nat.prefill_rows_per_tile(q.shape[1] // k_cache.shape[1])
+        if tile_map is None:
+            tile_map = prefill_tile_map(cu_q.cpu(), rows).to(q.device)
+        out = torch.empty_like(q)
+        nat.prefill_attention(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, tile_map, scale)
+        return out
+    return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q.cpu(), start_pos.cpu(), scale)
+
+
+def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
+    if _use_native(x):
+        out = torch.empty(*x.shape[:-1], x.shape[-1] // 2, dtype=x.dtype, device=x.device)
+        native().silu_and_mul(out, x)
+        return out
+    return ref.silu_and_mul(x)
+
+
+def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
+    if _use_native(x):
+        out = torch.empty_like(x)
+        native().gelu_tanh(out, x)
+        return out
+    return ref.gelu_tanh(x)
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
+           seeds: torch.Tensor, offsets: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-row ``offsets`` (int64, device-resident: the knight's position) keep hipGraph replays deterministic."""
+    if _use_native(logits):
+        if out is None:
+            out = torch.empty(logits.shape[0], dtype=torch.int64, device=logits.device)
+        native().sample(out, logits, temperature, top_p, top_k, seeds, offsets)
+        return out
+    return ref.sample(logits, temperature, top_p, top_k, seeds, offsets)

@@ -1,0 +1,213 @@
+"""Plain-PyTorch reference semantics of every hand-written kernel (the numerics oracle).
+
+These run on CPU (unit tests, the GPT-2 CPU plumbing config) and are what the HIP
+kernels in ``csrc/`` are tested against. Layouts are the engine's:
+
+* ``k_cache``: ``[num_blocks, n_kv_heads, block_size, head_dim]`` (key rows contiguous)
+* ``v_cache``: ``[num_blocks, n_kv_heads, head_dim, block_size]`` (V stored transposed per
+  block, so the P.V MFMA B-operand is a contiguous load; see csrc/attention_decode.hip)
+* ``slot = block_id * block_size + offset``
+* ``cos_sin``: ``[max_pos, head_dim]`` fp32 = ``[cos(pos*f_i) | sin(pos*f_i)]`` over
+  ``i < head_dim/2`` (Llama rotate-half convention).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+MASK64 = (1 << 64) - 1
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (y * w.float()).to(x.dtype)
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                       eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    r = (x.float() + residual.float()).to(x.dtype)
+    return rms_norm(r, w, eps), r
+
+
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def fused_add_layer_norm(x, residual, w, b, eps):
+    r = (x.float() + residual.float()).to(x.dtype)
+    return layer_norm(r, w, b, eps), r
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)
+
+
+def _rotate(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
+    # x [T, H, D] float; cs [T, D]
+    d2 = x.shape[-1] // 2
+    cos, sin = cs[:, None, :d2], cs[:, None, d2:]
+    x1, x2 = x[..., :d2], x[..., d2:]
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+
+
+def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional[torch.Tensor],
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, slot_mapping: torch.Tensor,
+                   n_heads: int, n_kv_heads: int, head_dim: int) -> torch.Tensor:
+    """Split fused qkv, rotate q/k (if cos_sin given), scatter k/v into the paged cache, return q."""
+    T = qkv.shape[0]
+    q = qkv[:, :n_heads * head_dim].reshape(T, n_heads, head_dim).float()
+    k = qkv[:, n_heads * head_dim:(n_heads + n_kv_heads) * head_dim].reshape(T, n_kv_heads, head_dim).float()
+    v = qkv[:, (n_heads + n_kv_heads) * head_dim:].reshape(T, n_kv_heads, head_dim)
+    if cos_sin is not None:
+        cs = cos_sin[positions.long()]
+        q = _rotate(q, cs)
+        k = _rotate(k, cs)
+    bs = k_cache.shape[2]
+    slots = slot_mapping.long()
+    blk, off = slots // bs, slots % bs
+    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
+    v_cache[blk, :, :, off] = v.to(v_cache.dtype)
+    return q.to(qkv.dtype)
+
+
+def _gather_kv(k_cache, v_cache, block_table, n):
+    bs = k_cache.shape[2]
+    nblk = (n + bs - 1) // bs
+    blocks = block_table[:nblk].long()
+    k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nblk * bs, k_cache.shape[1], -1)[:n]
+    v = v_cache[blocks].permute(0, 3, 1, 2).reshape(nblk * bs, v_cache.shape[1], -1)[:n]
+    return k.float(), v.float()
+
+
+def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           block_tables: torch.Tensor, ctx_lens: torch.Tensor, scale: float) -> torch.Tensor:
+    B, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    out = torch.empty_like(q)
+    for b in range(B):
+        n = int(ctx_lens[b])
+        k, v = _gather_kv(k_cache, v_cache, block_tables[b], n)     # [n, Hkv, D]
+        qb = q[b].float().reshape(Hkv, G, D)
+        s = torch.einsum("hgd,nhd->hgn", qb, k) * scale
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hgn,nhd->hgd", p, v)
+        out[b] = o.reshape(Hq, D).to(q.dtype)
+    return out
+
+
+def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                      block_tables: torch.Tensor, cu_q: torch.Tensor, start_pos: torch.Tensor,
+                      scale: float) -> torch.Tensor:
+    """Varlen causal attention: sequence s has queries cu_q[s]:cu_q[s+1] at absolute positions
+    start_pos[s] + i, attending to cached keys [0, start_pos[s] + i]."""
+    T, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    G = Hq // Hkv
+    out = torch.empty_like(q)
+    for s in range(cu_q.shape[0] - 1):
+        a, b = int(cu_q[s]), int(cu_q[s + 1])
+        if b == a:
+            continue
+        st = int(start_pos[s])
+        n = st + (b - a)
+        k, v = _gather_kv(k_cache, v_cache, block_tables[s], n)
+        qs = q[a:b].float().reshape(b - a, Hkv, G, D)
+        sc = torch.einsum("thgd,nhd->thgn", qs, k) * scale
+        qpos = torch.arange(st, n)[:, None]
+        kpos = torch.arange(n)[None, :]
+        mask = (kpos <= qpos)[:, None, None, :]
+        sc = sc.masked_fill(~mask, float("-inf"))
+        p = torch.softmax(sc, dim=-1)
+        o = torch.einsum("thgn,nhd->thgd", p, v)
+        out[a:b] = o.reshape(b - a, Hq, D).to(q.dtype)
+    return out
+
+
+def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
+    d = x.shape[-1] // 2
+    xf = x.float()
+    return (torch.nn.functional.silu(xf[..., :d]) * xf[..., d:]).to(x.dtype)
+
+
+def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
+    return torch.nn.functional.gelu(x.float(), approximate="tanh").to(x.dtype)
+
+
+# ---- sampling -----------------------------------------------------------------------------
+# Counter-based RNG shared bit-for-bit with csrc/sampling.hip: u = mix(seed, offset, idx).
+
+def _mix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & MASK64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+    return z ^ (z >> 31)
+
+
+def uniform_tensor(seed: int, offset: int, n: int) -> torch.Tensor:
+    """u in (0,1) for token indices 0..n-1 (vectorized with int64 wraparound arithmetic)."""
+    key = _mix64((seed & MASK64) ^ _mix64(offset & MASK64))
+    idx = torch.arange(n, dtype=torch.int64)
+    z = _mix_t(idx + _to_signed(key))
+    # top 24 bits -> (0,1)
+    hi = (z >> 40) & 0xFFFFFF
+    return (hi.double() + 0.5) / float(1 << 24)
+
+
+def _to_signed(x: int) -> int:
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def _mix_t(z: torch.Tensor) -> torch.Tensor:
+    def mul(a, c):
+        return a * _to_signed(c)  # int64 multiply wraps mod 2^64
+
+    def srl(a, s):  # logical right shift on int64
+        return (a >> s) & ((1 << (64 - s)) - 1)
+
+    z = z + _to_signed(0x9E3779B97F4A7C15)
+    z = mul(z ^ srl(z, 30), 0xBF58476D1CE4E5B9)
+    z = mul(z ^ srl(z, 27), 0x94D049BB133111EB)
+    return z ^ srl(z, 31)
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
+           seeds: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
+    """Greedy when temperature <= 0; else Gumbel-max over the top-k ∩ top-p set.
+
+    Row b's noise is a pure function of (seeds[b], offsets[b], token index); the engine
+    passes each knight's token position as its offset, so a knight's sample stream is
+    independent of batching, graph replay and round mode."""
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int64)
+    for b in range(B):
+        l = logits[b].float()
+        t = float(temperature[b])
+        if t <= 0:
+            out[b] = int(torch.argmax(l))
+            continue
+        z = (l - l.max()) / t
+        allowed = torch.ones(V, dtype=torch.bool)
+        k = int(top_k[b])
+        if 0 < k < V:
+            kth = torch.topk(z, k).values[-1]
+            allowed &= z >= kth
+        p = float(top_p[b])
+        if p < 1.0:
+            w = torch.where(allowed, torch.exp(z.double()), torch.zeros((), dtype=torch.float64))
+            srt, _ = torch.sort(w, descending=True)
+            cs = torch.cumsum(srt, 0)
+            cut = int(torch.searchsorted(cs, p * cs[-1]).clamp(max=V - 1))
+            thr = srt[cut]
+            allowed &= w >= thr
+        u = uniform_tensor(int(seeds[b]), int(offsets[b]), V)
+        g = -torch.log(-torch.log(u))
+        score = torch.where(allowed, z.double() + g, torch.full((), float("-inf"), dtype=torch.float64))
+        out[b] = int(torch.argmax(score))
+    return out

@@ -1,0 +1,107 @@
+"""Process topology: one process per GPU, RCCL world + gloo control plane.
+
+``torch.distributed`` with backend ``nccl`` is RCCL on ROCm; every rank owns exactly
+one GPU (``cuda:LOCAL_RANK``). A second, CPU ``gloo`` group carries host control
+traffic (seeds, turn metadata, error strings) so tiny Python objects never stall the
+xGMI links, and so the whole control plane also runs in CPU-only CI (world_size > 1
+with gloo everywhere).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Cluster:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: str = "cpu"
+    backend: str = "none"
+    cpu_group: Optional[object] = None
+
+    @property
+    def is_leader(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    # ---- control plane (gloo) -------------------------------------------------------------
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.distributed:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.cpu_group)
+        return box[0]
+
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        if not self.distributed:
+            return [obj]
+        out: List[Any] = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.cpu_group)
+        return out
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def max_scalar(self, x: float) -> float:
+        if not self.distributed:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.cpu_group)
+        return float(t[0])
+
+    def sum_scalar(self, x: float) -> float:
+        if not self.distributed:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.cpu_group)
+        return float(t[0])
+
+
+_CLUSTER: Optional[Cluster] = None
+
+
+def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
+    """Initialize from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); single process otherwise."""
+    global _CLUSTER
+    if _CLUSTER is not None:
+        return _CLUSTER
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    device = f"cuda:{local}" if use_gpu else "cpu"
+    if use_gpu:
+        torch.cuda.set_device(local)
+    c = Cluster(rank=rank, world=world, local_rank=local, device=device)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if use_gpu:
+            kw["device_id"] = torch.device(device)
+        dist.init_process_group(**kw)
+        c.backend = backend
+        c.cpu_group = dist.new_group(backend="gloo") if backend == "nccl" else dist.group.WORLD
+    _CLUSTER = c
+    return c
+
+
+def shutdown_cluster() -> None:
+    global _CLUSTER
+    if _CLUSTER is not None and _CLUSTER.distributed and dist.is_initialized():
+        dist.destroy_process_group()
+    _CLUSTER = None

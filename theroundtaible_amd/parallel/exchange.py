@@ -1,0 +1,49 @@
+"""C1: exchange every knight's turn output between ranks after a (parallel) round.
+
+Token ids travel as one padded ``int32`` tensor per rank through
+``all_gather_into_tensor`` on the default process group — RCCL over xGMI on GPUs
+(gloo in CPU CI). Each rank contributes only the knights it *leads* (the first rank
+of a knight's TP group); ~2 KB per knight, so the collective is latency-bound and
+one call per round suffices. Metadata (errors, metrics, text for backends without
+token ids) rides the gloo control group.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .cluster import Cluster
+
+# (slot, ids) pairs contributed by this rank
+Contribution = List[Tuple[int, List[int]]]
+
+
+def exchange_token_ids(cluster: Cluster, mine: Contribution, device: str) -> Dict[int, List[int]]:
+    """All-gather ragged token-id lists keyed by request slot. Returns {slot: ids} for all ranks."""
+    if not cluster.distributed:
+        return {s: list(ids) for s, ids in mine}
+    # agree on the padded shape (tiny gloo all-reduce of (rows, max_len))
+    shape = torch.tensor([len(mine), max((len(i) for _, i in mine), default=0)], dtype=torch.int64)
+    dist.all_reduce(shape, op=dist.ReduceOp.MAX, group=cluster.cpu_group)
+    rows, width = int(shape[0]), int(shape[1]) + 2
+    if rows == 0:
+        return {}
+    buf = torch.full((rows, width), -1, dtype=torch.int32)
+    for r, (slot, ids) in enumerate(mine):
+        buf[r, 0] = slot
+        buf[r, 1] = len(ids)
+        if ids:
+            buf[r, 2:2 + len(ids)] = torch.tensor(ids, dtype=torch.int32)
+    use_dev = device if cluster.backend == "nccl" else "cpu"
+    src = buf.to(use_dev)
+    out = torch.empty((cluster.world * rows, width), dtype=torch.int32, device=use_dev)
+    dist.all_gather_into_tensor(out, src)
+    host = out.cpu()
+    res: Dict[int, List[int]] = {}
+    for row in host.tolist():
+        slot, n = row[0], row[1]
+        if slot >= 0:
+            res[slot] = row[2:2 + n]
+    return res

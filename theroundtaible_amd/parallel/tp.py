@@ -1,0 +1,59 @@
+"""Tensor parallelism (Megatron-style) for oversized knights.
+
+Column-parallel: fused QKV (whole heads per rank) and gate/up; row-parallel: o_proj
+and down_proj followed by one RCCL all-reduce each (C2); the lm_head is
+vocab-parallel followed by an all-gather of the logit shards (C3). One process per
+GPU; ``torch.distributed`` backend ``nccl`` is RCCL on ROCm, ``gloo`` on CPU tests.
+
+Decode all-reduces are tiny (``[B, hidden]`` bf16 = 16 KB at B=1, 70B): they are
+latency-bound on xGMI, so they are issued on the compute stream inside the captured
+hipGraph (RCCL supports graph capture) rather than bucketed.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPInfo:
+    size: int = 1
+    rank: int = 0
+    group: Optional[object] = None   # torch.distributed ProcessGroup
+
+    @property
+    def enabled(self) -> bool:
+        return self.size > 1
+
+    def shard(self, n: int) -> int:
+        if n % self.size:
+            raise ValueError(f"dimension {n} not divisible by tp={self.size}")
+        return n // self.size
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            dist.all_reduce(x, group=self.group)
+        return x
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        """Concatenate shards along the last dim (vocab-parallel logits)."""
+        if self.size == 1:
+            return x
+        parts: List[torch.Tensor] = [torch.empty_like(x) for _ in range(self.size)]
+        dist.all_gather(parts, x.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+
+def shard_rows(w: torch.Tensor, tp: TPInfo) -> torch.Tensor:
+    """Slice the output (row of [out, in]) dimension: column-parallel linear."""
+    n = tp.shard(w.shape[0])
+    return w[tp.rank * n:(tp.rank + 1) * n].contiguous()
+
+
+def shard_cols(w: torch.Tensor, tp: TPInfo) -> torch.Tensor:
+    """Slice the input dimension: row-parallel linear."""
+    n = tp.shard(w.shape[1])
+    return w[:, tp.rank * n:(tp.rank + 1) * n].contiguous()
