@@ -149,7 +149,9 @@ def test_prefill_varlen(hq, hkv, d):
 
 def test_sample_greedy_and_topk1():
     B, V = 5, 128256
-    logits = bf(B, V, scale=3.0, seed=31)
+    # fp32 logits: bf16 random rows contain exact ties at the max, where top-k=1 legitimately
+    # keeps both tied tokens (threshold semantics) while argmax picks the lowest index.
+    logits = bf(B, V, scale=3.0, seed=31).float() + torch.arange(V, device=DEV).float() * 1e-6
     z = torch.zeros(B, device=DEV)
     one = torch.ones(B, device=DEV)
     k0 = torch.zeros(B, dtype=torch.int32, device=DEV)
