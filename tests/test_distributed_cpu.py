@@ -1,0 +1,110 @@
+"""Multi-process paths on CPU with gloo: TP equivalence, C1 token exchange, SPMD bench."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, model, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+        from theroundtaible_amd.parallel.tp import TPInfo
+        tp = TPInfo(size=world, rank=rank, group=dist.group.WORLD)
+        e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9"), tp)
+        ids = e.encode_prompt("tensor parallel knight over xGMI")
+        logits = e.prefill([(e.kv.seq("k"), ids)])
+        out = e.run_turns([Turn("k2", "tensor parallel", SamplingParams(temperature=0, max_new_tokens=6,
+                                                                        ignore_eos=True, stop_on_consensus=False))])[0]
+        if rank == 0:
+            q.put((logits.tolist(), out.ids))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-gpt2"])
+def test_tp2_matches_tp1(model):
+    from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+    e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9"))
+    ids = e.encode_prompt("tensor parallel knight over xGMI")
+    ref_logits = e.prefill([(e.kv.seq("k"), ids)])
+    ref_ids = e.run_turns([Turn("k2", "tensor parallel", SamplingParams(temperature=0, max_new_tokens=6,
+                                                                        ignore_eos=True, stop_on_consensus=False))])[0].ids
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, model, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    logits, got_ids = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert torch.allclose(torch.tensor(logits), ref_logits, atol=1e-3, rtol=1e-3)
+    assert got_ids == ref_ids
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from theroundtaible_amd.parallel.cluster import Cluster
+        from theroundtaible_amd.parallel.exchange import exchange_token_ids
+        c = Cluster(rank=rank, world=world, backend="gloo", cpu_group=dist.group.WORLD)
+        mine = [(rank * 10 + i, list(range(rank + i + 1))) for i in range(rank + 1)]
+        got = exchange_token_ids(c, mine, "cpu")
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_token_exchange_ragged():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+    expect = {r * 10 + i: list(range(r + i + 1)) for r in range(3) for i in range(r + 1)}
+    for r in range(3):
+        assert res[r] == expect
+
+
+def _bench(nproc, extra=()):
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--device", "cpu", "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "8",
+           "--temperature", "0", *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line)
+
+
+def test_spmd_bench_two_ranks():
+    out = _bench(2)
+    assert out["n_gpus"] == 2 and out["config"]["knights"] == 6 and out["config"]["tables"] == 2
+    assert out["detail"]["decode_tokens"] == 6 * 8 * 2
+    assert out["value"] > 0 and out["scaling"] == "weak"

@@ -1,0 +1,105 @@
+"""Engine plumbing on CPU (PyTorch reference ops): paged KV, prefix reuse, errors, config 1 shapes."""
+import pytest
+import torch
+
+from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+from theroundtaible_amd.engine.kv_cache import BlockAllocator, KVCacheOOM, PagedKVCache
+from theroundtaible_amd.errors import AdapterError
+from theroundtaible_amd.prompt import Prompt
+
+GREEDY = SamplingParams(temperature=0.0, max_new_tokens=10, ignore_eos=True, stop_on_consensus=False)
+
+
+def cpu_engine(model="tiny-llama", **kw):
+    cfg = dict(model=model, device="cpu", dtype="fp32", num_blocks=128, weights="random:2")
+    cfg.update(kw)
+    return Engine(EngineConfig(**cfg))
+
+
+def test_block_allocator_refcounts():
+    a = BlockAllocator(4)
+    b = [a.alloc() for _ in range(4)]
+    with pytest.raises(KVCacheOOM):
+        a.alloc()
+    a.incref(b[0])
+    a.release(b[0])
+    assert a.num_free == 0
+    a.release(b[0])
+    assert a.num_free == 1
+
+
+def test_truncate_fork_cow():
+    kv = PagedKVCache(1, 1, 8, 16, 4, "cpu", torch.float32)
+    s = kv.seq("a")
+    kv.ensure_capacity(s, 6)
+    s.tokens.extend(range(6))
+    kv.k[0, s.blocks[1]].fill_(7.0)
+    f = kv.fork("a", "b")
+    assert f.blocks == s.blocks and kv.alloc.ref[s.blocks[0]] == 2
+    kv.ensure_capacity(f, 7)          # tail block shared & partial -> copy-on-write
+    assert f.blocks[1] != s.blocks[1] and float(kv.k[0, f.blocks[1]].mean()) == 7.0
+    kv.truncate(s, 3)
+    assert len(s.blocks) == 1 and s.tokens == [0, 1, 2]
+    kv.free_seq("a")
+    kv.free_seq("b")
+    assert kv.alloc.num_free == 16
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-llama-128", "tiny-gpt2"])
+def test_prefix_reuse_is_exact(model):
+    e = cpu_engine(model)
+    t1 = e.run_turns([Turn("K", "Onderwerp: caching in de tafel.", GREEDY)])[0]
+    p2 = Prompt().add("Onderwerp: caching in de tafel.").add(t1.text, t1.ids, e.tokenizer.family).add(" Verder.")
+    t2 = e.run_turns([Turn("K", p2, GREEDY)])[0]
+    assert t2.metrics["reused_tokens"] == t1.metrics["prompt_tokens"] + len(t1.ids) - 1
+    fresh = cpu_engine(model).run_turns([Turn("K", p2, GREEDY)])[0]
+    assert fresh.ids == t2.ids
+
+
+def test_batched_equals_single():
+    e = cpu_engine()
+    both = e.run_turns([Turn("A", "eerste knight", GREEDY), Turn("B", "tweede knight, langer prompt", GREEDY)])
+    solo = cpu_engine().run_turns([Turn("B", "tweede knight, langer prompt", GREEDY)])
+    assert both[1].ids == solo[0].ids
+
+
+def test_chunked_prefill_matches_unchunked():
+    long = "woord " * 300
+    a = cpu_engine(prefill_chunk=64).run_turns([Turn("K", long, GREEDY)])[0]
+    b = cpu_engine(prefill_chunk=8192).run_turns([Turn("K", long, GREEDY)])[0]
+    assert a.ids == b.ids
+
+
+def test_oom_is_classified_and_recovers():
+    e = cpu_engine(num_blocks=4)
+    out = e.run_turns([Turn("K", "x " * 400, GREEDY)])[0]
+    assert isinstance(out.error, AdapterError) and out.error.kind == "oom"
+    assert e.kv.alloc.num_free == 4
+    ok = e.run_turns([Turn("K", "kort", SamplingParams(temperature=0, max_new_tokens=4, ignore_eos=True,
+                                                        stop_on_consensus=False))])[0]
+    assert ok.error is None and len(ok.ids) == 4
+
+
+def test_timeout():
+    e = cpu_engine(sync_every=1)
+    out = e.run_turns([Turn("K", "hallo", SamplingParams(temperature=0, max_new_tokens=50, ignore_eos=True,
+                                                         stop_on_consensus=False), timeout_s=0.0)])[0]
+    assert out.error is not None and out.error.kind == "timeout"
+
+
+def test_stop_on_consensus_cuts_generation(monkeypatch):
+    from theroundtaible_amd.engine import engine as eng_mod
+    e = cpu_engine()
+    tok = e.tokenizer
+    block = tok.encode('```json\n{"consensus_score": 9}\n```')
+    ids = block + tok.encode(" trailing junk")
+    assert eng_mod._cut_at_consensus(tok, ids) == block or len(eng_mod._cut_at_consensus(tok, ids)) <= len(block)
+
+
+def test_gpt2_small_shapes_cpu():
+    """Config 1's model builds and runs on CPU with the real GPT-2-small shapes."""
+    e = Engine(EngineConfig(model="gpt2-small", device="cpu", dtype="fp32", num_blocks=64, weights="random:0"))
+    assert e.cfg.n_layers == 12 and e.cfg.hidden == 768 and e.cfg.vocab == 50257
+    out = e.run_turns([Turn("K", "GPT-2 knight", SamplingParams(temperature=0.7, max_new_tokens=4, ignore_eos=True,
+                                                                 stop_on_consensus=False))])[0]
+    assert len(out.ids) == 4 and all(0 <= i < 50257 for i in out.ids)

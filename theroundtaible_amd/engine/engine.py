@@ -115,7 +115,7 @@ class Engine:
                 budget = int(free * self.ecfg.kv_cache_fraction) - (2 << 30)  # leave 2 GiB for activations
                 nb = max(64, budget // per_block)
             else:
-                nb = 2048
+                nb = 256   # CPU plumbing runs: 8K resident tokens per engine
         if self.ecfg.max_kv_tokens:
             nb = min(nb, (self.ecfg.max_kv_tokens + bs - 1) // bs + self.ecfg.max_batch)
         return PagedKVCache(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, int(nb), bs,

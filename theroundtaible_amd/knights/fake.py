@@ -47,7 +47,7 @@ class FakeBackend(KnightBackend):
         return self.max_chars
 
     def _run(self, req: TurnRequest, timeout_s: float) -> TurnResult:
-        seq_key, prompt = req.seq_key, req.prompt
+        seq_key, prompt = req.seq_key.split("/")[-1], req.prompt   # drop a table prefix "t3/"
         idx = self.calls[seq_key]
         self.calls[seq_key] += 1
         text = prompt_text(prompt)

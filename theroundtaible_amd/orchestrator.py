@@ -129,6 +129,7 @@ class Orchestrator:
         self.layout = self.opt.prompt_layout or config.rules.prompt_layout
         # append layout: transcript segments shared by every knight (grows append-only)
         self.transcript: List[Segment] = []
+        self.table_id = ""   # prefix of engine sequence keys (unique per table when tables share engines)
 
     # ---- fallback (orchestrator.ts:45-73) ---------------------------------------------
     def _fallback_for(self, knight: KnightConfig) -> Optional[KnightBackend]:
@@ -293,16 +294,16 @@ class Orchestrator:
                 self.ui.warn(f"  {knight.name} didn't show up today. Typical.")
                 continue
             prompt = self._prompt(knight, self.ctx, visible, rnd, self.cont is not None, files, cmds)
-            plan.append((knight, backend, TurnRequest(knight.name, prompt, rnd, self.opt.max_new_tokens)))
+            plan.append((knight, backend, TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens)))
         store.update_status(self.session_path, phase="discussing", current_knight=None, round=rnd)
         return plan
 
     def record_parallel(self, rnd: int, order: Sequence[KnightConfig],
                         results: Dict[str, Union[TurnResult, BaseException]]) -> None:
         for knight in order:
-            if knight.name not in results:
+            if self.table_id + knight.name not in results:
                 continue
-            out = results[knight.name]
+            out = results[self.table_id + knight.name]
             if isinstance(out, BaseException):
                 self._report_failure(knight, out)
                 continue
@@ -320,7 +321,7 @@ class Orchestrator:
                                   self.tool_state["files"], self.tool_state["commands"])
             msgs = THINKING.get(knight.name, ["is thinking...", "prepares their response..."])
             self.ui.print(f"  {knight.name} {msgs[self.rng.randrange(len(msgs))]}", "dim")
-            req = TurnRequest(knight.name, prompt, rnd, self.opt.max_new_tokens)
+            req = TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens)
             try:
                 res = self._execute_with_fallback(knight, backend, req, self.timeout_s)
             except Exception as e:  # noqa: BLE001 - skip the knight, continue the round
@@ -347,7 +348,7 @@ class Orchestrator:
                             out = self._execute_with_fallback_retry(knight, req, self.timeout_s, out)
                         except Exception as e:  # noqa: BLE001
                             out = e
-                    results[knight.name] = out
+                    results[req.seq_key] = out
         return results
 
     def end_round(self, rnd: int, round_ms: float) -> Optional[SessionResult]:
@@ -448,7 +449,9 @@ def run_tables_parallel(tables: Sequence[Orchestrator], topics: Sequence[str],
     """Run several independent tables in lockstep (parallel round mode): each round, every
     still-open table plans its turns, all turns execute as ONE batch (grouped per engine /
     distributed pool), then each table records and checks consensus on its own."""
-    for t, topic in zip(tables, topics):
+    for i, (t, topic) in enumerate(zip(tables, topics)):
+        if len(tables) > 1 and not t.table_id:
+            t.table_id = f"t{i}/"
         t.begin(topic)
     open_ = list(tables)
     rnd = min(t.start for t in tables)
