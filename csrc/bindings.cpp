@@ -22,7 +22,13 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
                    int max_blocks, float scale, hipStream_t stream);
 int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
                   const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
-                  const int64_t* offsets, hipStream_t stream);
+                  const int64_t* offsets, float* ws, hipStream_t stream);
+int sample_workspace_floats(int B);
+
+int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
+                       int pro, int epi, hipStream_t stream);
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, hipStream_t stream);
+
 
 namespace {
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -169,8 +175,9 @@ void gelu_tanh(torch::Tensor out, torch::Tensor x) {
 }
 
 void sample(torch::Tensor out, torch::Tensor logits, torch::Tensor temperature, torch::Tensor top_p,
-            torch::Tensor top_k, torch::Tensor seeds, torch::Tensor offsets) {
+            torch::Tensor top_k, torch::Tensor seeds, torch::Tensor offsets, torch::Tensor ws) {
   check_type(out, torch::kInt64, "out");
+  check_type(ws, torch::kFloat32, "sample workspace");
   TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V] row-major");
   const bool bf = logits.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "logits must be bf16 or fp32");
@@ -183,13 +190,63 @@ void sample(torch::Tensor out, torch::Tensor logits, torch::Tensor temperature, 
   TORCH_CHECK(out.numel() >= B && temperature.numel() >= B && top_p.numel() >= B && top_k.numel() >= B &&
                   seeds.numel() >= B && offsets.numel() >= B,
               "sampling parameter vectors shorter than the batch");
+  TORCH_CHECK(ws.numel() >= sample_workspace_floats((int)B), "sample workspace too small");
   launch_sample(out.data_ptr<int64_t>(), logits.data_ptr(), bf, (int)B, (int)logits.size(1), logits.stride(0),
                 temperature.data_ptr<float>(), top_p.data_ptr<float>(), top_k.data_ptr<int>(),
-                seeds.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), cur_stream());
+                seeds.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), ws.data_ptr<float>(), cur_stream());
+}
+// Ws: fragment-shuffled weight [N_w, K] (N_w = 2N for SwiGLU); out [M, N] (unused for RESID).
+void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t pro, int64_t epi,
+                 c10::optional<torch::Tensor> res, double eps) {
+  check_bf16(x, "x");
+  check_bf16(Ws, "Ws");
+  TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm: x [M,K], Ws [N,K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny_gemm: 1 <= M <= 16");
+  TORCH_CHECK(K % 32 == 0, "skinny_gemm: K must be a multiple of 32");
+  int64_t N = Ws.size(0);
+  if (epi == 2) {
+    TORCH_CHECK(N % 32 == 0, "swiglu W must stack [gate; up]");
+    N /= 2;
+  }
+  TORCH_CHECK(N % 16 == 0, "skinny_gemm: N must be a multiple of 16");
+  void* rp = nullptr;
+  int64_t ldo = N;
+  if (epi == 1) {
+    TORCH_CHECK(res.has_value(), "resid epilogue needs res");
+    check_bf16(*res, "res");
+    TORCH_CHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N, "resid epilogue shapes");
+    rp = res->data_ptr();
+  } else {
+    check_bf16(out, "out");
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N, "out must be [M, N]");
+    ldo = out.stride(0);
+  }
+  const int rc = launch_skinny_gemm(epi == 1 ? nullptr : out.data_ptr(), x.data_ptr(), Ws.data_ptr(), rp, (int)M,
+                                    (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, cur_stream());
+  TORCH_CHECK(rc == 0, "skinny_gemm: unsupported configuration (rc=", rc, ")");
+}
+
+void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tensor> gamma) {
+  check_bf16(Ws, "Ws");
+  check_bf16(W, "W");
+  TORCH_CHECK(W.dim() == 2 && Ws.sizes() == W.sizes(), "shuffle_weight shapes");
+  TORCH_CHECK(W.size(0) % 16 == 0 && W.size(1) % 32 == 0, "shuffle_weight: N%16, K%32");
+  const void* gp = nullptr;
+  if (gamma.has_value()) {
+    check_bf16(*gamma, "gamma");
+    TORCH_CHECK(gamma->numel() == W.size(1), "gamma must have K elements");
+    gp = gamma->data_ptr();
+  }
+  launch_shuffle_weight(Ws.data_ptr(), W.data_ptr(), gp, (int)W.size(0), (int)W.size(1), cur_stream());
 }
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
+  m.def("skinny_gemm", &skinny_gemm, "decode GEMM (M<=16), shuffled weights, fused norm / resid / swiglu",
+        py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("epi"), py::arg("res") = py::none(),
+        py::arg("eps") = 1e-5);
+  m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none());
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
@@ -202,5 +259,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_and_mul", &silu_and_mul);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("sample", &sample);
+  m.def("sample_workspace_floats", &sample_workspace_floats);
   m.attr("arch") = "gfx950";
 }

@@ -1,0 +1,197 @@
+// Decode-path linear layers (M <= 16 rows): y[M,N] = x[M,K] . W[N,K]^T on MFMA, with the
+// layer's elementwise work fused in, so a decode layer needs no separate norm/act kernels.
+//
+// Weight layout ("fragment-shuffled", built once at load time by `shuffle_weight`):
+//     Ws[N/16][K/32][64 lanes][8]   with  Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j]
+// i.e. exactly the order in which the 64 lanes of a wave hold the B operand of
+// v_mfma_f32_16x16x32_bf16. Every wave load instruction therefore reads 1 KiB of
+// contiguous HBM and a workgroup streams its 16-row panel front to back — decode GEMMs
+// are pure weight streams, so this is the whole game (on 288 GB HBM the extra copy next
+// to the row-major prefill weights is affordable: +16 GB for an 8B knight).
+//
+// One workgroup = 16 output columns (32 W rows for SwiGLU) x all of K; its 4 waves take
+// interleaved 32-deep k-steps (adjacent waves -> adjacent KiB), with the next UNROLL
+// steps' loads issued before the current steps' MFMAs (register double-buffering). M is
+// padded to the 16 MFMA rows. The waves' partial tiles are summed through LDS.
+//
+// Fusions:
+//   prologue NORM : RMSNorm of the residual stream. The norm weight gamma is folded into W
+//                   at load time, and 1/rms(x_m) factors out of the k-sum, so the kernel
+//                   feeds raw x to the MFMA, accumulates sum(x^2) from the same fragments,
+//                   and scales row m of the result by rsqrt(ss_m/K + eps) in the epilogue
+//                   (no extra pass, no atomics: deterministic).
+//   epilogue RESID: res[m,n] = bf16(acc + res[m,n])   (the residual add, in place)
+//   epilogue SWIGLU: out[m,n] = silu(acc_gate) * acc_up,  W = [gate(I) ; up(I)]
+#include "common.h"
+
+namespace {
+using rt::bf16x8;
+using rt::float4_;
+using rt::short8;
+
+constexpr int U = 4;  // k-steps per wave per pipeline stage (x2 stages in flight)
+
+enum : int { PRO_PLAIN = 0, PRO_NORM = 1 };
+enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2 };
+
+RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
+
+template <int EPI>
+struct Stage {
+  short8 w[U];
+  short8 w2[(EPI == EPI_SWIGLU) ? U : 1];
+  short8 a[U];
+};
+
+template <int EPI>
+RT_DEVICE void issue(Stage<EPI>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2,
+                     const uint16_t* __restrict__ xr, bool row_ok, int s0, int nsteps, int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int s = s0 + 4 * u;
+    if (s < nsteps) {
+      st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * 64 + lane);
+      if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt2 + (size_t)s * 64 + lane);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int s = s0 + 4 * u;
+    st.a[u] = (row_ok && s < nsteps) ? *reinterpret_cast<const short8*>(xr + s * 32) : short8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+template <int PRO, int EPI>
+RT_DEVICE void consume(const Stage<EPI>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (s0 + 4 * u < nsteps) {
+      const bf16x8 a = __builtin_bit_cast(bf16x8, st.a[u]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u]), acc, 0, 0, 0);
+      if constexpr (EPI == EPI_SWIGLU)
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u]), acc2, 0, 0, 0);
+      if constexpr (PRO == PRO_NORM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = rt::bf2f((uint16_t)st.a[u][j]);
+          ssq = fmaf(f, f, ssq);
+        }
+      }
+    }
+  }
+}
+
+template <int PRO, int EPI>
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
+                                                          const short8* __restrict__ Ws, uint16_t* __restrict__ res,
+                                                          int M, int N, int K, int ldo, float eps) {
+  __shared__ float red[4][(EPI == EPI_SWIGLU) ? 2 : 1][16][17];
+  __shared__ float sq[4][16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x;
+  const int nsteps = K / 32;
+  const bool row_ok = r < M;
+  const uint16_t* xr = x + (size_t)(row_ok ? r : 0) * K + 8 * g;
+  const short8* wt = Ws + (size_t)tile * nsteps * 64;
+  const short8* wt2 = (EPI == EPI_SWIGLU) ? Ws + (size_t)(N / 16 + tile) * nsteps * 64 : nullptr;
+
+  float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  float ssq = 0.f;
+  Stage<EPI> st0, st1;
+  int s = wid;
+  issue<EPI>(st0, wt, wt2, xr, row_ok, s, nsteps, lane);
+  for (;;) {
+    const int sn = s + 4 * U;
+    if (sn < nsteps) issue<EPI>(st1, wt, wt2, xr, row_ok, sn, nsteps, lane);
+    consume<PRO, EPI>(st0, acc, acc2, ssq, s, nsteps);
+    if (sn >= nsteps) break;
+    s = sn;
+    const int sn2 = s + 4 * U;
+    if (sn2 < nsteps) issue<EPI>(st0, wt, wt2, xr, row_ok, sn2, nsteps, lane);
+    consume<PRO, EPI>(st1, acc, acc2, ssq, s, nsteps);
+    if (sn2 >= nsteps) break;
+    s = sn2;
+  }
+
+  // C layout: acc[i] = C[m = 4g + i][n = r]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[wid][0][4 * g + i][r] = acc[i];
+    if constexpr (EPI == EPI_SWIGLU) red[wid][(EPI == EPI_SWIGLU) ? 1 : 0][4 * g + i][r] = acc2[i];
+  }
+  if constexpr (PRO == PRO_NORM) {
+    ssq += __shfl_xor(ssq, 16, 64);
+    ssq += __shfl_xor(ssq, 32, 64);
+    if (g == 0) sq[wid][r] = ssq;
+  }
+  __syncthreads();
+  const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
+  if (m < M) {
+    float v = red[0][0][m][n] + red[1][0][m][n] + red[2][0][m][n] + red[3][0][m][n];
+    float inv = 1.f;
+    if constexpr (PRO == PRO_NORM) inv = rsqrtf((sq[0][m] + sq[1][m] + sq[2][m] + sq[3][m]) / (float)K + eps);
+    v *= inv;
+    const int col = tile * 16 + n;
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int u1 = (EPI == EPI_SWIGLU) ? 1 : 0;
+      const float up = (red[0][u1][m][n] + red[1][u1][m][n] + red[2][u1][m][n] + red[3][u1][m][n]) * inv;
+      out[(size_t)m * ldo + col] = rt::f2bf(silu(v) * up);
+    } else if constexpr (EPI == EPI_RESID) {
+      uint16_t* rp = res + (size_t)m * N + col;
+      *rp = rt::f2bf(v + rt::bf2f(*rp));
+    } else {
+      out[(size_t)m * ldo + col] = rt::f2bf(v);
+    }
+  }
+}
+
+// Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j] (optionally W * gamma[k] folded in)
+__global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restrict__ W,
+                               const uint16_t* __restrict__ gamma, int N, int K) {
+  const int nsteps = K / 32;
+  const int64_t total = (int64_t)(N / 16) * nsteps * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(i & 63);
+    const int64_t ts = i >> 6;
+    const int s = (int)(ts % nsteps);
+    const int64_t t = ts / nsteps;
+    const int row = (int)(16 * t + (l & 15));
+    const int k0 = 32 * s + 8 * (l >> 4);
+    short8 v = *reinterpret_cast<const short8*>(W + (size_t)row * K + k0);
+    if (gamma != nullptr) {
+      const short8 gv = *reinterpret_cast<const short8*>(gamma + k0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (short)rt::f2bf(rt::bf2f((uint16_t)v[j]) * rt::bf2f((uint16_t)gv[j]));
+    }
+    Ws[i] = v;
+  }
+}
+}  // namespace
+
+int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
+                       int pro, int epi, hipStream_t stream) {
+  if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
+  dim3 grid(N / 16), block(256);
+#define RT_SG(P, E)                                                                                                \
+  hipLaunchKernelGGL((skinny_gemm_kernel<P, E>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)x,       \
+                     (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps)
+  if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SG(PRO_PLAIN, EPI_STORE);
+  else if (pro == PRO_NORM && epi == EPI_STORE) RT_SG(PRO_NORM, EPI_STORE);
+  else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_SG(PRO_PLAIN, EPI_RESID);
+  else if (pro == PRO_NORM && epi == EPI_SWIGLU) RT_SG(PRO_NORM, EPI_SWIGLU);
+  else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_SG(PRO_PLAIN, EPI_SWIGLU);
+  else return -2;
+#undef RT_SG
+  return 0;
+}
+
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, hipStream_t stream) {
+  if (K % 32 || N % 16) return -1;
+  const int64_t total = (int64_t)N * K / 8;
+  int64_t grid = (total + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(shuffle_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (short8*)Ws, (const uint16_t*)W,
+                     (const uint16_t*)gamma, N, K);
+  return 0;
+}

@@ -1,18 +1,42 @@
-// K6: fused sampler — greedy / temperature / top-k / top-p in one kernel, graph-safe RNG.
+// K6: fused sampler — greedy / temperature / top-k / top-p, graph-safe RNG, multi-CU.
 //
-// One 1024-thread workgroup per row (B <= 32 rows, V up to 128256: the row stays
-// L2-resident across passes). Sampling is Gumbel-max: token = argmax(z_i + g_i) over the
-// allowed set, z = (logit - max)/T, g_i = -log(-log(u_i)), u_i a counter-based hash of
-// (seed, offset, i) — no RNG state, so a captured hipGraph replays deterministically
-// and the stream of a knight depends only on (seed, knight, position) (the engine passes
-// each row's token position as its offset). Top-k and top-p thresholds are found
-// EXACTLY with a 4-pass 8-bit radix select over order-preserving float keys, weighted
-// by count (top-k) or probability mass (top-p): no sort, no bisection.
+// Sampling is Gumbel-max: token = argmax(z_i + g_i) over the allowed set, z = (logit - max)/T,
+// g_i = -log(-log(u_i)), u_i a counter-based hash of (seed, offset, i): no RNG state, so a
+// captured hipGraph replays deterministically and a knight's stream depends only on
+// (seed, knight, position) (the engine passes each row's token position as `offset`).
+//
+// Each row is split into C chunks handled by C workgroups (a single workgroup per row is
+// LDS-atomic-bound: 2 x 128K histogram atomics on one CU), in five graph-capturable launches:
+//   1 stats  : per-chunk max/argmax                                  (grid B x C)
+//   2 hist   : coarse 2048-bin histogram of z over [-ZR, 0] (count + probability mass),
+//              chunk-local in LDS then merged with one global atomic per non-empty bin
+//   3 select : per row, block-scan the histogram -> the bin where top-k (count) or top-p
+//              (mass) crosses                                          (grid B)
+//   4 refine : 2048-bin sub-histogram of that one bin                 (grid B x C)
+//   5 final  : threshold from the sub-histogram, Gumbel-argmax over the chunk, then the
+//              last-arriving chunk of each row reduces the partials   (grid B x C)
+// Threshold resolution ZR/4M ~ 7e-6 in z; every pass uses 16-byte vector loads (G13).
 // Bit-for-bit RNG twin: theroundtaible_amd/ops/reference.py::uniform_tensor.
 #include "common.h"
 
 namespace {
-constexpr int NT = 1024;
+constexpr int NB = 2048;
+constexpr int NT = 256;
+constexpr int C = 32;       // chunks (workgroups) per row
+constexpr float ZR = 30.f;  // exp(-30) * 128K < 1e-8 of the mass: ignored
+
+// per-row workspace layout (floats / ints interchangeable, 4 bytes each)
+constexpr int W_MAX = 0;                 // [C] chunk max
+constexpr int W_ARG = W_MAX + C;         // [C] chunk argmax (int)
+constexpr int W_HC = W_ARG + C;          // [NB] coarse count
+constexpr int W_HM = W_HC + NB;          // [NB] coarse mass
+constexpr int W_SC = W_HM + NB;          // [NB] sub count
+constexpr int W_SM = W_SC + NB;          // [NB] sub mass
+constexpr int W_SEL = W_SM + NB;         // bsel(int), by_count(int), need(float), row max(float)
+constexpr int W_PV = W_SEL + 4;          // [C] partial score
+constexpr int W_PI = W_PV + C;           // [C] partial index (int)
+constexpr int W_CNT = W_PI + C;          // arrival counter (int)
+constexpr int W_ROW = W_CNT + 4;         // floats per row (memset region: whole row)
 
 RT_DEVICE uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -25,161 +49,345 @@ RT_DEVICE float gumbel(uint64_t key, uint32_t i) {
   const float u = ((float)(uint32_t)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
   return -__logf(-__logf(u));
 }
-RT_DEVICE uint32_t okey(float f) {  // order-preserving float -> uint32
-  const uint32_t b = __float_as_uint(f);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
 
-template <typename T>
-RT_DEVICE float ld(const T* p, int i) {
-  return rt::DT<T>::load(p + i);
-}
-
-// Radix select: smallest key K such that weight(keys > K) < target <= weight(keys >= K),
-// over elements with key >= floor_key. WEIGHTED: weight = exp(z); else weight = 1.
-template <typename T, bool WEIGHTED>
-RT_DEVICE uint32_t radix_select(const T* row, int V, float mx, float invT, uint32_t floor_key, float target,
-                                float* hist, uint32_t* sh_u, float* sh_f) {
-  uint32_t prefix = 0, mask = 0;
-  float remaining = target;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int b = threadIdx.x; b < 256; b += NT) hist[b] = 0.f;
-    __syncthreads();
-    for (int i = threadIdx.x; i < V; i += NT) {
-      const float z = (ld(row, i) - mx) * invT;
-      const uint32_t k = okey(z);
-      if (k >= floor_key && (k & mask) == prefix) {
-        const float w = WEIGHTED ? __expf(z) : 1.f;
-        atomicAdd(&hist[(k >> shift) & 0xFF], w);
-      }
+template <typename T, bool VEC, typename F>
+RT_DEVICE void for_chunk(const T* row, int lo, int hi, F&& f) {
+  // lo is a multiple of 8 (chunk boundaries are), so the vector path stays aligned
+  if constexpr (VEC && sizeof(T) == 2) {
+    const int nv = (hi - lo) >> 3;
+    const rt::short8* p = reinterpret_cast<const rt::short8*>(row + lo);
+    for (int c = threadIdx.x; c < nv; c += NT) {
+      const rt::short8 v = p[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f(lo + c * 8 + j, rt::bf2f((uint16_t)v[j]));
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float cum = 0.f;
-      int sel = 0;
-      for (int b = 255; b >= 0; --b) {
-        if (cum + hist[b] >= remaining) {
-          sel = b;
-          break;
-        }
-        cum += hist[b];
-        if (b == 0) sel = 0;  // rounding: fall back to the lowest bin
-      }
-      *sh_u = (uint32_t)sel;
-      *sh_f = cum;
+    for (int i = lo + (nv << 3) + threadIdx.x; i < hi; i += NT) f(i, rt::DT<T>::load(row + i));
+  } else if constexpr (VEC) {
+    const int nv = (hi - lo) >> 2;
+    const float4* p = reinterpret_cast<const float4*>(row + lo);
+    for (int c = threadIdx.x; c < nv; c += NT) {
+      const float4 v = p[c];
+      f(lo + c * 4 + 0, v.x);
+      f(lo + c * 4 + 1, v.y);
+      f(lo + c * 4 + 2, v.z);
+      f(lo + c * 4 + 3, v.w);
     }
-    __syncthreads();
-    prefix |= (*sh_u) << shift;
-    mask |= 0xFFu << shift;
-    remaining -= *sh_f;
-    __syncthreads();
+    for (int i = lo + (nv << 2) + threadIdx.x; i < hi; i += NT) f(i, rt::DT<T>::load(row + i));
+  } else {
+    for (int i = lo + threadIdx.x; i < hi; i += NT) f(i, rt::DT<T>::load(row + i));
   }
-  return prefix;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(NT) sample_kernel(int64_t* __restrict__ out, const T* __restrict__ logits, int V,
-                                                    int64_t ld_row, const float* __restrict__ temperature,
-                                                    const float* __restrict__ top_p, const int* __restrict__ top_k,
-                                                    const int64_t* __restrict__ seeds,
-                                                    const int64_t* __restrict__ offsets) {
-  __shared__ float hist[256];
-  __shared__ float red_f[32];
-  __shared__ int red_i[32];
-  __shared__ uint32_t sh_u;
-  __shared__ float sh_f;
-  const int b = blockIdx.x;
-  const T* row = logits + (size_t)b * ld_row;
-  const float temp = temperature[b];
+struct ArgMax {
+  float v;
+  int i;
+};
+RT_DEVICE void am_merge(ArgMax& a, float v, int i) {
+  if (v > a.v || (v == a.v && i < a.i)) {
+    a.v = v;
+    a.i = i;
+  }
+}
+RT_DEVICE ArgMax block_argmax(ArgMax a, float* sv, int* si) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am_merge(a, __shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64));
+  __syncthreads();
+  if (lane == 0) {
+    sv[wid] = a.v;
+    si[wid] = a.i;
+  }
+  __syncthreads();
+  ArgMax b{lane < NT / 64 ? sv[lane] : -INFINITY, lane < NT / 64 ? si[lane] : 0x7fffffff};
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am_merge(b, __shfl_xor(b.v, o, 64), __shfl_xor(b.i, o, 64));
+  return b;
+}
 
-  // pass 1: max (greedy: argmax directly)
-  float best = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int i = threadIdx.x; i < V; i += NT) {
-    const float v = ld(row, i);
-    if (v > best) {  // i increasing per thread: keeps the lowest index on ties
-      best = v;
-      bi = i;
+RT_DEVICE void chunk_range(int V, int c, int& lo, int& hi) {
+  const int per = ((V + C - 1) / C + 7) & ~7;
+  lo = min(V, c * per);
+  hi = min(V, lo + per);
+}
+
+RT_DEVICE float row_max(const float* ws) {
+  float m = -INFINITY;
+  for (int c = 0; c < C; ++c) m = fmaxf(m, ws[W_MAX + c]);
+  return m;
+}
+
+// ---- 1: chunk max / argmax -----------------------------------------------------------------
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(NT) smp_stats(float* __restrict__ ws, const T* __restrict__ logits, int V,
+                                                int64_t ld) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int b = blockIdx.x, c = blockIdx.y;
+  int lo, hi;
+  chunk_range(V, c, lo, hi);
+  ArgMax a{-INFINITY, 0x7fffffff};
+  for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) { am_merge(a, v, i); });
+  a = block_argmax(a, sv, si);
+  if (threadIdx.x == 0) {
+    float* w = ws + (size_t)b * W_ROW;
+    w[W_MAX + c] = a.v;
+    reinterpret_cast<int*>(w)[W_ARG + c] = a.i;
+  }
+}
+
+// ---- 2 / 4: (sub-)histograms ---------------------------------------------------------------
+template <typename T, bool VEC, bool SUB>
+__global__ void __launch_bounds__(NT) smp_hist(float* __restrict__ ws, const T* __restrict__ logits, int V, int64_t ld,
+                                               const float* __restrict__ temperature, const float* __restrict__ top_p,
+                                               const int* __restrict__ top_k) {
+  __shared__ float hc[NB], hm[NB];
+  const int b = blockIdx.x, c = blockIdx.y;
+  float* w = ws + (size_t)b * W_ROW;
+  const float temp = temperature[b];
+  const int k = top_k[b];
+  if (!(temp > 0.f) || !((k > 0 && k < V) || top_p[b] < 1.f)) return;
+  int bsel = 0;
+  if constexpr (SUB) {
+    bsel = reinterpret_cast<const int*>(w)[W_SEL];
+    if (bsel >= NB) return;
+  }
+  for (int i = threadIdx.x; i < NB; i += NT) {
+    hc[i] = 0.f;
+    hm[i] = 0.f;
+  }
+  __syncthreads();
+  const float mx = row_max(w), invT = 1.f / temp, scale = NB / ZR;
+  const float top_edge = -(float)bsel / scale;
+  const float sub = scale * NB;
+  int lo, hi;
+  chunk_range(V, c, lo, hi);
+  for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int, float v) {
+    const float z = (v - mx) * invT;
+    const float fb = -z * scale;
+    if constexpr (SUB) {
+      if (fb >= (float)bsel && fb < (float)(bsel + 1)) {
+        int sb = (int)((top_edge - z) * sub);
+        sb = sb < 0 ? 0 : (sb >= NB ? NB - 1 : sb);
+        atomicAdd(&hc[sb], 1.f);
+        atomicAdd(&hm[sb], __expf(z));
+      }
+    } else if (fb < (float)NB) {
+      const int bin = (int)fb;
+      atomicAdd(&hc[bin], 1.f);
+      atomicAdd(&hm[bin], __expf(z));
+    }
+  });
+  __syncthreads();
+  float* gc = w + (SUB ? W_SC : W_HC);
+  float* gm = w + (SUB ? W_SM : W_HM);
+  for (int i = threadIdx.x; i < NB; i += NT) {
+    if (hc[i] != 0.f) {
+      atomicAdd(gc + i, hc[i]);
+      atomicAdd(gm + i, hm[i]);
     }
   }
-  auto argmax_reduce = [&](float& v, int& idx) {
+}
+
+// First bin whose inclusive prefix of `a` reaches ta or of `bm` reaches tb (1024 threads, 2 bins each).
+RT_DEVICE int first_crossing(const float* a, const float* bm, float ta, float tb, float* scr, int* res, float* pa,
+                             float* pb) {
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const float a0 = a[2 * t], a1 = a[2 * t + 1], b0 = bm[2 * t], b1 = bm[2 * t + 1];
+  float sa = a0 + a1, sb = b0 + b1;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(v, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (ov > v || (ov == v && oi < idx)) {
-        v = ov;
-        idx = oi;
-      }
+  for (int o = 1; o < 64; o <<= 1) {
+    const float xa = __shfl_up(sa, o, 64), xb = __shfl_up(sb, o, 64);
+    if (lane >= o) {
+      sa += xa;
+      sb += xb;
     }
-    if (lane == 0) {
-      red_f[wid] = v;
-      red_i[wid] = idx;
-    }
-    __syncthreads();
-    v = lane < NT / 64 ? red_f[lane] : -INFINITY;
-    idx = lane < NT / 64 ? red_i[lane] : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(v, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (ov > v || (ov == v && oi < idx)) {
-        v = ov;
-        idx = oi;
-      }
-    }
-    __syncthreads();
-  };
-  argmax_reduce(best, bi);
-  if (!(temp > 0.f)) {
-    if (threadIdx.x == 0) out[b] = bi;
+  }
+  __syncthreads();
+  if (lane == 63) {
+    scr[wid] = sa;
+    scr[32 + wid] = sb;
+  }
+  if (t == 0) *res = NB;
+  __syncthreads();
+  float oa = 0.f, ob = 0.f;
+  for (int w = 0; w < wid; ++w) {
+    oa += scr[w];
+    ob += scr[32 + w];
+  }
+  const float ia = oa + sa, ib = ob + sb, ea = ia - a0 - a1, eb = ib - b0 - b1;
+  int cross = NB;
+  if (ea + a0 >= ta || eb + b0 >= tb) cross = 2 * t;
+  else if (ia >= ta || ib >= tb) cross = 2 * t + 1;
+  if (cross < NB) atomicMin(res, cross);
+  __syncthreads();
+  const int cb = *res;
+  if (cb < NB && (cb >> 1) == t) {
+    *pa = (cb & 1) ? ea + a0 : ea;
+    *pb = (cb & 1) ? eb + b0 : eb;
+  }
+  __syncthreads();
+  return cb;
+}
+
+// ---- 3: select the threshold bin ---------------------------------------------------------------
+__global__ void __launch_bounds__(1024) smp_select(float* __restrict__ ws, int V, const float* __restrict__ temperature,
+                                                   const float* __restrict__ top_p, const int* __restrict__ top_k) {
+  __shared__ float scr[64];
+  __shared__ int sres;
+  __shared__ float spa, spb;
+  const int b = blockIdx.x;
+  float* w = ws + (size_t)b * W_ROW;
+  int* wi = reinterpret_cast<int*>(w);
+  const int k = top_k[b];
+  const float p = top_p[b];
+  if (!(temperature[b] > 0.f) || !((k > 0 && k < V) || p < 1.f)) {
+    if (threadIdx.x == 0) wi[W_SEL] = NB;
     return;
   }
-  const float mx = best;
-  const float invT = 1.f / temp;
-  uint32_t floor_key = 0;
-  const int k = top_k[b];
-  if (k > 0 && k < V) floor_key = radix_select<T, false>(row, V, mx, invT, 0u, (float)k, hist, &sh_u, &sh_f);
-  const float p = top_p[b];
-  if (p < 1.f) {
-    float zs = 0.f;
-    for (int i = threadIdx.x; i < V; i += NT) {
-      const float z = (ld(row, i) - mx) * invT;
-      if (okey(z) >= floor_key) zs += __expf(z);
+  const float* hc = w + W_HC;
+  const float* hm = w + W_HM;
+  float tm = 0.f;
+  for (int i = threadIdx.x; i < NB; i += 1024) tm += hm[i];
+  tm = rt::block_sum(tm, scr);
+  __syncthreads();
+  const bool use_k = k > 0 && k < V;
+  const float tk = use_k ? (float)k : 3.0e38f;
+  int bk = NB;
+  float pre_c = 0.f, zk_mass = tm;
+  if (use_k) {
+    bk = first_crossing(hc, hm, tk, 3.0e38f, scr, &sres, &spa, &spb);
+    if (bk < NB) {
+      zk_mass = spb + hm[bk];
+      pre_c = spa;
     }
-    zs = rt::block_sum(zs, red_f);
-    __syncthreads();
-    const uint32_t tp = radix_select<T, true>(row, V, mx, invT, floor_key, p * zs, hist, &sh_u, &sh_f);
-    floor_key = tp > floor_key ? tp : floor_key;
+  }
+  const float tp = p < 1.f ? p * zk_mass : 3.0e38f;
+  int bp = NB;
+  float pre_m = 0.f;
+  if (p < 1.f) {
+    bp = first_crossing(hc, hm, 3.0e38f, tp, scr, &sres, &spa, &spb);
+    pre_m = spb;
+  }
+  if (threadIdx.x == 0) {
+    if (bk <= bp) {
+      wi[W_SEL] = bk;
+      wi[W_SEL + 1] = 1;
+      w[W_SEL + 2] = tk - pre_c;
+    } else {
+      wi[W_SEL] = bp;
+      wi[W_SEL + 1] = 0;
+      w[W_SEL + 2] = tp - pre_m;
+    }
+  }
+}
+
+// ---- 5: threshold + Gumbel argmax + last-arriver reduction --------------------------------------
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(1024) smp_final(int64_t* __restrict__ out, float* __restrict__ ws,
+                                                  const T* __restrict__ logits, int V, int64_t ld,
+                                                  const float* __restrict__ temperature,
+                                                  const int64_t* __restrict__ seeds,
+                                                  const int64_t* __restrict__ offsets) {
+  __shared__ float scr[64];
+  __shared__ int sres;
+  __shared__ float spa, spb;
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  __shared__ int last;
+  const int b = blockIdx.x, c = blockIdx.y;
+  float* w = ws + (size_t)b * W_ROW;
+  int* wi = reinterpret_cast<int*>(w);
+  const float temp = temperature[b];
+  if (!(temp > 0.f)) {  // greedy: argmax over the chunk maxima
+    if (c == 0 && threadIdx.x == 0) {
+      ArgMax a{-INFINITY, 0x7fffffff};
+      for (int j = 0; j < C; ++j) am_merge(a, w[W_MAX + j], wi[W_ARG + j]);
+      out[b] = a.i;
+    }
+    return;
+  }
+  const float mx = row_max(w), invT = 1.f / temp, scale = NB / ZR;
+  float zthr = -INFINITY;
+  const int bsel = wi[W_SEL];
+  if (bsel < NB) {
+    const bool by_count = wi[W_SEL + 1] != 0;
+    const float need = w[W_SEL + 2];
+    const int cb = by_count ? first_crossing(w + W_SC, w + W_SM, need, 3.0e38f, scr, &sres, &spa, &spb)
+                            : first_crossing(w + W_SC, w + W_SM, 3.0e38f, need, scr, &sres, &spa, &spb);
+    const int cc = cb < NB ? cb : NB - 1;
+    zthr = -(float)bsel / scale - (float)(cc + 1) / (scale * NB);
   }
   const uint64_t key = mix64((uint64_t)seeds[b] ^ mix64((uint64_t)offsets[b]));
-  float bv = -INFINITY;
-  int bidx = 0x7fffffff;
-  for (int i = threadIdx.x; i < V; i += NT) {
-    const float z = (ld(row, i) - mx) * invT;
-    if (okey(z) >= floor_key) {
-      const float s = z + gumbel(key, (uint32_t)i);
-      if (s > bv) {
-        bv = s;
-        bidx = i;
+  int lo, hi;
+  chunk_range(V, c, lo, hi);
+  ArgMax a{-INFINITY, 0x7fffffff};
+  // 1024 threads walk the chunk (NT is 256 in for_chunk's stride: walk 4 sub-ranges)
+  const T* row = logits + (size_t)b * ld;
+  for (int i = lo + threadIdx.x; i < hi; i += 1024) {
+    const float z = (rt::DT<T>::load(row + i) - mx) * invT;
+    if (z >= zthr) am_merge(a, z + gumbel(key, (uint32_t)i), i);
+  }
+  // block argmax over 16 waves
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am_merge(a, __shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64));
+  if (lane == 0) {
+    sv[wid] = a.v;
+    si[wid] = a.i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ArgMax bm{-INFINITY, 0x7fffffff};
+    for (int j = 0; j < 16; ++j) am_merge(bm, sv[j], si[j]);
+    // publish this chunk's partial, then count arrivals (release/acquire at agent scope, G16)
+    __hip_atomic_store(&w[W_PV + c], bm.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&wi[W_PI + c], bm.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int prev = __hip_atomic_fetch_add(&wi[W_CNT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (prev == C - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      ArgMax r{-INFINITY, 0x7fffffff};
+      for (int j = 0; j < C; ++j)
+        am_merge(r, __hip_atomic_load(&w[W_PV + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&wi[W_PI + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (r.i == 0x7fffffff) {  // empty allowed set (rounding): fall back to the row argmax
+        for (int j = 0; j < C; ++j) am_merge(r, w[W_MAX + j], wi[W_ARG + j]);
       }
+      out[b] = r.i;
     }
   }
-  argmax_reduce(bv, bidx);
-  if (threadIdx.x == 0) out[b] = bidx == 0x7fffffff ? bi : bidx;
 }
 }  // namespace
 
+int sample_workspace_floats(int B) { return B * W_ROW; }
+
 int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
                   const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
-                  const int64_t* offsets, hipStream_t stream) {
+                  const int64_t* offsets, float* ws, hipStream_t stream) {
   if (B == 0) return 0;
-  if (is_bf16)
-    hipLaunchKernelGGL(sample_kernel<uint16_t>, dim3(B), dim3(NT), 0, stream, out, (const uint16_t*)logits, V, ld_row,
-                       temperature, top_p, top_k, seeds, offsets);
-  else
-    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(NT), 0, stream, out, (const float*)logits, V, ld_row,
-                       temperature, top_p, top_k, seeds, offsets);
+  const size_t esz = is_bf16 ? 2 : 4;
+  const bool vec = ((uintptr_t)logits % 16 == 0) && ((ld_row * esz) % 16 == 0);
+  hipMemsetAsync(ws, 0, sizeof(float) * (size_t)B * W_ROW, stream);  // histograms + counters, every call
+  const dim3 g2(B, C);
+#define RT_SMP(TT, VV)                                                                                              \
+  do {                                                                                                              \
+    hipLaunchKernelGGL((smp_stats<TT, VV>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row);             \
+    hipLaunchKernelGGL((smp_hist<TT, VV, false>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,        \
+                       temperature, top_p, top_k);                                                                  \
+    hipLaunchKernelGGL(smp_select, dim3(B), dim3(1024), 0, stream, ws, V, temperature, top_p, top_k);              \
+    hipLaunchKernelGGL((smp_hist<TT, VV, true>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,         \
+                       temperature, top_p, top_k);                                                                  \
+    hipLaunchKernelGGL((smp_final<TT, VV>), g2, dim3(1024), 0, stream, out, ws, (const TT*)logits, V, ld_row,       \
+                       temperature, seeds, offsets);                                                                \
+  } while (0)
+  if (is_bf16) {
+    if (vec) RT_SMP(uint16_t, true);
+    else RT_SMP(uint16_t, false);
+  } else {
+    if (vec) RT_SMP(float, true);
+    else RT_SMP(float, false);
+  }
+#undef RT_SMP
   return 0;
 }

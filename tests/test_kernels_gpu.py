@@ -190,3 +190,4 @@ def test_sample_top_p_nucleus():
                          torch.tensor([s], device=DEV))
         hits.add(int(tok))
     assert hits <= {0, 1} and len(hits) == 2
+

@@ -95,6 +95,8 @@ class Engine:
         with torch.no_grad():
             weights = materialize(self.cfg, ecfg.weights, self.device, self.dtype, self.tp)
             self.model = build_model(self.cfg, weights, self.device, self.dtype, self.tp)
+            if self.on_gpu and hasattr(self.model, "decode_weights") and self.tp.size == 1:
+                self.model.decode_weights()   # shuffled decode copies before sizing the KV pool
         self.load_s = time.perf_counter() - t0
         self.kv = self._alloc_kv()
         self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}

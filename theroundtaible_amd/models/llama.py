@@ -68,8 +68,55 @@ class LlamaModel:
         return ops.prefill_attention(q, kc, vc, meta.block_tables, meta.cu_q, meta.start_pos, self.scale,
                                      meta.tile_map)
 
+    def fused_decode_ok(self, ids: torch.Tensor) -> bool:
+        cfg = self.cfg
+        return (ids.is_cuda and self.tp.size == 1 and 1 <= ids.shape[0] <= 16 and self.use_fused
+                and cfg.hidden % 32 == 0 and cfg.ffn % 32 == 0 and (cfg.n_heads * cfg.head_dim) % 32 == 0
+                and self.w["lm_head"].shape[0] % 16 == 0)
+
+    use_fused = True
+    _dec = None
+
+    def decode_weights(self):
+        """Fragment-shuffled, norm-folded copies of every linear for the fused decode path
+        (built lazily once; +1x weight memory, affordable on 288 GB HBM)."""
+        if self._dec is None:
+            with torch.no_grad():
+                layers = []
+                for lw in self.layers:
+                    layers.append({
+                        "wqkv": ops.shuffle_weight(lw["wqkv"], lw["attn_norm"]),
+                        "wo": ops.shuffle_weight(lw["wo"]),
+                        "w_gate_up": ops.shuffle_weight(lw["w_gate_up"], lw["ffn_norm"]),
+                        "w_down": ops.shuffle_weight(lw["w_down"]),
+                    })
+                self._dec = {"layers": layers, "lm_head": ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])}
+        return self._dec
+
+    def forward_decode_fused(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta) -> torch.Tensor:
+        """Decode step with every norm / residual / activation fused into the MFMA GEMMs
+        (csrc/gemm_skinny.hip): per layer qkv(+RMSNorm) -> K2 -> K3 -> o(+residual) ->
+        gate_up(+RMSNorm, SwiGLU) -> down(+residual). 6 launches per layer, no norm kernels."""
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        dec = self.decode_weights()
+        res = F.embedding(ids, self.w["embed"]).contiguous()
+        B = ids.shape[0]
+        for l, lw in enumerate(dec["layers"]):
+            qkv = ops.skinny_gemm(res, lw["wqkv"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
+            q = ops.rope_and_cache(qkv, positions, self.cos_sin, kv.k_layer(l), kv.v_layer(l), meta.slot_mapping,
+                                   self.n_heads, self.n_kv_heads, self.head_dim)
+            a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)
+            ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
+            g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps)
+            ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
+        logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
+        return logits[:, :cfg.vocab]
+
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta) -> torch.Tensor:
         """Returns logits [rows, vocab] (all rows for decode, ``meta.last_rows`` for prefill)."""
+        if meta.kind == "decode" and self.fused_decode_ok(ids):
+            return self.forward_decode_fused(ids, positions, kv, meta)
         cfg, tp = self.cfg, self.tp
         T = ids.shape[0]
         h = F.embedding(ids, self.w["embed"])

@@ -153,6 +153,32 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q.cpu(), start_pos.cpu(), scale)
 
 
+PRO_PLAIN, PRO_NORM = 0, 1
+EPI_STORE, EPI_RESID, EPI_SWIGLU = 0, 1, 2
+
+
+def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode-weight copy in the MFMA fragment order of csrc/gemm_skinny.hip, with an RMSNorm
+    weight ``gamma`` (over K) optionally folded in. On CPU: the row-major ``W * gamma``."""
+    if _use_native(W):
+        Ws = torch.empty_like(W)
+        native().shuffle_weight(Ws, W.contiguous(), gamma)
+        return Ws
+    return ref.fold_gamma(W, gamma)
+
+
+def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: int = EPI_STORE,
+                res: Optional[torch.Tensor] = None, eps: float = 1e-5) -> Optional[torch.Tensor]:
+    """Decode linear (M <= 16) on shuffled weights with fused RMSNorm prologue (gamma pre-folded)
+    and residual / SwiGLU epilogue. Returns the output (None for RESID, which updates ``res``)."""
+    if _use_native(x):
+        n = Ws.shape[0] // (2 if epi == EPI_SWIGLU else 1)
+        out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device) if epi != EPI_RESID else x
+        native().skinny_gemm(out, x, Ws, pro, epi, res, eps)
+        return None if epi == EPI_RESID else out
+    return ref.skinny_gemm(x, Ws, pro, epi, res, eps)
+
+
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
     if _use_native(x):
         out = torch.empty(*x.shape[:-1], x.shape[-1] // 2, dtype=x.dtype, device=x.device)
@@ -175,6 +201,8 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     if _use_native(logits):
         if out is None:
             out = torch.empty(logits.shape[0], dtype=torch.int64, device=logits.device)
-        native().sample(out, logits, temperature, top_p, top_k, seeds, offsets)
+        nat = native()
+        ws = torch.empty(nat.sample_workspace_floats(logits.shape[0]), dtype=torch.float32, device=logits.device)
+        nat.sample(out, logits, temperature, top_p, top_k, seeds, offsets, ws)
         return out
     return ref.sample(logits, temperature, top_p, top_k, seeds, offsets)

@@ -130,6 +130,30 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return out
 
 
+def fold_gamma(W, gamma=None):
+    """W * gamma[None, :] rounded to W's dtype (the RMSNorm weight folded into the next linear)."""
+    if gamma is None:
+        return W.clone()
+    return (W.float() * gamma.float()[None, :]).to(W.dtype)
+
+
+def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5):
+    """Semantics of csrc/gemm_skinny.hip on the (gamma-folded, row-major) weight ``Wf``:
+    y = rsqrt(mean(x^2) + eps)[:, None] * (x @ Wf^T) for the NORM prologue."""
+    M, K = x.shape
+    xf = x.float()
+    y = xf @ Wf.float().t()
+    if pro == 1:
+        y = y * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    if epi == 2:
+        n = Wf.shape[0] // 2
+        return (torch.nn.functional.silu(y[:, :n]) * y[:, n:]).to(x.dtype)
+    if epi == 1:
+        res.copy_((y + res.float()).to(res.dtype))
+        return None
+    return y.to(x.dtype)
+
+
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
     d = x.shape[-1] // 2
     xf = x.float()
