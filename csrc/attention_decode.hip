@@ -15,7 +15,7 @@
 // Decode is HBM-bound: K/V go straight to VGPRs (cdna_hip_programming App. B "Attention
 // decode") with the next tile's loads in flight while the current tile computes;
 // LDS is used to merge the 4 waves' partial softmax states. Long contexts split the key
-// range over workgroups; `paged_decode_reduce` merges the splits.
+// range over workgroups; the last split to finish merges them (no second launch).
 #include "common.h"
 
 namespace {
@@ -54,8 +54,8 @@ template <int D>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, int max_blocks, float scale_log2,
-    int num_splits) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int Hq, int Hkv,
+    int max_blocks, float scale_log2, int num_splits) {
   __shared__ float s_m[NW][16];
   __shared__ float s_l[NW][16];
   __shared__ float s_o[NW][16][D + 4];
@@ -198,56 +198,95 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     if (num_splits == 1) {
       out[((size_t)b * Hq + head) * D + d] = rt::f2bf(L > 0.f ? O / L : 0.f);
     } else {
+      // agent-scope relaxed atomic stores = write-through past this XCD's L2 (sc1), so the
+      // combining workgroup, possibly on another XCD, reads them without any L2 writeback
       const size_t pi = ((size_t)b * Hq + head) * num_splits + split;
-      part_o[pi * D + d] = O;
+      __hip_atomic_store(part_o + pi * D + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d == 0) {
-        part_ml[pi * 2] = M;
-        part_ml[pi * 2 + 1] = L;
+        __hip_atomic_store(part_ml + pi * 2, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part_ml + pi * 2 + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+  }
+  if (num_splits == 1) return;
+  // ---- split-KV combine inside the launch: the last-arriving split of (b, hk) merges all
+  // splits and re-arms the counter to 0 for the next launch (hipGraph replays need no memset
+  // node). Protocol: every partial is an agent-scope atomic (sc1) store, each thread drains
+  // its stores (vmcnt(0)) before the barrier, then one lane bumps the arrival counter; the
+  // last arriver reads the partials with agent-scope atomic (sc1, L2-bypassing) loads.
+  // A release/acquire fence pair would emit buffer_wbl2/buffer_inv of the whole L2 per
+  // workgroup (measured: 2x slower kernel), which this avoids.
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == num_splits - 1;
+    if (s_last) __hip_atomic_store(counters + bh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // Combine. Latency-bound (a few KB of L2-bypassing loads), so every load is issued
+  // before any is consumed: (m, l) of all (head, split) pairs by distinct threads, then
+  // per-split weights through LDS, then 8 independent part_o loads in flight per thread.
+  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  constexpr int MAXS = 64;
+  __shared__ float s_w[16][MAXS];   // per (head, split) weight exp2(m_s - M) / L
+  const size_t bh_q0 = (size_t)b * Hq + hk * G;
+  for (int i = threadIdx.x; i < G * num_splits; i += blockDim.x) {
+    const int qi = i / num_splits, s2 = i - qi * num_splits;
+    const float* ml = part_ml + ((bh_q0 + qi) * num_splits + s2) * 2;
+    const float m = ld(ml), l = ld(ml + 1);
+    s_w[qi][s2] = l > 0.f ? m : -INFINITY;
+    s_o[0][qi][s2] = l;  // reuse the (now idle) merge buffer for l
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    const int qi = threadIdx.x;
+    float M = -INFINITY;
+    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, s_w[qi][s2]);
+    float L = 0.f;
+    for (int s2 = 0; s2 < num_splits; ++s2) {
+      const float f = (M == -INFINITY || s_w[qi][s2] == -INFINITY) ? 0.f : exp2f(s_w[qi][s2] - M);
+      s_w[qi][s2] = f;
+      L += f * s_o[0][qi][s2];
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    for (int s2 = 0; s2 < num_splits; ++s2) s_w[qi][s2] *= inv;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
+    const int qi = idx / D, d = idx - qi * D;
+    const float* po = part_o + (bh_q0 + qi) * num_splits * D + d;
+    float O = 0.f;
+    for (int s0 = 0; s0 < num_splits; s0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (s0 + j < num_splits) ? ld(po + (size_t)(s0 + j) * D) : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s0 + j < num_splits) O = fmaf(s_w[qi][s0 + j], v[j], O);
+    }
+    out[(bh_q0 + qi) * D + d] = rt::f2bf(O);
   }
 }
 
-template <int D>
-__global__ void __launch_bounds__(D) paged_decode_reduce(uint16_t* __restrict__ out, const float* __restrict__ part_o,
-                                                         const float* __restrict__ part_ml, int num_splits) {
-  const int bh = blockIdx.x;  // b * Hq + head
-  const int d = threadIdx.x;
-  const float* ml = part_ml + (size_t)bh * num_splits * 2;
-  float M = -INFINITY;
-  for (int s = 0; s < num_splits; ++s)
-    if (ml[2 * s + 1] > 0.f) M = fmaxf(M, ml[2 * s]);
-  float L = 0.f, O = 0.f;
-  if (M != -INFINITY) {
-    for (int s = 0; s < num_splits; ++s) {
-      const float l = ml[2 * s + 1];
-      if (l > 0.f) {
-        const float f = exp2f(ml[2 * s] - M);
-        L += f * l;
-        O += f * part_o[((size_t)bh * num_splits + s) * D + d];
-      }
-    }
-  }
-  out[(size_t)bh * D + d] = rt::f2bf(L > 0.f ? O / L : 0.f);
-}
 }  // namespace
 
 // q [B, Hq, D]; k_cache [NB, Hkv, 32, D]; v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32.
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
-                        const int* ctx_lens, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D,
-                        int max_blocks, float scale, int num_splits, hipStream_t stream) {
+                        const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
+                        int D, int max_blocks, float scale, int num_splits, hipStream_t stream) {
   if (B == 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16) return -1;
   if (num_splits < 1) num_splits = 1;
+  if (num_splits > 64 || (num_splits > 1 && num_splits > D + 4)) return -3;  // combine staging limits
   dim3 grid(B * Hkv, num_splits), block(256);
   const float sl2 = scale * LOG2E;
 #define RT_DEC(DD)                                                                                               \
   hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)q,      \
                      (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, part_o, part_ml, \
-                     Hq, Hkv, max_blocks, sl2, num_splits);                                                      \
-  if (num_splits > 1)                                                                                            \
-    hipLaunchKernelGGL((paged_decode_reduce<DD>), dim3(B * Hq), dim3(DD), 0, stream, (uint16_t*)out, part_o,     \
-                       part_ml, num_splits);
+                     counters, Hq, Hkv, max_blocks, sl2, num_splits);
   if (D == 128) {
     RT_DEC(128)
   } else if (D == 64) {

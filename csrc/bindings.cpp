@@ -14,8 +14,8 @@ void launch_rope_cache(void* q_out, const void* qkv, const int64_t* positions, c
 void launch_silu_mul(void* out, const void* x, int rows, int I, hipStream_t stream);
 void launch_gelu(void* out, const void* x, int64_t n, hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
-                        const int* ctx_lens, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D,
-                        int max_blocks, float scale, int num_splits, hipStream_t stream);
+                        const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
+                        int D, int max_blocks, float scale, int num_splits, hipStream_t stream);
 int prefill_rows_per_tile(int G);
 int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                    const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv, int D,
@@ -26,8 +26,12 @@ int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, 
 int sample_workspace_floats(int B);
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, hipStream_t stream);
-int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, hipStream_t stream);
+                       int pro, int epi, const void* rope, hipStream_t stream);
+int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
+                            const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
+                            const int64_t* slots, int Hq, int Hkv, int D, int BS, hipStream_t stream);
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
+                          hipStream_t stream);
 
 
 namespace {
@@ -116,7 +120,7 @@ void rope_and_cache(torch::Tensor q_out, torch::Tensor qkv, torch::Tensor positi
 
 void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
                             torch::Tensor block_tables, torch::Tensor ctx_lens, double scale, int64_t num_splits,
-                            torch::Tensor part_o, torch::Tensor part_ml) {
+                            torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor counters) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
@@ -130,9 +134,12 @@ void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_
   check_type(part_ml, torch::kFloat32, "partial_ml");
   TORCH_CHECK(num_splits >= 1 && part_o.numel() >= B * Hq * num_splits * D && part_ml.numel() >= B * Hq * num_splits * 2,
               "split workspace too small");
+  check_type(counters, torch::kInt32, "counters");
+  TORCH_CHECK(counters.numel() >= B * k_cache.size(1), "split counters too small");
   const int rc = launch_paged_decode(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                      block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), part_o.data_ptr<float>(),
-                                     part_ml.data_ptr<float>(), (int)B, (int)Hq, (int)k_cache.size(1), (int)D,
+                                     part_ml.data_ptr<float>(), counters.data_ptr<int>(), (int)B, (int)Hq,
+                                     (int)k_cache.size(1), (int)D,
                                      (int)block_tables.size(1), (float)scale, (int)num_splits, cur_stream());
   TORCH_CHECK(rc == 0, "paged_attention_decode: unsupported configuration (rc=", rc, ")");
 }
@@ -223,11 +230,37 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
     ldo = out.stride(0);
   }
   const int rc = launch_skinny_gemm(epi == 1 ? nullptr : out.data_ptr(), x.data_ptr(), Ws.data_ptr(), rp, (int)M,
-                                    (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, cur_stream());
+                                    (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "skinny_gemm: unsupported configuration (rc=", rc, ")");
 }
 
-void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tensor> gamma) {
+// qkv decode projection with the RoPE + paged-cache epilogue (Ws built with rope_heads = Hq + Hkv).
+void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, int64_t pro, torch::Tensor positions,
+                      torch::Tensor cos_sin, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots,
+                      int64_t Hq, int64_t Hkv, int64_t D, double eps) {
+  check_bf16(q_out, "q_out");
+  check_bf16(x, "x");
+  check_bf16(Ws, "Ws");
+  TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm_rope: x [M,K], Ws [N,K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16 && K % 32 == 0, "skinny_gemm_rope: 1 <= M <= 16, K % 32 == 0");
+  TORCH_CHECK(Ws.size(0) == (Hq + 2 * Hkv) * D && D % 16 == 0, "skinny_gemm_rope: Ws must be [(Hq+2Hkv)*D, K]");
+  TORCH_CHECK(q_out.numel() == M * Hq * D, "q_out must be [M, Hq, D]");
+  check_type(positions, torch::kInt64, "positions");
+  check_type(slots, torch::kInt64, "slots");
+  check_type(cos_sin, torch::kFloat32, "cos_sin");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "positions/slots must cover M rows");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  check_caches(k_cache, v_cache, Hkv, D);
+  const int rc = launch_skinny_gemm_rope(q_out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)M, (int)K, (int)pro,
+                                         (float)eps, positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                                         k_cache.data_ptr(), v_cache.data_ptr(), slots.data_ptr<int64_t>(), (int)Hq,
+                                         (int)Hkv, (int)D, (int)k_cache.size(2), cur_stream());
+  TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
+}
+
+void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tensor> gamma, int64_t rope_heads,
+                    int64_t head_dim) {
   check_bf16(Ws, "Ws");
   check_bf16(W, "W");
   TORCH_CHECK(W.dim() == 2 && Ws.sizes() == W.sizes(), "shuffle_weight shapes");
@@ -238,7 +271,9 @@ void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tens
     TORCH_CHECK(gamma->numel() == W.size(1), "gamma must have K elements");
     gp = gamma->data_ptr();
   }
-  launch_shuffle_weight(Ws.data_ptr(), W.data_ptr(), gp, (int)W.size(0), (int)W.size(1), cur_stream());
+  const int rc = launch_shuffle_weight(Ws.data_ptr(), W.data_ptr(), gp, (int)W.size(0), (int)W.size(1),
+                                       (int)(rope_heads * head_dim), (int)head_dim, cur_stream());
+  TORCH_CHECK(rc == 0, "shuffle_weight: unsupported configuration (rc=", rc, ")");
 }
 }  // namespace
 
@@ -246,7 +281,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm, "decode GEMM (M<=16), shuffled weights, fused norm / resid / swiglu",
         py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("epi"), py::arg("res") = py::none(),
         py::arg("eps") = 1e-5);
-  m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none());
+  m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
+        py::arg("rope_heads") = 0, py::arg("head_dim") = 0);
+  m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write");
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);

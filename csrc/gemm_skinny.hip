@@ -22,6 +22,12 @@
 //                   (no extra pass, no atomics: deterministic).
 //   epilogue RESID: res[m,n] = bf16(acc + res[m,n])   (the residual add, in place)
 //   epilogue SWIGLU: out[m,n] = silu(acc_gate) * acc_up,  W = [gate(I) ; up(I)]
+//   epilogue ROPE  : the qkv projection. Its q/k weight rows are stored pair-interleaved per
+//                   head (row 2i <- d=i, row 2i+1 <- d=i+D/2; `shuffle_weight(rope_heads=)`),
+//                   so both halves of every rotate-half pair land in the same 16-column tile:
+//                   the epilogue rotates them (fp32 cos|sin table), writes q to [M, Hq, D] and
+//                   scatters k / v straight into the paged caches (k [blk][h][off][D], v
+//                   transposed [blk][h][D][off]). Replaces the K2 rope/cache launch.
 #include "common.h"
 
 namespace {
@@ -32,7 +38,16 @@ using rt::short8;
 constexpr int U = 4;  // k-steps per wave per pipeline stage (x2 stages in flight)
 
 enum : int { PRO_PLAIN = 0, PRO_NORM = 1 };
-enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2 };
+enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_ROPE = 3 };
+
+struct RopeEpi {
+  const int64_t* positions;  // [M]
+  const float* cos_sin;      // [max_pos][D]: cos(D/2) | sin(D/2)
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  const int64_t* slots;      // [M]
+  int Hq, Hkv, D, BS;
+};
 
 RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -43,12 +58,12 @@ struct Stage {
   short8 a[U];
 };
 
-template <int EPI>
+template <int EPI, int NW>
 RT_DEVICE void issue(Stage<EPI>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2,
                      const uint16_t* __restrict__ xr, bool row_ok, int s0, int nsteps, int lane) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int s = s0 + 4 * u;
+    const int s = s0 + NW * u;
     if (s < nsteps) {
       st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * 64 + lane);
       if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt2 + (size_t)s * 64 + lane);
@@ -56,16 +71,16 @@ RT_DEVICE void issue(Stage<EPI>& st, const short8* __restrict__ wt, const short8
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int s = s0 + 4 * u;
+    const int s = s0 + NW * u;
     st.a[u] = (row_ok && s < nsteps) ? *reinterpret_cast<const short8*>(xr + s * 32) : short8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 }
 
-template <int PRO, int EPI>
+template <int PRO, int EPI, int NW>
 RT_DEVICE void consume(const Stage<EPI>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (s0 + 4 * u < nsteps) {
+    if (s0 + NW * u < nsteps) {
       const bf16x8 a = __builtin_bit_cast(bf16x8, st.a[u]);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u]), acc, 0, 0, 0);
       if constexpr (EPI == EPI_SWIGLU)
@@ -81,12 +96,12 @@ RT_DEVICE void consume(const Stage<EPI>& st, float4_& acc, float4_& acc2, float&
   }
 }
 
-template <int PRO, int EPI>
-__global__ void __launch_bounds__(256) skinny_gemm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
+template <int PRO, int EPI, int NW>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
                                                           const short8* __restrict__ Ws, uint16_t* __restrict__ res,
-                                                          int M, int N, int K, int ldo, float eps) {
-  __shared__ float red[4][(EPI == EPI_SWIGLU) ? 2 : 1][16][17];
-  __shared__ float sq[4][16];
+                                                          int M, int N, int K, int ldo, float eps, RopeEpi re) {
+  __shared__ float red[NW][(EPI == EPI_SWIGLU) ? 2 : 1][16][17];
+  __shared__ float sq[NW][16];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int tile = blockIdx.x;
@@ -100,16 +115,16 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(uint16_t* __restrict__
   float ssq = 0.f;
   Stage<EPI> st0, st1;
   int s = wid;
-  issue<EPI>(st0, wt, wt2, xr, row_ok, s, nsteps, lane);
+  issue<EPI, NW>(st0, wt, wt2, xr, row_ok, s, nsteps, lane);
   for (;;) {
-    const int sn = s + 4 * U;
-    if (sn < nsteps) issue<EPI>(st1, wt, wt2, xr, row_ok, sn, nsteps, lane);
-    consume<PRO, EPI>(st0, acc, acc2, ssq, s, nsteps);
+    const int sn = s + NW * U;
+    if (sn < nsteps) issue<EPI, NW>(st1, wt, wt2, xr, row_ok, sn, nsteps, lane);
+    consume<PRO, EPI, NW>(st0, acc, acc2, ssq, s, nsteps);
     if (sn >= nsteps) break;
     s = sn;
-    const int sn2 = s + 4 * U;
-    if (sn2 < nsteps) issue<EPI>(st0, wt, wt2, xr, row_ok, sn2, nsteps, lane);
-    consume<PRO, EPI>(st1, acc, acc2, ssq, s, nsteps);
+    const int sn2 = s + NW * U;
+    if (sn2 < nsteps) issue<EPI, NW>(st0, wt, wt2, xr, row_ok, sn2, nsteps, lane);
+    consume<PRO, EPI, NW>(st1, acc, acc2, ssq, s, nsteps);
     if (sn2 >= nsteps) break;
     s = sn2;
   }
@@ -127,19 +142,51 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(uint16_t* __restrict__
   }
   __syncthreads();
   const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
-  if (m < M) {
-    float v = red[0][0][m][n] + red[1][0][m][n] + red[2][0][m][n] + red[3][0][m][n];
+  if (threadIdx.x < 256 && m < M) {
+    float v = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      v += red[w][0][m][n];
+      if constexpr (PRO == PRO_NORM) ss += sq[w][m];
+    }
     float inv = 1.f;
-    if constexpr (PRO == PRO_NORM) inv = rsqrtf((sq[0][m] + sq[1][m] + sq[2][m] + sq[3][m]) / (float)K + eps);
+    if constexpr (PRO == PRO_NORM) inv = rsqrtf(ss / (float)K + eps);
     v *= inv;
     const int col = tile * 16 + n;
     if constexpr (EPI == EPI_SWIGLU) {
       const int u1 = (EPI == EPI_SWIGLU) ? 1 : 0;
-      const float up = (red[0][u1][m][n] + red[1][u1][m][n] + red[2][u1][m][n] + red[3][u1][m][n]) * inv;
+      float up = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) up += red[w][u1][m][n];
+      up *= inv;
       out[(size_t)m * ldo + col] = rt::f2bf(silu(v) * up);
     } else if constexpr (EPI == EPI_RESID) {
       uint16_t* rp = res + (size_t)m * N + col;
       *rp = rt::f2bf(v + rt::bf2f(*rp));
+    } else if constexpr (EPI == EPI_ROPE) {
+      const int D = re.D, half = D >> 1;
+      const int h = col / D, p = col - h * D;
+      const int64_t slot = re.slots[m];
+      const int64_t blk = slot / re.BS;
+      const int off = (int)(slot - blk * re.BS);
+      if (h < re.Hq + re.Hkv) {
+        float partner = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) partner += red[w][0][m][n ^ 1];
+        partner *= inv;
+        const int i = p >> 1, hi = p & 1;
+        const float* cs = re.cos_sin + (size_t)re.positions[m] * D;
+        const float c = cs[i], sn = cs[half + i];
+        // pair (x1 = d i, x2 = d i+D/2): y1 = x1 c - x2 s ; y2 = x2 c + x1 s
+        const float y = hi ? fmaf(v, c, partner * sn) : fmaf(v, c, -partner * sn);
+        const int d = i + hi * half;
+        uint16_t* dst = (h < re.Hq) ? out + ((size_t)m * re.Hq + h) * D + d
+                                    : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
+        *dst = rt::f2bf(y);
+      } else {
+        const int hv = h - re.Hq - re.Hkv;
+        re.v_cache[(((size_t)blk * re.Hkv + hv) * D + p) * re.BS + off] = rt::f2bf(v);
+      }
     } else {
       out[(size_t)m * ldo + col] = rt::f2bf(v);
     }
@@ -147,8 +194,10 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(uint16_t* __restrict__
 }
 
 // Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j] (optionally W * gamma[k] folded in)
+// If rope_rows > 0, output row r < rope_rows takes source row h*D + (p>>1) + (p&1)*D/2
+// (r = h*D + p): the pair-interleaved q/k order the ROPE epilogue expects.
 __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restrict__ W,
-                               const uint16_t* __restrict__ gamma, int N, int K) {
+                               const uint16_t* __restrict__ gamma, int N, int K, int rope_rows, int D) {
   const int nsteps = K / 32;
   const int64_t total = (int64_t)(N / 16) * nsteps * 64;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -156,7 +205,11 @@ __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restri
     const int64_t ts = i >> 6;
     const int s = (int)(ts % nsteps);
     const int64_t t = ts / nsteps;
-    const int row = (int)(16 * t + (l & 15));
+    int row = (int)(16 * t + (l & 15));
+    if (row < rope_rows) {
+      const int h = row / D, p = row - h * D;
+      row = h * D + (p >> 1) + (p & 1) * (D >> 1);
+    }
     const int k0 = 32 * s + 8 * (l >> 4);
     short8 v = *reinterpret_cast<const short8*>(W + (size_t)row * K + k0);
     if (gamma != nullptr) {
@@ -170,28 +223,53 @@ __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restri
 }  // namespace
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, hipStream_t stream) {
+                       int pro, int epi, const void* rope, hipStream_t stream) {
   if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
-  dim3 grid(N / 16), block(256);
-#define RT_SG(P, E)                                                                                                \
-  hipLaunchKernelGGL((skinny_gemm_kernel<P, E>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)x,       \
-                     (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps)
+  RopeEpi re{};
+  if (epi == EPI_ROPE) {
+    if (rope == nullptr) return -3;
+    re = *static_cast<const RopeEpi*>(rope);
+    if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
+  }
+  // few column tiles (o/down/qkv projections: <= 1 workgroup per CU) -> 8 waves per workgroup
+  // so each CU keeps 64 KB of weight loads in flight; wide GEMMs (gate_up, lm_head) -> 4.
+  const bool wide = (N / 16) >= 768;
+  dim3 grid(N / 16);
+#define RT_SG(P, E)                                                                                                 \
+  do {                                                                                                              \
+    if (wide)                                                                                                       \
+      hipLaunchKernelGGL((skinny_gemm_kernel<P, E, 4>), grid, dim3(256), 0, stream, (uint16_t*)out,                \
+                         (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re);             \
+    else                                                                                                            \
+      hipLaunchKernelGGL((skinny_gemm_kernel<P, E, 8>), grid, dim3(512), 0, stream, (uint16_t*)out,                \
+                         (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re);             \
+  } while (0)
   if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SG(PRO_PLAIN, EPI_STORE);
   else if (pro == PRO_NORM && epi == EPI_STORE) RT_SG(PRO_NORM, EPI_STORE);
   else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_SG(PRO_PLAIN, EPI_RESID);
   else if (pro == PRO_NORM && epi == EPI_SWIGLU) RT_SG(PRO_NORM, EPI_SWIGLU);
   else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_SG(PRO_PLAIN, EPI_SWIGLU);
+  else if (pro == PRO_NORM && epi == EPI_ROPE) RT_SG(PRO_NORM, EPI_ROPE);
+  else if (pro == PRO_PLAIN && epi == EPI_ROPE) RT_SG(PRO_PLAIN, EPI_ROPE);
   else return -2;
 #undef RT_SG
   return 0;
 }
 
-int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, hipStream_t stream) {
-  if (K % 32 || N % 16) return -1;
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
+                          hipStream_t stream) {
+  if (K % 32 || N % 16 || rope_rows > N || (rope_rows > 0 && (D <= 0 || D % 2 || rope_rows % D))) return -1;
   const int64_t total = (int64_t)N * K / 8;
   int64_t grid = (total + 255) / 256;
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(shuffle_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (short8*)Ws, (const uint16_t*)W,
-                     (const uint16_t*)gamma, N, K);
+                     (const uint16_t*)gamma, N, K, rope_rows, D);
   return 0;
+}
+
+int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
+                            const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
+                            const int64_t* slots, int Hq, int Hkv, int D, int BS, hipStream_t stream) {
+  const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS};
+  return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, stream);
 }

@@ -86,3 +86,33 @@ def test_fused_decode_is_deterministic():
         e = Engine(EngineConfig(model="tiny-llama-128", weights="random:5", device=DEV, num_blocks=64))
         outs.append([t.ids for t in e.run_turns([Turn("a", "determinisme", sp), Turn("b", "nog een", sp)])])
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("M,hq,hkv,d", [(1, 32, 8, 128), (3, 32, 8, 128), (16, 12, 4, 64), (5, 8, 8, 128)])
+def test_skinny_gemm_rope_epilogue(M, hq, hkv, d):
+    """qkv GEMM + RMSNorm + RoPE + paged K/V scatter in one kernel == fp32 GEMM -> K2 reference."""
+    K = 512
+    N = (hq + 2 * hkv) * d
+    x = bf(M, K, seed=61)
+    W = bf(N, K, scale=0.05, seed=62)
+    gam = bf(K, seed=63)
+    cos_sin = ref.rope_cos_sin(4096, d, 500000.0, DEV)
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int64)
+    nb = 8
+    slots = torch.randperm(nb * 32, device=DEV)[:M].to(torch.int64)
+    kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+    kc_r, vc_r = kc.cpu().clone(), vc.cpu().clone()
+    Ws = ops.shuffle_weight(W, gam, rope_heads=hq + hkv, head_dim=d)
+    q = ops.skinny_gemm_rope(x, Ws, ops.PRO_NORM, positions, cos_sin, kc, vc, slots, hq, hkv, d, 1e-5)
+    Wp = ref.fold_gamma(W.cpu(), gam.cpu(), hq + hkv, d)
+    q_r = ref.skinny_gemm_rope(x.cpu(), Wp, 1, positions.cpu(), cos_sin.cpu(), kc_r, vc_r, slots.cpu(), hq, hkv, d,
+                               1e-5)
+    close(q, q_r.to(DEV), 0.05, 0.02)
+    close(kc, kc_r.to(DEV), 0.05, 0.02)
+    close(vc, vc_r.to(DEV), 0.05, 0.02)
+    # the permuted reference equals the plain (unpermuted) path: GEMM -> rope_and_cache
+    kc2, vc2 = torch.zeros_like(kc_r), torch.zeros_like(vc_r)
+    qkv = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W.cpu(), gam.cpu()), 1, eps=1e-5)
+    q2 = ref.rope_and_cache(qkv, positions.cpu(), cos_sin.cpu(), kc2, vc2, slots.cpu(), hq, hkv, d)
+    close(q_r, q2, 0.05, 0.02)

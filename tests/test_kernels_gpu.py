@@ -101,6 +101,11 @@ def test_paged_decode(hq, hkv, d, splits):
     out = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws)
     exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, cl, scale)
     close(out, exp.to(DEV), 0.02, 0.02)
+    # the in-kernel split combine re-arms its arrival counters: a second launch on the same
+    # workspace must reproduce the first bit for bit
+    out2 = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws)
+    assert torch.equal(out, out2)
+    assert int(ws.counters.abs().sum()) == 0
 
 
 def test_paged_decode_spike():

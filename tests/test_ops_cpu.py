@@ -1,0 +1,55 @@
+"""CPU checks of the op reference semantics the HIP kernels are tested against.
+
+The fused decode kernels (csrc/gemm_skinny.hip) work on re-laid-out weights; these tests
+pin that the re-layouts are semantic no-ops, so the GPU tests' fp32 oracle is the model.
+"""
+import torch
+
+from theroundtaible_amd import ops
+from theroundtaible_amd.ops import reference as ref
+
+
+def test_rope_row_perm_is_pair_interleave():
+    p = ref.rope_row_perm(3 * 8 + 4, 3, 8)
+    assert p[:8].tolist() == [0, 4, 1, 5, 2, 6, 3, 7]
+    assert p[8:16].tolist() == [8, 12, 9, 13, 10, 14, 11, 15]
+    assert p[24:].tolist() == [24, 25, 26, 27]
+    assert sorted(p.tolist()) == list(range(28))
+
+
+def test_skinny_gemm_rope_reference_matches_unfused():
+    torch.manual_seed(0)
+    M, hq, hkv, d, K = 3, 8, 2, 64, 128
+    N = (hq + 2 * hkv) * d
+    x = torch.randn(M, K).bfloat16()
+    W = (torch.randn(N, K) * 0.05).bfloat16()
+    g = torch.randn(K).bfloat16()
+    cs = ref.rope_cos_sin(256, d, 10000.0)
+    pos = torch.tensor([5, 100, 200])
+    slots = torch.tensor([3, 40, 77])
+    kc = torch.zeros(4, hkv, 32, d).bfloat16()
+    vc = torch.zeros(4, hkv, d, 32).bfloat16()
+    Wp = ops.shuffle_weight(W, g, rope_heads=hq + hkv, head_dim=d)
+    q = ops.skinny_gemm_rope(x, Wp, ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    qkv = ref.skinny_gemm(x, ref.fold_gamma(W, g), ops.PRO_NORM)
+    q2 = ref.rope_and_cache(qkv, pos, cs, kc2, vc2, slots, hq, hkv, d)
+    assert (q.float() - q2.float()).abs().max() < 0.02
+    assert (kc.float() - kc2.float()).abs().max() < 0.02
+    assert torch.equal(vc, vc2)
+
+
+def test_skinny_gemm_norm_prologue_equals_rmsnorm_then_linear():
+    torch.manual_seed(1)
+    x = torch.randn(4, 256).bfloat16()
+    W = (torch.randn(64, 256) * 0.05).bfloat16()
+    g = torch.randn(256).bfloat16()
+    fused = ref.skinny_gemm(x, ref.fold_gamma(W, g), ops.PRO_NORM, eps=1e-5).float()
+    plain = ref.rms_norm(x, g, 1e-5).float() @ W.float().t()
+    assert (fused - plain).abs().max() < 0.05
+
+
+def test_decode_splits_bounds():
+    assert ops.decode_splits(1, 8) == 32
+    assert ops.decode_splits(16, 8) == 4
+    assert ops.decode_splits(64, 8) == 1

@@ -85,7 +85,9 @@ class LlamaModel:
                 layers = []
                 for lw in self.layers:
                     layers.append({
-                        "wqkv": ops.shuffle_weight(lw["wqkv"], lw["attn_norm"]),
+                        "wqkv": ops.shuffle_weight(lw["wqkv"], lw["attn_norm"],
+                                                   rope_heads=self.n_heads + self.n_kv_heads,
+                                                   head_dim=self.head_dim),
                         "wo": ops.shuffle_weight(lw["wo"]),
                         "w_gate_up": ops.shuffle_weight(lw["w_gate_up"], lw["ffn_norm"]),
                         "w_down": ops.shuffle_weight(lw["w_down"]),
@@ -95,17 +97,18 @@ class LlamaModel:
 
     def forward_decode_fused(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta) -> torch.Tensor:
         """Decode step with every norm / residual / activation fused into the MFMA GEMMs
-        (csrc/gemm_skinny.hip): per layer qkv(+RMSNorm) -> K2 -> K3 -> o(+residual) ->
-        gate_up(+RMSNorm, SwiGLU) -> down(+residual). 6 launches per layer, no norm kernels."""
+        (csrc/gemm_skinny.hip): per layer qkv(+RMSNorm, +RoPE/KV-cache write) -> K3 (split-KV
+        combined in-kernel) -> o(+residual) -> gate_up(+RMSNorm, SwiGLU) -> down(+residual).
+        5 launches per layer, no norm / rope / reduce kernels."""
         cfg = self.cfg
         eps = cfg.norm_eps
         dec = self.decode_weights()
         res = F.embedding(ids, self.w["embed"]).contiguous()
         B = ids.shape[0]
         for l, lw in enumerate(dec["layers"]):
-            qkv = ops.skinny_gemm(res, lw["wqkv"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
-            q = ops.rope_and_cache(qkv, positions, self.cos_sin, kv.k_layer(l), kv.v_layer(l), meta.slot_mapping,
-                                   self.n_heads, self.n_kv_heads, self.head_dim)
+            q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kv.k_layer(l),
+                                     kv.v_layer(l), meta.slot_mapping, self.n_heads, self.n_kv_heads,
+                                     self.head_dim, eps)
             a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)
             ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
             g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps)

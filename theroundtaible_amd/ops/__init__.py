@@ -102,6 +102,9 @@ class DecodeWorkspace:
         self.max_splits = max_splits
         self.partial_o = torch.empty(max_batch * n_heads * max_splits * head_dim, dtype=torch.float32, device=device)
         self.partial_ml = torch.empty(max_batch * n_heads * max_splits * 2, dtype=torch.float32, device=device)
+        # per-(sequence, kv head) split arrival counters; the kernel re-arms them to 0 itself.
+        # Sized by n_heads (>= n_kv_heads) so one workspace serves every GQA ratio.
+        self.counters = torch.zeros(max_batch * n_heads, dtype=torch.int32, device=device)
 
 
 def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 32) -> int:
@@ -124,7 +127,8 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
         if workspace is None:
             workspace = DecodeWorkspace(q.shape[0], q.shape[1], q.shape[2], max(1, num_splits), q.device)
         native().paged_attention_decode(out, q, k_cache, v_cache, block_tables, ctx_lens, scale,
-                                        int(num_splits), workspace.partial_o, workspace.partial_ml)
+                                        int(num_splits), workspace.partial_o, workspace.partial_ml,
+                                        workspace.counters)
         return out
     return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
 
@@ -154,17 +158,20 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
 
 
 PRO_PLAIN, PRO_NORM = 0, 1
-EPI_STORE, EPI_RESID, EPI_SWIGLU = 0, 1, 2
+EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
 
 
-def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None) -> torch.Tensor:
+def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None, rope_heads: int = 0,
+                   head_dim: int = 0) -> torch.Tensor:
     """Decode-weight copy in the MFMA fragment order of csrc/gemm_skinny.hip, with an RMSNorm
-    weight ``gamma`` (over K) optionally folded in. On CPU: the row-major ``W * gamma``."""
+    weight ``gamma`` (over K) optionally folded in and, for a qkv weight used with
+    :func:`skinny_gemm_rope`, the first ``rope_heads`` heads' rows pair-interleaved.
+    On CPU: the row-major ``W * gamma`` (rows permuted the same way)."""
     if _use_native(W):
         Ws = torch.empty_like(W)
-        native().shuffle_weight(Ws, W.contiguous(), gamma)
+        native().shuffle_weight(Ws, W.contiguous(), gamma, int(rope_heads), int(head_dim))
         return Ws
-    return ref.fold_gamma(W, gamma)
+    return ref.fold_gamma(W, gamma, rope_heads, head_dim)
 
 
 def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: int = EPI_STORE,
@@ -177,6 +184,21 @@ def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: in
         native().skinny_gemm(out, x, Ws, pro, epi, res, eps)
         return None if epi == EPI_RESID else out
     return ref.skinny_gemm(x, Ws, pro, epi, res, eps)
+
+
+def skinny_gemm_rope(x: torch.Tensor, Ws: torch.Tensor, pro: int, positions: torch.Tensor, cos_sin: torch.Tensor,
+                     k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor, n_heads: int,
+                     n_kv_heads: int, head_dim: int, eps: float = 1e-5) -> torch.Tensor:
+    """Decode qkv projection (+ optional RMSNorm prologue) with RoPE and the paged K/V cache
+    write fused into the epilogue; returns q [M, n_heads, head_dim]. ``Ws`` must come from
+    ``shuffle_weight(Wqkv, gamma, rope_heads=n_heads + n_kv_heads, head_dim=head_dim)``."""
+    if _use_native(x):
+        q = torch.empty(x.shape[0], n_heads, head_dim, dtype=x.dtype, device=x.device)
+        native().skinny_gemm_rope(q, x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
+                                  head_dim, eps)
+        return q
+    return ref.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
+                                head_dim, eps)
 
 
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:

@@ -130,11 +130,24 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return out
 
 
-def fold_gamma(W, gamma=None):
-    """W * gamma[None, :] rounded to W's dtype (the RMSNorm weight folded into the next linear)."""
-    if gamma is None:
-        return W.clone()
-    return (W.float() * gamma.float()[None, :]).to(W.dtype)
+def rope_row_perm(n_rows: int, rope_heads: int, head_dim: int) -> torch.Tensor:
+    """Source row of every output row in the pair-interleaved q/k order of the ROPE epilogue:
+    row h*D + 2i <- h*D + i, row h*D + 2i + 1 <- h*D + i + D/2 (rows past the q/k heads: identity)."""
+    idx = torch.arange(n_rows)
+    r = rope_heads * head_dim
+    if r:
+        h, p = idx[:r] // head_dim, idx[:r] % head_dim
+        idx[:r] = h * head_dim + p // 2 + (p % 2) * (head_dim // 2)
+    return idx
+
+
+def fold_gamma(W, gamma=None, rope_heads: int = 0, head_dim: int = 0):
+    """W * gamma[None, :] rounded to W's dtype (the RMSNorm weight folded into the next linear),
+    rows optionally permuted for the ROPE epilogue (``rope_heads`` leading heads)."""
+    out = W.clone() if gamma is None else (W.float() * gamma.float()[None, :]).to(W.dtype)
+    if rope_heads:
+        out = out[rope_row_perm(W.shape[0], rope_heads, head_dim)].contiguous()
+    return out
 
 
 def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5):
@@ -151,7 +164,21 @@ def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5):
     if epi == 1:
         res.copy_((y + res.float()).to(res.dtype))
         return None
+    if epi == 3:
+        return y  # fp32 pre-rope projection (see skinny_gemm_rope)
     return y.to(x.dtype)
+
+
+def skinny_gemm_rope(x, Wp, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads, head_dim,
+                     eps=1e-5):
+    """ROPE-epilogue semantics: fp32 projection on the pair-permuted weight, columns restored
+    to natural order, then RoPE + paged K/V scatter with no bf16 rounding in between."""
+    y = skinny_gemm(x, Wp, pro, 3, None, eps)
+    perm = rope_row_perm(Wp.shape[0], n_heads + n_kv_heads, head_dim)
+    qkv = torch.empty_like(y)
+    qkv[:, perm] = y
+    q = rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads, head_dim)
+    return q.to(x.dtype)
 
 
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
