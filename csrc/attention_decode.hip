@@ -1,21 +1,24 @@
 // K3: paged-KV decode attention (one query token per sequence), GQA, MFMA bf16, split-KV.
 //
-// Grid (B * Hkv, num_splits), 256 threads = 4 waves. A workgroup owns one (sequence, kv
-// head, key range); its G = Hq/Hkv query heads share every K/V byte it loads (GQA
-// packing: the G queries are the 16 MFMA columns, G <= 16).
+// Grid (B * Hkv, num_splits), NW = 8 waves per workgroup. A workgroup owns one (sequence,
+// kv head, key range); its G = Hq/Hkv query heads share every K/V byte it loads (GQA
+// packing: the G queries are the 16 MFMA columns, G <= 16). The split count is chosen so the
+// grid is ~one 8-wave workgroup per CU (ops.decode_splits): decode attention is a pure
+// K/V stream, so what matters is bytes in flight per CU and few round trips per launch.
 //
 // Per 32-key tile (= one cache block, BS = 32) each wave computes
-//   S^T[32 keys x 16 q] = K . Q^T     4*(D/32)... 2 halves x D/32  mfma_f32_16x16x32_bf16
+//   S^T[32 keys x 16 q] = K . Q^T     2 halves x D/32  mfma_f32_16x16x32_bf16
 //   online softmax down each q column (in-register; 2 xor-shuffles per reduction)
 //   O[16 q x D]        += P . V       D/16 mfma_f32_16x16x32_bf16
-// The S^T accumulator of lane l already IS the A-operand fragment of P.V (keys permuted
-// consistently on both operands), so P never leaves registers. K rows are read as
-// 64 contiguous bytes per lane (d permuted consistently on K and Q); V is cached
-// transposed per block ([D][32]) so its B-fragments are two 8-byte contiguous loads.
-// Decode is HBM-bound: K/V go straight to VGPRs (cdna_hip_programming App. B "Attention
-// decode") with the next tile's loads in flight while the current tile computes;
-// LDS is used to merge the 4 waves' partial softmax states. Long contexts split the key
-// range over workgroups; the last split to finish merges them (no second launch).
+// K rows are fed to the MFMA in the order key(h, row) = 8*(row>>2) + 4h + (row&3), so lane
+// (r, g) of the S^T accumulator holds keys 8g..8g+7 of column r — exactly the A-operand
+// fragment of P.V (P never leaves registers) — and the matching B fragment of the
+// transposed value cache ([D][32] per block) is ONE 16-byte load per lane per d-chunk.
+// K rows are read as 64 contiguous bytes per lane (d permuted consistently on K and Q).
+// K/V go straight to VGPRs (cdna_hip_programming App. B "Attention decode") with the next
+// tile's loads in flight while the current tile computes. The 8 waves' softmax states
+// merge through LDS; the splits of one (sequence, kv head) are combined in the same launch
+// by whichever workgroup arrives last (sc1 write-through hand-off, see below).
 #include "common.h"
 
 namespace {
@@ -24,34 +27,32 @@ using rt::float4_;
 using rt::short8;
 
 constexpr int BS = 32;
-constexpr int NW = 4;
+constexpr int NW = 8;
+constexpr int MAXS = 64;  // max splits (combine staging)
 constexpr float LOG2E = 1.4426950408889634f;
 
 template <int D>
 struct Tile {
-  short8 k[2][D / 32];              // [half][chunk]: K rows 16h + r, d = (D/4)*g + 8c + j
-  uint2 v[D / 16][2];               // [d-chunk][key group]: 4 keys each
+  short8 k[2][D / 32];  // [half][chunk]: K row key(h, r), d = (D/4)*g + 8c + j
+  short8 v[D / 16];     // [d-chunk]: V[keys 8g..8g+7][d = 16e + r]
 };
 
 template <int D>
 RT_DEVICE void load_tile(Tile<D>& t, const uint16_t* __restrict__ kblk, const uint16_t* __restrict__ vblk, int r,
                          int g) {
+  const int krow = 8 * (r >> 2) + (r & 3);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const uint16_t* kr = kblk + (16 * h + r) * D + (D / 4) * g;
+    const uint16_t* kr = kblk + (krow + 4 * h) * D + (D / 4) * g;
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) t.k[h][c] = *reinterpret_cast<const short8*>(kr + 8 * c);
   }
 #pragma unroll
-  for (int e = 0; e < D / 16; ++e) {
-    const uint16_t* vr = vblk + (16 * e + r) * BS;
-    t.v[e][0] = *reinterpret_cast<const uint2*>(vr + 4 * g);
-    t.v[e][1] = *reinterpret_cast<const uint2*>(vr + 16 + 4 * g);
-  }
+  for (int e = 0; e < D / 16; ++e) t.v[e] = *reinterpret_cast<const short8*>(vblk + (16 * e + r) * BS + 8 * g);
 }
 
 template <int D>
-__global__ void __launch_bounds__(256) paged_decode_kernel(
+__global__ void __launch_bounds__(NW * 64) paged_decode_kernel(
     uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens,
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int Hq, int Hkv,
@@ -59,6 +60,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   __shared__ float s_m[NW][16];
   __shared__ float s_l[NW][16];
   __shared__ float s_o[NW][16][D + 4];
+  __shared__ float s_wt[16][MAXS];
+  __shared__ float s_lt[16][MAXS];
+  __shared__ int s_last;
 
   const int bh = blockIdx.x;
   const int b = bh / Hkv, hk = bh - (bh / Hkv) * Hkv;
@@ -88,8 +92,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   float4_ oacc[D / 16];
 #pragma unroll
   for (int e = 0; e < D / 16; ++e) oacc[e] = float4_{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY;   // running max (log2 domain) of column r
-  float lsum = 0.f;      // lane-partial running sum of column r
+  float m = -INFINITY;  // running max (log2 domain) of column r
+  float lsum = 0.f;     // lane-partial running sum of column r
 
   const int* bt = block_tables + (size_t)b * max_blocks;
   const size_t blk_stride = (size_t)Hkv * BS * D;
@@ -115,16 +119,15 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
         s[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur.k[h][c]),
                                                        __builtin_bit_cast(bf16x8, qf[c]), s[h], 0, 0, 0);
     }
-    // ---- online softmax down column r ----
-    const int key0 = t * BS;
+    // ---- online softmax down column r: lane holds keys 8g + 4h + i ----
+    const int key0 = t * BS + 8 * g;
     float tmax = -INFINITY;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int key = key0 + 16 * h + 4 * g + i;
         float v = s[h][i] * scale_log2;
-        v = key < ctx ? v : -INFINITY;
+        v = key0 + 4 * h + i < ctx ? v : -INFINITY;
         s[h][i] = v;
         tmax = fmaxf(tmax, v);
       }
@@ -154,13 +157,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       float4_ o = oacc[e];
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] *= al[i];
-      uint4 vb;
-      vb.x = cur.v[e][0].x;
-      vb.y = cur.v[e][0].y;
-      vb.z = cur.v[e][1].x;
-      vb.w = cur.v[e][1].y;
       oacc[e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pa),
-                                                        __builtin_bit_cast(bf16x8, vb), o, 0, 0, 0);
+                                                        __builtin_bit_cast(bf16x8, cur.v[e]), o, 0, 0, 0);
     }
     cur = nxt;
   }
@@ -168,7 +166,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
 
-  // ---- merge the 4 waves through LDS ----
+  // ---- merge the waves through LDS (only the G live query rows) ----
   if (g == 0) {
     s_m[wid][r] = m;
     s_l[wid][r] = lsum;
@@ -176,47 +174,50 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 #pragma unroll
   for (int e = 0; e < D / 16; ++e)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s_o[wid][4 * g + i][16 * e + r] = oacc[e][i];
+    for (int i = 0; i < 4; ++i)
+      if (4 * g + i < G) s_o[wid][4 * g + i][16 * e + r] = oacc[e][i];
   __syncthreads();
 
-  // G x D outputs, 256 threads
-  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
-    const int qi = idx / D, d = idx - qi * D;
+  const size_t bh_q0 = (size_t)b * Hq + hk * G;  // first query head of this workgroup
+  const auto po_rsrc = rt::buf_rsrc(part_o + bh_q0 * num_splits * D);
+  const auto pml_rsrc = rt::buf_rsrc(part_ml + bh_q0 * num_splits * 4);
+  for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
+    const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
     float M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][qi]);
-    float L = 0.f, O = 0.f;
+    float L = 0.f;
+    float4_ O = {0.f, 0.f, 0.f, 0.f};
     if (M != -INFINITY) {
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         const float f = exp2f(s_m[w][qi] - M);
         L += f * s_l[w][qi];
-        O += f * s_o[w][qi][d];
+        const float4_ ow = *reinterpret_cast<const float4_*>(&s_o[w][qi][d0]);
+        O += f * ow;
       }
     }
-    const int head = hk * G + qi;
     if (num_splits == 1) {
-      out[((size_t)b * Hq + head) * D + d] = rt::f2bf(L > 0.f ? O / L : 0.f);
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      uint2 pk;
+      pk.x = rt::pack2(O[0] * inv, O[1] * inv);
+      pk.y = rt::pack2(O[2] * inv, O[3] * inv);
+      *reinterpret_cast<uint2*>(out + (bh_q0 + qi) * D + d0) = pk;
     } else {
-      // agent-scope relaxed atomic stores = write-through past this XCD's L2 (sc1), so the
-      // combining workgroup, possibly on another XCD, reads them without any L2 writeback
-      const size_t pi = ((size_t)b * Hq + head) * num_splits + split;
-      __hip_atomic_store(part_o + pi * D + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == 0) {
-        __hip_atomic_store(part_ml + pi * 2, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(part_ml + pi * 2 + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      // partials leave as 16-B write-through (sc1) stores: the combining workgroup, possibly
+      // on another XCD, reads them with sc1 loads and no L2 writeback/invalidate is needed
+      rt::sc1_store4(po_rsrc, ((qi * num_splits + split) * D + d0) * 4, O);
+      if (d0 == 0) rt::sc1_store4(pml_rsrc, (qi * num_splits + split) * 16, float4_{M, L, 0.f, 0.f});
     }
   }
   if (num_splits == 1) return;
-  // ---- split-KV combine inside the launch: the last-arriving split of (b, hk) merges all
-  // splits and re-arms the counter to 0 for the next launch (hipGraph replays need no memset
-  // node). Protocol: every partial is an agent-scope atomic (sc1) store, each thread drains
-  // its stores (vmcnt(0)) before the barrier, then one lane bumps the arrival counter; the
-  // last arriver reads the partials with agent-scope atomic (sc1, L2-bypassing) loads.
-  // A release/acquire fence pair would emit buffer_wbl2/buffer_inv of the whole L2 per
-  // workgroup (measured: 2x slower kernel), which this avoids.
-  __shared__ int s_last;
+
+  // ---- split-KV combine inside the launch (MI355X_MICROARCH "Valid forms", row 1): every
+  // partial is stored sc1 and drained (vmcnt(0)) by each storing wave before the barrier;
+  // ONE lane then bumps the (sequence, kv head) arrival counter; the workgroup whose add
+  // returns num_splits-1 combines, reading every partial with sc1 loads, and re-arms the
+  // counter for the next launch (hipGraph replays need no memset node). A release/acquire
+  // fence pair instead would write back / invalidate caches per workgroup (measured 2x slower).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -226,74 +227,71 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   }
   __syncthreads();
   if (!s_last) return;
-  // Combine. Latency-bound (a few KB of L2-bypassing loads), so every load is issued
-  // before any is consumed: (m, l) of all (head, split) pairs by distinct threads, then
-  // per-split weights through LDS, then 8 independent part_o loads in flight per thread.
-  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  constexpr int MAXS = 64;
-  __shared__ float s_w[16][MAXS];   // per (head, split) weight exp2(m_s - M) / L
-  const size_t bh_q0 = (size_t)b * Hq + hk * G;
+
+  // latency-bound: (m, l) of all (head, split) pairs by distinct threads, weights via LDS,
+  // then 8 independent 16-B partial loads in flight per thread
   for (int i = threadIdx.x; i < G * num_splits; i += blockDim.x) {
+    const float4_ ml = rt::sc1_load4(pml_rsrc, i * 16);
     const int qi = i / num_splits, s2 = i - qi * num_splits;
-    const float* ml = part_ml + ((bh_q0 + qi) * num_splits + s2) * 2;
-    const float m = ld(ml), l = ld(ml + 1);
-    s_w[qi][s2] = l > 0.f ? m : -INFINITY;
-    s_o[0][qi][s2] = l;  // reuse the (now idle) merge buffer for l
+    s_wt[qi][s2] = ml[1] > 0.f ? ml[0] : -INFINITY;
+    s_lt[qi][s2] = ml[1];
   }
   __syncthreads();
   if (threadIdx.x < G) {
     const int qi = threadIdx.x;
     float M = -INFINITY;
-    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, s_w[qi][s2]);
+    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, s_wt[qi][s2]);
     float L = 0.f;
     for (int s2 = 0; s2 < num_splits; ++s2) {
-      const float f = (M == -INFINITY || s_w[qi][s2] == -INFINITY) ? 0.f : exp2f(s_w[qi][s2] - M);
-      s_w[qi][s2] = f;
-      L += f * s_o[0][qi][s2];
+      const float f = (M == -INFINITY || s_wt[qi][s2] == -INFINITY) ? 0.f : exp2f(s_wt[qi][s2] - M);
+      s_wt[qi][s2] = f;
+      L += f * s_lt[qi][s2];
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
-    for (int s2 = 0; s2 < num_splits; ++s2) s_w[qi][s2] *= inv;
+    for (int s2 = 0; s2 < num_splits; ++s2) s_wt[qi][s2] *= inv;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
-    const int qi = idx / D, d = idx - qi * D;
-    const float* po = part_o + (bh_q0 + qi) * num_splits * D + d;
-    float O = 0.f;
+  for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
+    const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
+    float4_ O = {0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < num_splits; s0 += 8) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (s0 + j < num_splits) ? ld(po + (size_t)(s0 + j) * D) : 0.f;
+      float4_ v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (s0 + j < num_splits) O = fmaf(s_w[qi][s0 + j], v[j], O);
+        v[j] = (s0 + j < num_splits) ? rt::sc1_load4(po_rsrc, ((qi * num_splits + s0 + j) * D + d0) * 4)
+                                     : float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s0 + j < num_splits) O += s_wt[qi][s0 + j] * v[j];
     }
-    out[(bh_q0 + qi) * D + d] = rt::f2bf(O);
+    uint2 pk;
+    pk.x = rt::pack2(O[0], O[1]);
+    pk.y = rt::pack2(O[2], O[3]);
+    *reinterpret_cast<uint2*>(out + (bh_q0 + qi) * D + d0) = pk;
   }
 }
-
 }  // namespace
 
-// q [B, Hq, D]; k_cache [NB, Hkv, 32, D]; v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32.
+// q [B, Hq, D]; k_cache [NB, Hkv, 32, D]; v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32;
+// part_o >= B*Hq*splits*D floats, part_ml >= B*Hq*splits*4 floats, counters >= B*Hkv ints (zeroed once).
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, hipStream_t stream) {
   if (B == 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16) return -1;
   if (num_splits < 1) num_splits = 1;
-  if (num_splits > 64 || (num_splits > 1 && num_splits > D + 4)) return -3;  // combine staging limits
-  dim3 grid(B * Hkv, num_splits), block(256);
+  if (num_splits > MAXS) return -3;
+  dim3 grid(B * Hkv, num_splits), block(NW * 64);
   const float sl2 = scale * LOG2E;
-#define RT_DEC(DD)                                                                                               \
-  hipLaunchKernelGGL((paged_decode_kernel<DD>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)q,      \
-                     (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, part_o, part_ml, \
-                     counters, Hq, Hkv, max_blocks, sl2, num_splits);
-  if (D == 128) {
-    RT_DEC(128)
-  } else if (D == 64) {
-    RT_DEC(64)
-  } else {
+  if (D == 128)
+    hipLaunchKernelGGL((paged_decode_kernel<128>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)q,
+                       (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, part_o, part_ml,
+                       counters, Hq, Hkv, max_blocks, sl2, num_splits);
+  else if (D == 64)
+    hipLaunchKernelGGL((paged_decode_kernel<64>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)q,
+                       (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, part_o, part_ml,
+                       counters, Hq, Hkv, max_blocks, sl2, num_splits);
+  else
     return -2;
-  }
-#undef RT_DEC
   return 0;
 }

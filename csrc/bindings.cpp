@@ -132,7 +132,7 @@ void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && ctx_lens.numel() >= B, "metadata shape");
   check_type(part_o, torch::kFloat32, "partial_o");
   check_type(part_ml, torch::kFloat32, "partial_ml");
-  TORCH_CHECK(num_splits >= 1 && part_o.numel() >= B * Hq * num_splits * D && part_ml.numel() >= B * Hq * num_splits * 2,
+  TORCH_CHECK(num_splits >= 1 && part_o.numel() >= B * Hq * num_splits * D && part_ml.numel() >= B * Hq * num_splits * 4,
               "split workspace too small");
   check_type(counters, torch::kInt32, "counters");
   TORCH_CHECK(counters.numel() >= B * k_cache.size(1), "split counters too small");

@@ -68,6 +68,20 @@ RT_DEVICE float block_max(float v, float* scratch) {
   return wave_max(t);
 }
 
+// ---- cross-workgroup hand-off I/O (MI355X_MICROARCH "Valid forms": every handed-off byte
+// stored sc1 (write-through past the XCD L2) and loaded sc1 (L1-bypassing), 16 B per lane).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSC1 = 16;  // buffer cache-policy aux bit: scc -> sc1 on gfx94x/gfx950
+RT_DEVICE __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+RT_DEVICE float4_ sc1_load4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kSC1));
+}
+RT_DEVICE void sc1_store4(__amdgpu_buffer_rsrc_t r, int byte_off, float4_ v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, kSC1);
+}
+
 }  // namespace rt
 
 #define RT_HIP_CHECK(expr)                                                              \

@@ -30,12 +30,14 @@
 //                   transposed [blk][h][D][off]). Replaces the K2 rope/cache launch.
 #include "common.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace {
 using rt::bf16x8;
 using rt::float4_;
 using rt::short8;
 
-constexpr int U = 4;  // k-steps per wave per pipeline stage (x2 stages in flight)
 
 enum : int { PRO_PLAIN = 0, PRO_NORM = 1 };
 enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_ROPE = 3 };
@@ -51,15 +53,16 @@ struct RopeEpi {
 
 RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
 
-template <int EPI>
+// U = k-steps per wave per pipeline stage (x2 stages in flight)
+template <int EPI, int U>
 struct Stage {
   short8 w[U];
   short8 w2[(EPI == EPI_SWIGLU) ? U : 1];
   short8 a[U];
 };
 
-template <int EPI, int NW>
-RT_DEVICE void issue(Stage<EPI>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2,
+template <int EPI, int NW, int U>
+RT_DEVICE void issue(Stage<EPI, U>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2,
                      const uint16_t* __restrict__ xr, bool row_ok, int s0, int nsteps, int lane) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -76,8 +79,8 @@ RT_DEVICE void issue(Stage<EPI>& st, const short8* __restrict__ wt, const short8
   }
 }
 
-template <int PRO, int EPI, int NW>
-RT_DEVICE void consume(const Stage<EPI>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps) {
+template <int PRO, int EPI, int NW, int U>
+RT_DEVICE void consume(const Stage<EPI, U>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (s0 + NW * u < nsteps) {
@@ -96,7 +99,7 @@ RT_DEVICE void consume(const Stage<EPI>& st, float4_& acc, float4_& acc2, float&
   }
 }
 
-template <int PRO, int EPI, int NW>
+template <int PRO, int EPI, int NW, int U>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
                                                           const short8* __restrict__ Ws, uint16_t* __restrict__ res,
                                                           int M, int N, int K, int ldo, float eps, RopeEpi re) {
@@ -113,18 +116,18 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restri
 
   float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
   float ssq = 0.f;
-  Stage<EPI> st0, st1;
+  Stage<EPI, U> st0, st1;
   int s = wid;
-  issue<EPI, NW>(st0, wt, wt2, xr, row_ok, s, nsteps, lane);
+  issue<EPI, NW, U>(st0, wt, wt2, xr, row_ok, s, nsteps, lane);
   for (;;) {
     const int sn = s + NW * U;
-    if (sn < nsteps) issue<EPI, NW>(st1, wt, wt2, xr, row_ok, sn, nsteps, lane);
-    consume<PRO, EPI, NW>(st0, acc, acc2, ssq, s, nsteps);
+    if (sn < nsteps) issue<EPI, NW, U>(st1, wt, wt2, xr, row_ok, sn, nsteps, lane);
+    consume<PRO, EPI, NW, U>(st0, acc, acc2, ssq, s, nsteps);
     if (sn >= nsteps) break;
     s = sn;
     const int sn2 = s + NW * U;
-    if (sn2 < nsteps) issue<EPI, NW>(st0, wt, wt2, xr, row_ok, sn2, nsteps, lane);
-    consume<PRO, EPI, NW>(st1, acc, acc2, ssq, s, nsteps);
+    if (sn2 < nsteps) issue<EPI, NW, U>(st0, wt, wt2, xr, row_ok, sn2, nsteps, lane);
+    consume<PRO, EPI, NW, U>(st1, acc, acc2, ssq, s, nsteps);
     if (sn2 >= nsteps) break;
     s = sn2;
   }
@@ -231,19 +234,31 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     re = *static_cast<const RopeEpi*>(rope);
     if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
   }
-  // few column tiles (o/down/qkv projections: <= 1 workgroup per CU) -> 8 waves per workgroup
-  // so each CU keeps 64 KB of weight loads in flight; wide GEMMs (gate_up, lm_head) -> 4.
-  const bool wide = (N / 16) >= 768;
+  // Variant = (waves per workgroup NW, k-steps per stage U). Few column tiles (o/down/qkv
+  // projections: <= ~1.5 workgroups per CU) -> 8 waves so each CU keeps enough weight
+  // bytes in flight; wide GEMMs (gate_up, lm_head) -> 4. RT_SKINNY_CFG=<NW>x<U> (4x4, 8x4,
+  // 8x8, 4x8) pins one for microbenchmarks (tools/microbench.py).
+  static const int cfg_env = [] {
+    const char* e = getenv("RT_SKINNY_CFG");
+    if (!e) return 0;
+    int nw = 0, u = 0;
+    if (sscanf(e, "%dx%d", &nw, &u) != 2) return 0;
+    return nw * 100 + u;
+  }();
+  const int cfg = cfg_env ? cfg_env : ((N / 16) >= 768 ? 404 : 804);
   dim3 grid(N / 16);
-#define RT_SG(P, E)                                                                                                 \
-  do {                                                                                                              \
-    if (wide)                                                                                                       \
-      hipLaunchKernelGGL((skinny_gemm_kernel<P, E, 4>), grid, dim3(256), 0, stream, (uint16_t*)out,                \
-                         (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re);             \
-    else                                                                                                            \
-      hipLaunchKernelGGL((skinny_gemm_kernel<P, E, 8>), grid, dim3(512), 0, stream, (uint16_t*)out,                \
-                         (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re);             \
+#define RT_SG(P, E)                                                                                          \
+  do {                                                                                                       \
+    switch (cfg) {                                                                                           \
+      case 408: RT_SGV(P, E, 4, 8); break;                                                                   \
+      case 804: RT_SGV(P, E, 8, 4); break;                                                                   \
+      case 808: RT_SGV(P, E, 8, 8); break;                                                                   \
+      default: RT_SGV(P, E, 4, 4); break;                                                                    \
+    }                                                                                                        \
   } while (0)
+#define RT_SGV(P, E, NWV, UV)                                                                                \
+  hipLaunchKernelGGL((skinny_gemm_kernel<P, E, NWV, UV>), grid, dim3(NWV * 64), 0, stream, (uint16_t*)out,  \
+                     (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re)
   if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SG(PRO_PLAIN, EPI_STORE);
   else if (pro == PRO_NORM && epi == EPI_STORE) RT_SG(PRO_NORM, EPI_STORE);
   else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_SG(PRO_PLAIN, EPI_RESID);
@@ -253,6 +268,7 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   else if (pro == PRO_PLAIN && epi == EPI_ROPE) RT_SG(PRO_PLAIN, EPI_ROPE);
   else return -2;
 #undef RT_SG
+#undef RT_SGV
   return 0;
 }
 

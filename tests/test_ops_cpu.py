@@ -51,5 +51,7 @@ def test_skinny_gemm_norm_prologue_equals_rmsnorm_then_linear():
 
 def test_decode_splits_bounds():
     assert ops.decode_splits(1, 8) == 32
-    assert ops.decode_splits(16, 8) == 4
+    assert ops.decode_splits(4, 8) == 8
+    assert ops.decode_splits(16, 8) == 2
     assert ops.decode_splits(64, 8) == 1
+    assert ops.decode_splits(1, 1) == 64

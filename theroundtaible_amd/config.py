@@ -9,7 +9,7 @@ object that tells the local engine how to host that knight, and a top-level
 ``engine`` object holds defaults::
 
     "engine": {"default_model": "llama3-8b", "dtype": "bf16", "weights": "random:0",
-               "kv_block_size": 16, "max_new_tokens": 512, "temperature": 0.7,
+               "kv_block_size": 32, "max_new_tokens": 512, "temperature": 0.7,
                "top_p": 0.95, "top_k": 0, "seed": 0, "stop_on_consensus": true},
     "adapter_config": {"claude-cli": {"command": "claude", "args": [],
                                       "engine": {"model": "llama3-8b", "gpus": [0], "tp": 1}}}
@@ -37,7 +37,7 @@ ENGINE_DEFAULTS: Dict[str, Any] = {
     "default_model": "llama3-8b",
     "dtype": "bf16",
     "weights": "random:0",
-    "kv_block_size": 16,
+    "kv_block_size": 32,
     "max_new_tokens": 512,
     "temperature": 0.7,
     "top_p": 0.95,

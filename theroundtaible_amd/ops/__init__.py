@@ -101,19 +101,21 @@ class DecodeWorkspace:
     def __init__(self, max_batch: int, n_heads: int, head_dim: int, max_splits: int, device):
         self.max_splits = max_splits
         self.partial_o = torch.empty(max_batch * n_heads * max_splits * head_dim, dtype=torch.float32, device=device)
-        self.partial_ml = torch.empty(max_batch * n_heads * max_splits * 2, dtype=torch.float32, device=device)
+        self.partial_ml = torch.empty(max_batch * n_heads * max_splits * 4, dtype=torch.float32, device=device)
         # per-(sequence, kv head) split arrival counters; the kernel re-arms them to 0 itself.
         # Sized by n_heads (>= n_kv_heads) so one workspace serves every GQA ratio.
         self.counters = torch.zeros(max_batch * n_heads, dtype=torch.int32, device=device)
 
 
-def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 32) -> int:
-    """Split-KV count fixed per (batch bucket, kv heads): ~2 workgroups per CU at any context length.
+def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 64) -> int:
+    """Split-KV count fixed per (batch bucket, kv heads): about one 8-wave workgroup per CU
+    (measured on MI355X, tools/microbench.py: more, smaller workgroups only add hand-off
+    round trips to the in-launch combine).
 
     The kernel derives each split's key range from the *runtime* context length, so one
     captured hipGraph serves every length (splits past the end are empty and skipped by the
-    reduce) — no re-capture as a knight's discussion grows."""
-    want = max(1, (2 * num_cus) // max(1, batch * n_kv_heads))
+    combine) — no re-capture as a knight's discussion grows."""
+    want = -(-num_cus // max(1, batch * n_kv_heads))
     return int(max(1, min(max_splits, want)))
 
 

@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmarks on the GPU: the decode hot ops of a Llama-3-8B knight batch.
+
+Each op is captured N times into a hipGraph and replayed, so launch overhead does not
+inflate the per-call time. Weight-streaming ops rotate over enough distinct copies
+(>= 1 GiB) that the 256 MB MALL cannot serve repeats — matching a real decode step,
+which streams all 16 GB of weights once. Prints one markdown table (µs, achieved TB/s).
+
+    python tools/microbench.py [--batch 3] [--ctx 6000] [--only gemm,attn,sample,prefill]
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from theroundtaible_amd import ops  # noqa: E402
+from theroundtaible_amd.ops import reference as ref  # noqa: E402
+
+DEV = "cuda"
+ROWS = []
+
+
+def timed(fn, iters=20, reps=5):
+    """µs per call of ``fn(i)`` (i = call index) from hipGraph replays."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for i in range(3):
+            fn(i)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(iters):
+            fn(i)
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        best = min(best, a.elapsed_time(b) * 1000 / iters)
+    return best
+
+
+def row(name, us, nbytes=None, flops=None):
+    tbs = f"{nbytes / us / 1e6:.2f}" if nbytes else ""
+    tf = f"{flops / us / 1e6:.1f}" if flops else ""
+    ROWS.append((name, f"{us:.2f}", tbs, tf))
+    print(f"{name:58s} {us:9.2f} us  {tbs:>6s} TB/s {tf:>7s} TF/s", flush=True)
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+def bench_gemm(M):
+    hid, ffn, hq, hkv, d, vocab = 4096, 14336, 32, 8, 128, 128256
+    x = bf(M, hid)
+    res = bf(M, hid)
+    g_in = bf(M, ffn)
+    nb = 64
+    kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+    cs = ref.rope_cos_sin(8192, d, 500000.0, DEV)
+    pos = torch.arange(M, device=DEV, dtype=torch.int64) + 100
+    slots = torch.arange(M, device=DEV, dtype=torch.int64) + 40
+    shapes = [
+        ("qkv  (norm+rope+cache)", (hq + 2 * hkv) * d, hid),
+        ("o    (+resid)", hid, hq * d),
+        ("gate_up (norm+swiglu)", 2 * ffn, hid),
+        ("down (+resid)", hid, ffn),
+        ("lm_head (norm)", vocab, hid),
+    ]
+    for name, N, K in shapes:
+        nbytes = N * K * 2
+        copies = max(2, math.ceil(2**30 / nbytes))
+        Ws = [ops.shuffle_weight(bf(N, K, scale=0.02)) for _ in range(copies)]
+        # (the launcher reads RT_SKINNY_CFG once: compare variants from separate processes)
+        if name.startswith("qkv"):
+            fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d)
+        elif name.startswith("o ") or name.startswith("down"):
+            inp = x if name.startswith("o ") else g_in
+            fn = lambda i, inp=inp: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
+        elif name.startswith("gate_up"):
+            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM, ops.EPI_SWIGLU)
+        else:
+            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM)
+        us = timed(fn)
+        row(f"skinny {name} M={M} N={N} K={K} cfg={os.environ.get('RT_SKINNY_CFG', 'auto')}", us, nbytes, 2 * M * N * K)
+        del Ws
+        torch.cuda.empty_cache()
+
+
+def bench_attn(B, ctx, splits_list):
+    hq, hkv, d = 32, 8, 128
+    nblk = (ctx + 31) // 32
+    copies = 8
+    caches = []
+    for _ in range(copies):
+        kc = bf(B * nblk, hkv, 32, d)
+        vc = bf(B * nblk, hkv, d, 32)
+        caches.append((kc, vc))
+    bt = torch.arange(B * nblk, device=DEV, dtype=torch.int32).reshape(B, nblk)
+    cl = torch.full((B,), ctx, device=DEV, dtype=torch.int32)
+    q = bf(B, hq, d)
+    nbytes = B * ctx * hkv * d * 2 * 2
+    for splits in splits_list:
+        ws = ops.DecodeWorkspace(B, hq, d, splits, DEV)
+        out = torch.empty_like(q)
+        fn = lambda i, ws=ws, splits=splits, out=out: ops.paged_attention_decode(
+            q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out)
+        row(f"decode attn B={B} ctx={ctx} splits={splits}", timed(fn), nbytes)
+
+
+def bench_sample(B):
+    V = 128256
+    lg = bf(B, V)
+    t = torch.full((B,), 0.8, device=DEV)
+    tp = torch.full((B,), 0.9, device=DEV)
+    tk = torch.zeros(B, dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64)
+    offs = torch.zeros(B, device=DEV, dtype=torch.int64)
+    out = torch.empty(B, dtype=torch.int64, device=DEV)
+    row(f"sample top-p B={B} V={V}", timed(lambda i: ops.sample(lg, t, tp, tk, seeds, offs, out)), B * V * 2)
+
+
+def bench_prefill(T):
+    hq, hkv, d = 32, 8, 128
+    nblk = (T + 31) // 32
+    kc = bf(nblk, hkv, 32, d)
+    vc = bf(nblk, hkv, d, 32)
+    q = bf(T, hq, d)
+    bt = torch.arange(nblk, device=DEV, dtype=torch.int32)[None]
+    cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
+    sp = torch.zeros(1, device=DEV, dtype=torch.int32)
+    rows = ops.native().prefill_rows_per_tile(hq // hkv)
+    tm = ops.prefill_tile_map(cu.cpu(), rows).to(DEV)
+    flops = 4 * hq * d * T * T / 2
+    us = timed(lambda i: ops.prefill_attention(q, kc, vc, bt, cu, sp, 1 / math.sqrt(d), tm), iters=5, reps=3)
+    row(f"prefill attn causal T={T}", us, None, flops)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=3)
+    ap.add_argument("--ctx", type=int, default=6000)
+    ap.add_argument("--only", default="gemm,attn,sample,prefill")
+    ap.add_argument("--splits", default="4,8,11,16,32")
+    a = ap.parse_args()
+    only = set(a.only.split(","))
+    torch.manual_seed(0)
+    if "gemm" in only:
+        bench_gemm(a.batch)
+    if "attn" in only:
+        bench_attn(a.batch, a.ctx, [int(s) for s in a.splits.split(",")])
+        bench_attn(a.batch, 1500, [4, 8, 11, 16])
+    if "sample" in only:
+        bench_sample(a.batch)
+    if "prefill" in only:
+        bench_prefill(4096)
+    print("\n| op | us | TB/s | TF/s |\n|---|---|---|---|")
+    for r in ROWS:
+        print("| " + " | ".join(r) + " |")
+
+
+if __name__ == "__main__":
+    main()
