@@ -30,6 +30,12 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, hipStream_t stream);
+int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
+                       const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
+                       int64_t vocab, hipStream_t stream);
+int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
+                          const int64_t* next, int B, int max_steps, hipStream_t stream);
+int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
                           hipStream_t stream);
 
@@ -259,6 +265,52 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
+// Decode-step bookkeeping (csrc/decode_step.hip).
+void decode_prep(torch::Tensor slots, torch::Tensor offsets, torch::Tensor res, torch::Tensor ids,
+                 torch::Tensor positions, torch::Tensor block_tables, torch::Tensor embed, int64_t block_size) {
+  check_type(slots, torch::kInt64, "slots");
+  check_type(offsets, torch::kInt64, "offsets");
+  check_type(ids, torch::kInt64, "ids");
+  check_type(positions, torch::kInt64, "positions");
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_bf16(res, "res");
+  check_bf16(embed, "embed");
+  const int64_t B = ids.numel();
+  TORCH_CHECK(slots.numel() >= B && offsets.numel() >= B && positions.numel() >= B && block_tables.size(0) >= B,
+              "decode_prep: batch sizes");
+  TORCH_CHECK(res.dim() == 2 && res.size(0) == B && embed.dim() == 2 && res.size(1) == embed.size(1),
+              "decode_prep: res [B, H], embed [V, H]");
+  const int rc = launch_decode_prep(slots.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), res.data_ptr(),
+                                    ids.data_ptr<int64_t>(), positions.data_ptr<int64_t>(),
+                                    block_tables.data_ptr<int>(), embed.data_ptr(), (int)B, (int)block_tables.size(1),
+                                    (int)block_size, (int)embed.size(1), embed.size(0), cur_stream());
+  TORCH_CHECK(rc == 0, "decode_prep: unsupported configuration (rc=", rc, ")");
+}
+
+void decode_advance(torch::Tensor out, torch::Tensor ids, torch::Tensor positions, torch::Tensor ctx_lens,
+                    torch::Tensor step, torch::Tensor next) {
+  check_type(out, torch::kInt64, "out");
+  check_type(ids, torch::kInt64, "ids");
+  check_type(positions, torch::kInt64, "positions");
+  check_type(ctx_lens, torch::kInt32, "ctx_lens");
+  check_type(step, torch::kInt64, "step");
+  check_type(next, torch::kInt64, "next");
+  const int64_t B = ids.numel();
+  TORCH_CHECK(out.dim() == 2 && out.size(1) == B && next.numel() == B && positions.numel() == B &&
+                  ctx_lens.numel() == B,
+              "decode_advance: shapes");
+  launch_decode_advance(out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), positions.data_ptr<int64_t>(),
+                        ctx_lens.data_ptr<int>(), step.data_ptr<int64_t>(), next.data_ptr<int64_t>(), (int)B,
+                        (int)out.size(0), cur_stream());
+}
+
+// Pull a tensor's bytes into the MALL ahead of its consumer (side-stream warm-up).
+void prefetch(torch::Tensor t, int64_t nwg, torch::Tensor sink) {
+  check_gpu(t, "t");
+  check_type(sink, torch::kInt32, "sink");
+  launch_prefetch(t.data_ptr(), t.numel() * t.element_size(), (int)nwg, (uint32_t*)sink.data_ptr(), cur_stream());
+}
+
 void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tensor> gamma, int64_t rope_heads,
                     int64_t head_dim) {
   check_bf16(Ws, "Ws");
@@ -283,6 +335,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("eps") = 1e-5);
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
         py::arg("rope_heads") = 0, py::arg("head_dim") = 0);
+  m.def("decode_prep", &decode_prep);
+  m.def("decode_advance", &decode_advance);
+  m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));
   m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write");
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);

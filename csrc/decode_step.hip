@@ -1,0 +1,66 @@
+// Per-token bookkeeping of the captured decode step, fused into two tiny launches (was ~12
+// PyTorch elementwise kernels ≈ 45 µs per token, profiles/r01_*_v3*.md):
+//
+//   decode_prep    : slot[b]   = block_tables[b][pos/BS] * BS + pos % BS   (K/V write slot)
+//                    offset[b] = pos + 1                                   (sampler RNG offset)
+//                    res[b, :] = embed[ids[b], :]                          (embedding gather)
+//   decode_advance : out[step, b] = next[b]; ids[b] = next[b]; pos[b] += 1; ctx[b] += 1;
+//                    step += 1                                              (after sampling)
+//
+// Everything the next replay needs stays on the device, so a hipGraph replay takes no host
+// input. One workgroup per batch row; the embedding row copy is 16 B per lane.
+#include "common.h"
+
+namespace {
+__global__ void __launch_bounds__(256) decode_prep_kernel(
+    int64_t* __restrict__ slots, int64_t* __restrict__ offsets, uint16_t* __restrict__ res,
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ positions, const int* __restrict__ block_tables,
+    const uint16_t* __restrict__ embed, int max_blocks, int BS, int H, int64_t vocab) {
+  const int b = blockIdx.x;
+  const int64_t pos = positions[b];
+  if (threadIdx.x == 0) {
+    const int64_t blk = block_tables[(size_t)b * max_blocks + pos / BS];
+    slots[b] = blk * BS + pos % BS;
+    offsets[b] = pos + 1;
+  }
+  int64_t tok = ids[b];
+  tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);
+  const uint4* src = reinterpret_cast<const uint4*>(embed + (size_t)tok * H);
+  uint4* dst = reinterpret_cast<uint4*>(res + (size_t)b * H);
+  for (int i = threadIdx.x; i < H / 8; i += blockDim.x) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(64) decode_advance_kernel(int64_t* __restrict__ out, int64_t* __restrict__ ids,
+                                                            int64_t* __restrict__ positions, int* __restrict__ ctx_lens,
+                                                            int64_t* __restrict__ step, const int64_t* __restrict__ next,
+                                                            int B, int max_steps) {
+  const int64_t st = *step;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int64_t t = next[b];
+    if (st < max_steps) out[st * B + b] = t;
+    ids[b] = t;
+    positions[b] += 1;
+    ctx_lens[b] += 1;
+  }
+  __syncthreads();  // every lane has read *step before lane 0 bumps it
+  if (threadIdx.x == 0) *step = st + 1;
+}
+}  // namespace
+
+int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
+                       const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
+                       int64_t vocab, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (H % 8) return -1;
+  hipLaunchKernelGGL(decode_prep_kernel, dim3(B), dim3(256), 0, stream, slots, offsets, (uint16_t*)res, ids,
+                     positions, block_tables, (const uint16_t*)embed, max_blocks, BS, H, vocab);
+  return 0;
+}
+
+int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
+                          const int64_t* next, int B, int max_steps, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(64), 0, stream, out, ids, positions, ctx_lens, step, next,
+                     B, max_steps);
+  return 0;
+}

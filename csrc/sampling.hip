@@ -123,13 +123,20 @@ __global__ void __launch_bounds__(NT) smp_stats(float* __restrict__ ws, const T*
   __shared__ float sv[4];
   __shared__ int si[4];
   const int b = blockIdx.x, c = blockIdx.y;
+  float* w = ws + (size_t)b * W_ROW;
+  // zero this chunk's share of the row's histogram / counter region (replaces a per-call
+  // memset launch; launches 2-5 are stream-ordered after this one)
+  {
+    const int z0 = W_HC, zn = W_ROW - W_HC, per = (zn + C - 1) / C;
+    const int lo_z = z0 + c * per, hi_z = min(z0 + zn, lo_z + per);
+    for (int i = lo_z + threadIdx.x; i < hi_z; i += NT) w[i] = 0.f;
+  }
   int lo, hi;
   chunk_range(V, c, lo, hi);
   ArgMax a{-INFINITY, 0x7fffffff};
   for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) { am_merge(a, v, i); });
   a = block_argmax(a, sv, si);
   if (threadIdx.x == 0) {
-    float* w = ws + (size_t)b * W_ROW;
     w[W_MAX + c] = a.v;
     reinterpret_cast<int*>(w)[W_ARG + c] = a.i;
   }
@@ -339,14 +346,15 @@ __global__ void __launch_bounds__(1024) smp_final(int64_t* __restrict__ out, flo
   if (threadIdx.x == 0) {
     ArgMax bm{-INFINITY, 0x7fffffff};
     for (int j = 0; j < 16; ++j) am_merge(bm, sv[j], si[j]);
-    // publish this chunk's partial, then count arrivals (release/acquire at agent scope, G16)
+    // publish this chunk's partial with sc1 (write-through) stores, drain them, then count
+    // arrivals; the last arriver reads every partial with sc1 loads (MI355X_MICROARCH "Valid
+    // forms" row 1: no L2 writeback/invalidate fences needed)
     __hip_atomic_store(&w[W_PV + c], bm.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&wi[W_PI + c], bm.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int prev = __hip_atomic_fetch_add(&wi[W_CNT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = (prev == C - 1);
     if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       ArgMax r{-INFINITY, 0x7fffffff};
       for (int j = 0; j < C; ++j)
         am_merge(r, __hip_atomic_load(&w[W_PV + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -368,7 +376,6 @@ int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, 
   if (B == 0) return 0;
   const size_t esz = is_bf16 ? 2 : 4;
   const bool vec = ((uintptr_t)logits % 16 == 0) && ((ld_row * esz) % 16 == 0);
-  hipMemsetAsync(ws, 0, sizeof(float) * (size_t)B * W_ROW, stream);  // histograms + counters, every call
   const dim3 g2(B, C);
 #define RT_SMP(TT, VV)                                                                                              \
   do {                                                                                                              \

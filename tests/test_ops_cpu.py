@@ -54,4 +54,24 @@ def test_decode_splits_bounds():
     assert ops.decode_splits(4, 8) == 8
     assert ops.decode_splits(16, 8) == 2
     assert ops.decode_splits(64, 8) == 1
+    assert ops.decode_splits(3, 8) == 10
     assert ops.decode_splits(1, 1) == 64
+
+
+def test_decode_prep_and_advance_reference():
+    bt = torch.tensor([[5, 7, 9], [2, 3, 4]], dtype=torch.int32)
+    pos = torch.tensor([33, 64])
+    ids = torch.tensor([1, 3])
+    emb = torch.arange(4 * 8, dtype=torch.float32).reshape(4, 8).bfloat16()
+    slots, offs = torch.zeros(2, dtype=torch.int64), torch.zeros(2, dtype=torch.int64)
+    res = torch.zeros(2, 8).bfloat16()
+    ops.decode_prep(slots, offs, res, ids, pos, bt, emb, 32)
+    assert slots.tolist() == [7 * 32 + 1, 4 * 32 + 0]
+    assert offs.tolist() == [34, 65]
+    assert torch.equal(res, emb[[1, 3]])
+    out = torch.zeros(4, 2, dtype=torch.int64)
+    ctx = torch.tensor([34, 65], dtype=torch.int32)
+    step = torch.zeros(1, dtype=torch.int64)
+    ops.decode_advance(out, ids, pos, ctx, step, torch.tensor([11, 12]))
+    assert out[0].tolist() == [11, 12] and ids.tolist() == [11, 12]
+    assert pos.tolist() == [34, 65] and ctx.tolist() == [35, 66] and step.item() == 1

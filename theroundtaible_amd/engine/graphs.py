@@ -46,24 +46,35 @@ class DecodeGraph:
         self.seeds = torch.zeros(B, dtype=torch.int64, device=dev)
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
         self.out = torch.zeros(MAX_STEPS, B, dtype=torch.int64, device=dev)
+        self.slots = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.offsets = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.hidden = torch.zeros(B, engine.model.cfg.hidden, dtype=engine.model.dtype, device=dev)
         self.ws = ops.DecodeWorkspace(B, engine.model.n_heads, engine.cfg.head_dim, max(1, splits), dev)
         self.graph = None
         self._capture()
 
     def _body(self):
         e = self.engine
-        bs = self.bs
-        blk = self.block_tables.gather(1, (self.positions // bs).unsqueeze(1)).squeeze(1).long()
-        slots = blk * bs + self.positions % bs
+        fused = getattr(e.model, "accepts_hidden", False) and e.model.fused_decode_ok(self.input_ids)
+        if fused:
+            # one prologue launch: K/V slots, sampler offsets, embedding rows (csrc/decode_step.hip)
+            ops.decode_prep(self.slots, self.offsets, self.hidden, self.input_ids, self.positions,
+                            self.block_tables, e.model.w["embed"], self.bs)
+            slots, offsets, hidden = self.slots, self.offsets, self.hidden
+        else:
+            bs = self.bs
+            blk = self.block_tables.gather(1, (self.positions // bs).unsqueeze(1)).squeeze(1).long()
+            slots = blk * bs + self.positions % bs
+            offsets, hidden = self.positions + 1, None
         meta = AttnMeta(kind="decode", slot_mapping=slots, block_tables=self.block_tables, ctx_lens=self.ctx_lens,
                         num_splits=self.splits, workspace=self.ws)
-        logits = e.model.forward(self.input_ids, self.positions, e.kv, meta)
-        nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, self.positions + 1)
-        self.out.index_copy_(0, self.step, nxt.unsqueeze(0))
-        self.input_ids.copy_(nxt)
-        self.positions.add_(1)
-        self.ctx_lens.add_(1)
-        self.step.add_(1)
+        if hidden is not None:
+            logits = e.model.forward(self.input_ids, self.positions, e.kv, meta, hidden=hidden)
+        else:
+            logits = e.model.forward(self.input_ids, self.positions, e.kv, meta)
+        nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets)
+        # one epilogue launch: record ids, advance positions / lengths / step
+        ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt)
 
     def _reset_dummy(self):
         self.positions.zero_()

@@ -95,7 +95,10 @@ class LlamaModel:
                 self._dec = {"layers": layers, "lm_head": ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])}
         return self._dec
 
-    def forward_decode_fused(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta) -> torch.Tensor:
+    accepts_hidden = True  # forward(..., hidden=) takes pre-gathered embedding rows (decode_prep)
+
+    def forward_decode_fused(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
+                             hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Decode step with every norm / residual / activation fused into the MFMA GEMMs
         (csrc/gemm_skinny.hip): per layer qkv(+RMSNorm, +RoPE/KV-cache write) -> K3 (split-KV
         combined in-kernel) -> o(+residual) -> gate_up(+RMSNorm, SwiGLU) -> down(+residual).
@@ -103,7 +106,8 @@ class LlamaModel:
         cfg = self.cfg
         eps = cfg.norm_eps
         dec = self.decode_weights()
-        res = F.embedding(ids, self.w["embed"]).contiguous()
+        # the residual stream is updated in place by every RESID epilogue
+        res = hidden if hidden is not None else F.embedding(ids, self.w["embed"]).contiguous()
         B = ids.shape[0]
         for l, lw in enumerate(dec["layers"]):
             q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kv.k_layer(l),
@@ -116,10 +120,12 @@ class LlamaModel:
         logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
         return logits[:, :cfg.vocab]
 
-    def forward(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta) -> torch.Tensor:
-        """Returns logits [rows, vocab] (all rows for decode, ``meta.last_rows`` for prefill)."""
+    def forward(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
+                hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Returns logits [rows, vocab] (all rows for decode, ``meta.last_rows`` for prefill).
+        ``hidden``: optional pre-gathered embedding rows (used by the fused decode path only)."""
         if meta.kind == "decode" and self.fused_decode_ok(ids):
-            return self.forward_decode_fused(ids, positions, kv, meta)
+            return self.forward_decode_fused(ids, positions, kv, meta, hidden)
         cfg, tp = self.cfg, self.tp
         T = ids.shape[0]
         h = F.embedding(ids, self.w["embed"])

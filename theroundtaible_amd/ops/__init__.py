@@ -108,15 +108,15 @@ class DecodeWorkspace:
 
 
 def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 64) -> int:
-    """Split-KV count fixed per (batch bucket, kv heads): about one 8-wave workgroup per CU
-    (measured on MI355X, tools/microbench.py: more, smaller workgroups only add hand-off
-    round trips to the in-launch combine).
+    """Split-KV count fixed per (batch bucket, kv heads): at most one 8-wave workgroup per CU
+    (measured on MI355X, profiles/r01_microbench_v1.log: B=3, ctx 6000 -> 8 splits 22 µs,
+    11 splits 27 µs, 16 splits 28 µs; extra workgroups only add hand-off round trips).
 
     The kernel derives each split's key range from the *runtime* context length, so one
     captured hipGraph serves every length (splits past the end are empty and skipped by the
     combine) — no re-capture as a knight's discussion grows."""
-    want = -(-num_cus // max(1, batch * n_kv_heads))
-    return int(max(1, min(max_splits, want)))
+    want = num_cus // max(1, batch * n_kv_heads)   # never more workgroups than CUs: a second
+    return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
 
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
@@ -201,6 +201,24 @@ def skinny_gemm_rope(x: torch.Tensor, Ws: torch.Tensor, pro: int, positions: tor
         return q
     return ref.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
                                 head_dim, eps)
+
+
+def decode_prep(slots: torch.Tensor, offsets: torch.Tensor, res: torch.Tensor, ids: torch.Tensor,
+                positions: torch.Tensor, block_tables: torch.Tensor, embed: torch.Tensor, block_size: int) -> None:
+    """Captured-step prologue (csrc/decode_step.hip): K/V slots, sampler offsets, embedding rows."""
+    if _use_native(ids):
+        native().decode_prep(slots, offsets, res, ids, positions, block_tables, embed, int(block_size))
+        return
+    ref.decode_prep(slots, offsets, res, ids, positions, block_tables, embed, block_size)
+
+
+def decode_advance(out: torch.Tensor, ids: torch.Tensor, positions: torch.Tensor, ctx_lens: torch.Tensor,
+                   step: torch.Tensor, nxt: torch.Tensor) -> None:
+    """Captured-step epilogue: record the sampled ids and advance positions / lengths / step."""
+    if _use_native(ids):
+        native().decode_advance(out, ids, positions, ctx_lens, step, nxt)
+        return
+    ref.decode_advance(out, ids, positions, ctx_lens, step, nxt)
 
 
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:

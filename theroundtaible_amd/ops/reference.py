@@ -262,3 +262,24 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
         score = torch.where(allowed, z.double() + g, torch.full((), float("-inf"), dtype=torch.float64))
         out[b] = int(torch.argmax(score))
     return out
+
+
+def decode_prep(slots, offsets, res, ids, positions, block_tables, embed, block_size):
+    """Semantics of csrc/decode_step.hip::decode_prep (in place)."""
+    pos = positions.long()
+    blk = block_tables.long().gather(1, (pos // block_size).unsqueeze(1)).squeeze(1)
+    slots[:len(pos)] = blk * block_size + pos % block_size
+    offsets[:len(pos)] = pos + 1
+    tok = ids.long().clamp(0, embed.shape[0] - 1)
+    res.copy_(embed[tok].to(res.dtype))
+
+
+def decode_advance(out, ids, positions, ctx_lens, step, nxt):
+    """Semantics of csrc/decode_step.hip::decode_advance (in place)."""
+    st = int(step.item())
+    if st < out.shape[0]:
+        out[st] = nxt
+    ids.copy_(nxt)
+    positions.add_(1)
+    ctx_lens.add_(1)
+    step.add_(1)
