@@ -69,3 +69,31 @@ def test_long_context_split_decode():
     b = eng(num_blocks=1024, use_graphs=False)
     out2 = b.run_turns([Turn("K", long, GREEDY)])[0]
     assert out.ids == out2.ids
+
+
+def test_serve_on_gpu_batches_requests():
+    import json
+    import threading
+    import urllib.request
+    from theroundtaible_amd.serve import build_server
+    srv = build_server("tiny-llama-128", weights="random:2", device="cuda:0", port=0, max_batch=4, max_tokens=8,
+                       num_blocks=512).start()
+    try:
+        codes = []
+
+        def go(i):
+            req = urllib.request.Request(srv.url + "/v1/chat/completions", method="POST",
+                                         headers={"Content-Type": "application/json"},
+                                         data=json.dumps({"messages": [{"role": "user", "content": f"q{i}"}],
+                                                          "max_tokens": 8}).encode())
+            with urllib.request.urlopen(req, timeout=120) as r:
+                codes.append((r.status, json.loads(r.read())["usage"]["completion_tokens"]))
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert codes == [(200, 8)] * 4
+        assert srv.engine.graphs   # decode ran through captured hipGraphs
+    finally:
+        srv.close()

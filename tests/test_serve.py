@@ -1,0 +1,105 @@
+"""`roundtable serve` on a CPU engine: OpenAI + Ollama dialects, batching, session KV reuse."""
+import json
+import threading
+import urllib.request
+
+import pytest
+
+from theroundtaible_amd.serve import build_server, render_chat
+
+
+def _post(url, body):
+    req = urllib.request.Request(url, data=json.dumps(body).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    with urllib.request.urlopen(req, timeout=120) as r:
+        return r.status, r.read().decode()
+
+
+def _get(url):
+    with urllib.request.urlopen(url, timeout=30) as r:
+        return r.status, r.read().decode()
+
+
+@pytest.fixture(scope="module")
+def server():
+    srv = build_server("tiny-llama", weights="random:1", device="cpu", port=0, max_batch=4, max_tokens=8,
+                       num_blocks=256).start()
+    yield srv
+    srv.close()
+
+
+def test_models_health_metrics(server):
+    code, body = _get(server.url + "/v1/models")
+    assert code == 200 and json.loads(body)["data"][0]["id"] == "tiny-llama"
+    assert json.loads(_get(server.url + "/health")[1])["status"] == "ok"
+    assert "roundtable_requests_total" in _get(server.url + "/metrics")[1]
+
+
+def test_chat_completion_openai(server):
+    code, body = _post(server.url + "/v1/chat/completions",
+                       {"model": "tiny-llama", "messages": [{"role": "user", "content": "Hallo ridders"}],
+                        "max_tokens": 6, "temperature": 0})
+    d = json.loads(body)
+    assert code == 200 and d["object"] == "chat.completion"
+    assert d["choices"][0]["message"]["role"] == "assistant"
+    assert d["usage"]["completion_tokens"] == 6 and d["choices"][0]["finish_reason"] == "length"
+
+
+def test_stream_and_completions_and_ollama(server):
+    code, body = _post(server.url + "/v1/chat/completions",
+                       {"messages": [{"role": "user", "content": "x"}], "max_tokens": 3, "stream": True})
+    assert code == 200 and body.rstrip().endswith("data: [DONE]")
+    code, body = _post(server.url + "/v1/completions", {"prompt": "Onderwerp:", "max_tokens": 4})
+    assert json.loads(body)["object"] == "text_completion"
+    code, body = _post(server.url + "/api/chat", {"model": "tiny-llama", "messages": [{"role": "user", "content": "q"}],
+                                                  "options": {"num_predict": 5}, "stream": False})
+    d = json.loads(body)
+    assert d["done"] is True and d["eval_count"] == 5
+    ctx = json.loads(_post(server.url + "/api/show", {"name": "tiny-llama"})[1])["model_info"]
+    assert any(k.endswith(".context_length") for k in ctx)
+
+
+def test_greedy_is_deterministic_and_session_reuses_kv(server):
+    body = {"messages": [{"role": "user", "content": "Wat is het plan?"}], "max_tokens": 5, "temperature": 0}
+    a = json.loads(_post(server.url + "/v1/chat/completions", body)[1])["choices"][0]["message"]["content"]
+    b = json.loads(_post(server.url + "/v1/chat/completions", body)[1])["choices"][0]["message"]["content"]
+    assert a == b
+    conv = [{"role": "user", "content": "Eerste vraag over caching."}]
+    s1 = dict(body, messages=conv, user="knight-7")
+    r1 = json.loads(_post(server.url + "/v1/chat/completions", s1)[1])
+    conv2 = conv + [{"role": "assistant", "content": r1["choices"][0]["message"]["content"]},
+                    {"role": "user", "content": "En nu?"}]
+    before = server.sched.stats["reused_tokens"]
+    _post(server.url + "/v1/chat/completions", dict(body, messages=conv2, user="knight-7"))
+    assert server.sched.stats["reused_tokens"] - before > 10   # the first exchange stayed resident
+
+
+def test_concurrent_requests_are_batched(server):
+    results, errs = [], []
+
+    def go(i):
+        try:
+            results.append(_post(server.url + "/v1/chat/completions",
+                                 {"messages": [{"role": "user", "content": f"vraag {i}"}], "max_tokens": 4})[0])
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    b0 = server.sched.stats["batches"]
+    ts = [threading.Thread(target=go, args=(i,)) for i in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and results == [200] * 6
+    assert server.sched.stats["batches"] - b0 < 6   # at least two requests shared a batch
+
+
+def test_bad_requests(server):
+    import urllib.error
+    with pytest.raises(urllib.error.HTTPError) as ei:
+        _post(server.url + "/v1/chat/completions", {"messages": []})
+    assert ei.value.code == 400
+
+
+def test_render_chat():
+    s = render_chat([{"role": "system", "content": "S"}, {"role": "user", "content": [{"type": "text", "text": "U"}]}])
+    assert s.endswith("### Assistent:\n") and "### Systeem:\nS" in s and "### Gebruiker:\nU" in s

@@ -433,6 +433,22 @@ def cmd_bench(args, ui: UI) -> int:
     return subprocess.call(cmd)
 
 
+def cmd_serve(args, ui: UI) -> int:
+    from .serve import build_server
+    srv = build_server(args.model, weights=args.weights, device=args.device, dtype=args.dtype, host=args.host,
+                       port=args.port, max_batch=args.max_batch, max_tokens=args.max_tokens,
+                       use_graphs=not args.no_graphs, num_blocks=args.num_blocks)
+    ui.ok(f"  ✓ {args.model} on {srv.engine.device}: {srv.engine.kv_capacity_tokens} KV tokens resident capacity")
+    ui.dim(f"  serving {srv.url}/v1/chat/completions  (OpenAI)  and  {srv.url}/api/chat  (Ollama)")
+    try:
+        srv.serve_forever()
+    except KeyboardInterrupt:
+        pass
+    finally:
+        srv.close()
+    return 0
+
+
 # ---- parser -------------------------------------------------------------------------------------
 def _discuss_flags(p):
     g = p.add_mutually_exclusive_group()
@@ -503,6 +519,18 @@ def build_parser() -> argparse.ArgumentParser:
     md.add_argument("--replaced-by")
     msub.add_parser("check")
     m.set_defaults(fn=cmd_manifest)
+    sv = sub.add_parser("serve", help="Host a knight model behind an OpenAI/Ollama-compatible HTTP endpoint")
+    sv.add_argument("--model", default="llama3-8b")
+    sv.add_argument("--weights", default="random:0", help="random:<seed> | random-full:<seed> | <safetensors dir>")
+    sv.add_argument("--device", default="cuda:0")
+    sv.add_argument("--dtype", default="bf16")
+    sv.add_argument("--host", default="127.0.0.1")
+    sv.add_argument("--port", type=int, default=8000)
+    sv.add_argument("--max-batch", type=int, default=16)
+    sv.add_argument("--max-tokens", type=int, default=512, help="default completion budget per request")
+    sv.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: sized from free memory)")
+    sv.add_argument("--no-graphs", action="store_true")
+    sv.set_defaults(fn=cmd_serve)
     b = sub.add_parser("bench", help="Run the roundtable benchmark (wraps bench.py)")
     b.add_argument("bench_args", nargs=argparse.REMAINDER)
     b.set_defaults(fn=cmd_bench)

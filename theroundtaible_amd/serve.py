@@ -1,0 +1,356 @@
+"""``roundtable serve``: host a knight model on this GPU behind an OpenAI-/Ollama-compatible
+HTTP endpoint (bound to 127.0.0.1 by default).
+
+Why: the reference's only self-hosted path is its ``local-llm`` adapter talking to an
+Ollama / LM Studio server (`src/adapters/local-llm.ts:6-249`, discovery in
+`src/utils/local-detect.ts:103-134`). This module is that *server side*, built on the
+MI355X engine instead of a third-party runtime, so any client that speaks those two
+dialects (including another roundtable's knights, scripts, IDE plugins) can use a
+resident-KV, hipGraph-decoding MI355X knight.
+
+Serving model:
+
+* one :class:`~theroundtaible_amd.engine.Engine` per process (one process per GPU; run
+  several ``serve`` processes for several GPUs);
+* a batching scheduler thread: every request waiting when the engine becomes free joins
+  the next batch (up to ``max_batch``), so concurrent clients share one hipGraph replay
+  per token — the same batching the round table uses for parallel knights;
+* conversation KV reuse: a request carrying ``"user"`` (OpenAI) or ``"session"`` keeps
+  its KV sequence resident under that key, so the next request of the conversation
+  prefills only its new tokens (longest-common-prefix reuse, engine.sync_prefix);
+  anonymous requests get a fresh sequence that is released afterwards;
+* endpoints: ``GET /v1/models``, ``POST /v1/chat/completions`` (``stream`` answered as one
+  SSE delta + ``[DONE]``), ``POST /v1/completions``, ``POST /api/chat`` and
+  ``POST /api/show`` (Ollama), ``GET /health``, ``GET /metrics`` (Prometheus text).
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import queue
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Dict, List, Optional, Tuple
+
+from .engine import Engine, EngineConfig, SamplingParams, Turn
+
+ROLE_TAGS = {"system": "Systeem", "user": "Gebruiker", "assistant": "Assistent"}
+
+
+def render_chat(messages: List[Dict[str, Any]]) -> str:
+    """Plain role-tagged transcript ending in an open assistant turn (the bundled models
+    have no chat special tokens; the tags match the roundtable's own prompt style)."""
+    parts = []
+    for m in messages:
+        role = str(m.get("role", "user"))
+        content = m.get("content", "")
+        if isinstance(content, list):  # OpenAI content parts
+            content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
+        parts.append(f"### {ROLE_TAGS.get(role, role)}:\n{content}\n")
+    parts.append(f"### {ROLE_TAGS['assistant']}:\n")
+    return "\n".join(parts)
+
+
+@dataclass
+class _Request:
+    key: str
+    prompt: str
+    params: SamplingParams
+    persistent: bool
+    done: threading.Event = field(default_factory=threading.Event)
+    result: Any = None
+    error: Optional[BaseException] = None
+
+
+class Scheduler:
+    """Single engine worker; batches whatever is queued when the engine frees up."""
+
+    def __init__(self, engine: Engine, max_batch: int = 16, timeout_s: float = 600.0):
+        self.engine = engine
+        self.max_batch = max(1, int(max_batch))
+        self.timeout_s = timeout_s
+        self.q: "queue.Queue[_Request]" = queue.Queue()
+        self.stats = {"requests": 0, "batches": 0, "prompt_tokens": 0, "completion_tokens": 0,
+                      "reused_tokens": 0, "busy_s": 0.0, "errors": 0}
+        self._stop = threading.Event()
+        self._lock = threading.Lock()
+        self.thread = threading.Thread(target=self._loop, name="roundtable-serve", daemon=True)
+        self.thread.start()
+
+    def submit(self, req: _Request) -> _Request:
+        self.q.put(req)
+        return req
+
+    def close(self) -> None:
+        self._stop.set()
+        self.q.put(None)  # type: ignore[arg-type]
+        self.thread.join(timeout=5)
+
+    def _take_batch(self) -> List[_Request]:
+        first = self.q.get()
+        if first is None:
+            return []
+        batch, keys, later = [first], {first.key}, []
+        while len(batch) < self.max_batch:
+            try:
+                r = self.q.get_nowait()
+            except queue.Empty:
+                break
+            if r is None:
+                self._stop.set()
+                break
+            (later if r.key in keys else batch).append(r)  # one turn per sequence per batch
+            keys.add(r.key)
+        for r in later:
+            self.q.put(r)
+        return batch
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            batch = self._take_batch()
+            if not batch:
+                continue
+            t0 = time.perf_counter()
+            turns = [Turn(r.key, r.prompt, r.params, timeout_s=self.timeout_s) for r in batch]
+            try:
+                outs = self.engine.run_turns(turns)
+            except BaseException as e:  # noqa: BLE001 - reported per request
+                outs = [e] * len(batch)
+            dt = time.perf_counter() - t0
+            with self._lock:
+                self.stats["batches"] += 1
+                self.stats["busy_s"] += dt
+            for r, o in zip(batch, outs):
+                if isinstance(o, BaseException) or getattr(o, "error", None) is not None:
+                    r.error = o if isinstance(o, BaseException) else o.error
+                    with self._lock:
+                        self.stats["errors"] += 1
+                else:
+                    r.result = o
+                    with self._lock:
+                        self.stats["requests"] += 1
+                        self.stats["prompt_tokens"] += int(o.metrics.get("prompt_tokens", 0))
+                        self.stats["completion_tokens"] += len(o.ids)
+                        self.stats["reused_tokens"] += int(o.metrics.get("reused_tokens", 0))
+                if not r.persistent:
+                    try:
+                        self.engine.release(r.key)
+                    except Exception:  # noqa: BLE001
+                        pass
+                r.done.set()
+
+
+class RoundtableServer:
+    """The HTTP front end. ``start()`` serves on a background thread; ``serve_forever()`` blocks."""
+
+    _anon = itertools.count()
+
+    def __init__(self, engine: Engine, model_name: str, host: str = "127.0.0.1", port: int = 8000,
+                 max_batch: int = 16, default_max_tokens: int = 512, timeout_s: float = 600.0):
+        self.engine = engine
+        self.model_name = model_name
+        self.default_max_tokens = default_max_tokens
+        self.sched = Scheduler(engine, max_batch, timeout_s)
+        self.started = time.time()
+        server = self
+
+        class Handler(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, fmt, *args):  # quiet by default
+                pass
+
+            def _send(self, code: int, obj: Any, ctype: str = "application/json") -> None:
+                body = obj if isinstance(obj, bytes) else (
+                    obj.encode() if isinstance(obj, str) else json.dumps(obj).encode())
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def _json_body(self) -> Dict[str, Any]:
+                n = int(self.headers.get("Content-Length") or 0)
+                raw = self.rfile.read(n) if n else b"{}"
+                try:
+                    d = json.loads(raw or b"{}")
+                except ValueError:
+                    raise ValueError("request body is not valid JSON")
+                if not isinstance(d, dict):
+                    raise ValueError("request body must be a JSON object")
+                return d
+
+            def do_GET(self):  # noqa: N802
+                if self.path.rstrip("/") == "/v1/models":
+                    self._send(200, {"object": "list", "data": [
+                        {"id": server.model_name, "object": "model", "created": int(server.started),
+                         "owned_by": "theroundtaible-amd"}]})
+                elif self.path.rstrip("/") in ("/health", ""):
+                    self._send(200, {"status": "ok" if server.engine.healthy else "unhealthy",
+                                     "model": server.model_name, "device": str(server.engine.device)})
+                elif self.path.rstrip("/") == "/metrics":
+                    self._send(200, server.metrics_text(), "text/plain; version=0.0.4")
+                else:
+                    self._send(404, {"error": {"message": f"no route {self.path}"}})
+
+            def do_POST(self):  # noqa: N802
+                path = self.path.rstrip("/")
+                try:
+                    body = self._json_body()
+                    if path == "/v1/chat/completions":
+                        self._chat_openai(body)
+                    elif path == "/v1/completions":
+                        self._completion_openai(body)
+                    elif path == "/api/chat":
+                        self._chat_ollama(body)
+                    elif path == "/api/show":
+                        self._send(200, server.show())
+                    else:
+                        self._send(404, {"error": {"message": f"no route {self.path}"}})
+                except ValueError as e:
+                    self._send(400, {"error": {"message": str(e), "type": "invalid_request_error"}})
+                except Exception as e:  # noqa: BLE001
+                    self._send(500, {"error": {"message": str(e), "type": "server_error"}})
+
+            def _chat_openai(self, body):
+                msgs = body.get("messages")
+                if not isinstance(msgs, list) or not msgs:
+                    raise ValueError("'messages' must be a non-empty list")
+                out, r = server.generate(render_chat(msgs), body, body.get("user") or body.get("session"))
+                rid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
+                usage = server.usage(out)
+                if body.get("stream"):
+                    chunk = {"id": rid, "object": "chat.completion.chunk", "created": int(time.time()),
+                             "model": server.model_name,
+                             "choices": [{"index": 0, "delta": {"role": "assistant", "content": out.text},
+                                          "finish_reason": None}]}
+                    end = dict(chunk, choices=[{"index": 0, "delta": {}, "finish_reason": server.finish(out, r)}])
+                    sse = f"data: {json.dumps(chunk)}\n\ndata: {json.dumps(end)}\n\ndata: [DONE]\n\n"
+                    self._send(200, sse, "text/event-stream")
+                    return
+                self._send(200, {"id": rid, "object": "chat.completion", "created": int(time.time()),
+                                 "model": server.model_name,
+                                 "choices": [{"index": 0, "message": {"role": "assistant", "content": out.text},
+                                              "finish_reason": server.finish(out, r)}],
+                                 "usage": usage})
+
+            def _completion_openai(self, body):
+                prompt = body.get("prompt")
+                if isinstance(prompt, list):
+                    prompt = "".join(str(p) for p in prompt)
+                if not isinstance(prompt, str):
+                    raise ValueError("'prompt' must be a string")
+                out, r = server.generate(prompt, body, body.get("user"))
+                self._send(200, {"id": f"cmpl-{uuid.uuid4().hex[:24]}", "object": "text_completion",
+                                 "created": int(time.time()), "model": server.model_name,
+                                 "choices": [{"index": 0, "text": out.text, "finish_reason": server.finish(out, r)}],
+                                 "usage": server.usage(out)})
+
+            def _chat_ollama(self, body):
+                msgs = body.get("messages")
+                if not isinstance(msgs, list) or not msgs:
+                    raise ValueError("'messages' must be a non-empty list")
+                opts = body.get("options") or {}
+                params = {"temperature": opts.get("temperature"), "top_p": opts.get("top_p"),
+                          "top_k": opts.get("top_k"), "seed": opts.get("seed"),
+                          "max_tokens": opts.get("num_predict")}
+                out, _ = server.generate(render_chat(msgs), params, body.get("session"))
+                self._send(200, {"model": server.model_name, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ"),
+                                 "message": {"role": "assistant", "content": out.text}, "done": True,
+                                 "prompt_eval_count": int(out.metrics.get("prompt_tokens", 0)),
+                                 "eval_count": len(out.ids)})
+
+        self.httpd = ThreadingHTTPServer((host, port), Handler)
+        self.httpd.daemon_threads = True
+        self.host, self.port = self.httpd.server_address[:2]
+        self._thread: Optional[threading.Thread] = None
+
+    # ---- request plumbing -----------------------------------------------------------------
+    def sampling(self, body: Dict[str, Any]) -> SamplingParams:
+        def num(key, default, cast):
+            v = body.get(key)
+            return default if v is None else cast(v)
+        max_tokens = num("max_tokens", None, int)
+        if max_tokens is None:
+            max_tokens = num("max_completion_tokens", self.default_max_tokens, int)
+        if max_tokens < 1:
+            raise ValueError("max_tokens must be >= 1")
+        return SamplingParams(temperature=num("temperature", 0.7, float), top_p=num("top_p", 1.0, float),
+                              top_k=num("top_k", 0, int), seed=num("seed", 0, int),
+                              max_new_tokens=min(max_tokens, 8192), ignore_eos=False, stop_on_consensus=False)
+
+    def generate(self, prompt: str, body: Dict[str, Any], session: Optional[str]) -> Tuple[Any, _Request]:
+        params = self.sampling(body)
+        key = f"session:{session}" if session else f"anon:{next(self._anon)}"
+        r = self.sched.submit(_Request(key, prompt, params, persistent=bool(session)))
+        if not r.done.wait(self.sched.timeout_s + 30):
+            raise TimeoutError("generation timed out")
+        if r.error is not None:
+            raise RuntimeError(str(r.error))
+        return r.result, r
+
+    @staticmethod
+    def finish(out, r: _Request) -> str:
+        return "length" if len(out.ids) >= r.params.max_new_tokens else "stop"
+
+    @staticmethod
+    def usage(out) -> Dict[str, int]:
+        p = int(out.metrics.get("prompt_tokens", 0))
+        return {"prompt_tokens": p, "completion_tokens": len(out.ids), "total_tokens": p + len(out.ids)}
+
+    def show(self) -> Dict[str, Any]:
+        cfg = self.engine.cfg
+        arch = "llama" if cfg.arch == "llama" else cfg.arch
+        return {"modelfile": "", "details": {"family": arch, "parameter_size": cfg.name},
+                "model_info": {f"{arch}.context_length": int(min(cfg.max_pos, self.engine.kv_capacity_tokens)),
+                               f"{arch}.embedding_length": cfg.hidden, f"{arch}.block_count": cfg.n_layers}}
+
+    def metrics_text(self) -> str:
+        st = dict(self.sched.stats)
+        e = self.engine.stats
+        lines = [
+            "# TYPE roundtable_requests_total counter", f"roundtable_requests_total {st['requests']}",
+            "# TYPE roundtable_request_errors_total counter", f"roundtable_request_errors_total {st['errors']}",
+            "# TYPE roundtable_batches_total counter", f"roundtable_batches_total {st['batches']}",
+            "# TYPE roundtable_prompt_tokens_total counter", f"roundtable_prompt_tokens_total {st['prompt_tokens']}",
+            "# TYPE roundtable_completion_tokens_total counter",
+            f"roundtable_completion_tokens_total {st['completion_tokens']}",
+            "# TYPE roundtable_reused_kv_tokens_total counter", f"roundtable_reused_kv_tokens_total {st['reused_tokens']}",
+            "# TYPE roundtable_engine_busy_seconds_total counter", f"roundtable_engine_busy_seconds_total {st['busy_s']:.6f}",
+            "# TYPE roundtable_decode_tokens_total counter", f"roundtable_decode_tokens_total {e['decode_tokens']}",
+            "# TYPE roundtable_kv_capacity_tokens gauge", f"roundtable_kv_capacity_tokens {self.engine.kv_capacity_tokens}",
+            "# TYPE roundtable_engine_healthy gauge", f"roundtable_engine_healthy {int(bool(self.engine.healthy))}",
+        ]
+        return "\n".join(lines) + "\n"
+
+    # ---- lifecycle ----------------------------------------------------------------------------
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    def start(self) -> "RoundtableServer":
+        self._thread = threading.Thread(target=self.httpd.serve_forever, name="roundtable-http", daemon=True)
+        self._thread.start()
+        return self
+
+    def serve_forever(self) -> None:
+        self.httpd.serve_forever()
+
+    def close(self) -> None:
+        self.httpd.shutdown()
+        self.httpd.server_close()
+        self.sched.close()
+
+
+def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", dtype: str = "bf16",
+                 host: str = "127.0.0.1", port: int = 8000, max_batch: int = 16, max_tokens: int = 512,
+                 use_graphs: bool = True, num_blocks: Optional[int] = None) -> RoundtableServer:
+    ecfg = EngineConfig(model=model, weights=weights, device=device, dtype=dtype, use_graphs=use_graphs,
+                        max_batch=max_batch, num_blocks=num_blocks)
+    if ecfg.device == "cpu":
+        ecfg.dtype = "fp32" if dtype == "bf16" else dtype
+        ecfg.use_graphs = False
+    return RoundtableServer(Engine(ecfg), model, host, port, max_batch, max_tokens)
