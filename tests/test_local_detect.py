@@ -1,0 +1,62 @@
+"""Local checkpoint discovery (utils/local_detect.py) and its use by `roundtable init`."""
+import json
+import os
+
+from theroundtaible_amd.utils.local_detect import (detect_local_models, is_non_chat_model, match_preset,
+                                                    prettify_model_name)
+
+LLAMA8B_HF = {"model_type": "llama", "hidden_size": 4096, "num_hidden_layers": 32, "num_attention_heads": 32,
+              "num_key_value_heads": 8, "intermediate_size": 14336, "vocab_size": 128256,
+              "max_position_embeddings": 131072, "rope_theta": 500000.0, "rms_norm_eps": 1e-5}
+
+
+def _ckpt(d, hf):
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "config.json"), "w") as f:
+        json.dump(hf, f)
+    open(os.path.join(d, "model-00001-of-00001.safetensors"), "wb").close()
+
+
+def test_prettify_and_filters():
+    assert prettify_model_name("meta-llama/Meta-Llama-3-8b-instruct") == "Meta Llama 3 8B Instruct"
+    assert prettify_model_name("qwen2.5_coder-14b") == "Qwen2.5 Coder 14B"
+    assert is_non_chat_model("nomic-embed-text") and is_non_chat_model("bge-reranker-v2")
+    assert not is_non_chat_model("llama-3-8b")
+
+
+def test_detect_and_match(tmp_path):
+    _ckpt(str(tmp_path / "Meta-Llama-3-8B"), LLAMA8B_HF)
+    hub = tmp_path / "hub" / "models--mistralai--Mistral-7B-v0.3" / "snapshots" / "abc"
+    _ckpt(str(hub), dict(LLAMA8B_HF, model_type="mistral", vocab_size=32768, rope_theta=1e6,
+                         max_position_embeddings=32768))
+    _ckpt(str(tmp_path / "all-MiniLM-embed"), LLAMA8B_HF)                 # skipped: embedding model
+    os.makedirs(tmp_path / "no-weights")
+    with open(tmp_path / "no-weights" / "config.json", "w") as f:       # skipped: no safetensors
+        json.dump(LLAMA8B_HF, f)
+    found = {m.model_id: m for m in detect_local_models([str(tmp_path), str(tmp_path / "hub")])}
+    assert set(found) == {"Meta-Llama-3-8B", "mistralai/Mistral-7B-v0.3"}
+    assert found["Meta-Llama-3-8B"].preset == "llama3-8b" and found["Meta-Llama-3-8B"].overrides == {}
+    mis = found["mistralai/Mistral-7B-v0.3"]
+    assert mis.preset == "mistral-7b" and mis.overrides == {"vocab": 32768}
+    assert mis.adapter_slug() == "mistral-7b-v0-3"
+
+
+def test_match_gpt2():
+    preset, diff = match_preset({"arch": "gpt2", "n_layers": 12, "hidden": 768, "n_heads": 12, "n_kv_heads": 12,
+                                 "head_dim": 64, "ffn": 3072, "vocab": 50257, "max_pos": 1024, "rope_theta": 0.0,
+                                 "norm_eps": 1e-5, "tie_embeddings": True})
+    assert preset == "gpt2-small" and diff == {"max_pos": 1024}
+
+
+def test_init_seats_local_checkpoints(tmp_path, monkeypatch):
+    from theroundtaible_amd.cli import main
+    _ckpt(str(tmp_path / "models" / "Meta-Llama-3-8B"), LLAMA8B_HF)
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("HF_HOME", str(tmp_path / "nohf"))
+    monkeypatch.delenv("ROUNDTABLE_MODELS_DIR", raising=False)
+    assert main(["--quiet", "init", "--yes", "--knights", "2", "--local-models"]) == 0
+    cfg = json.load(open(tmp_path / ".roundtable" / "config.json"))
+    adapters = [k["adapter"] for k in cfg["knights"]]
+    assert "local-llm-meta-llama-3-8b" in adapters
+    eng = cfg["adapter_config"]["local-llm-meta-llama-3-8b"]["engine"]
+    assert eng["model"] == "llama3-8b" and eng["weights"].endswith("Meta-Llama-3-8B")

@@ -7,7 +7,7 @@ import pytest
 from theroundtaible_amd import store
 from theroundtaible_amd.knights.fake import FakeBackend, consensus_reply
 from theroundtaible_amd.orchestrator import (Orchestrator, RunOptions, compute_allowed_files,
-                                             run_tables_parallel, select_lead_knight)
+                                             run_tables_parallel, run_tables_sequential, select_lead_knight)
 from theroundtaible_amd.types import ConsensusBlock, ContinueOptions, KnightConfig, RoundtableConfig
 
 
@@ -172,3 +172,31 @@ def test_run_tables_lockstep(tmp_path):
     res = run_tables_parallel(tabs, ["A", "B"])
     assert res[0].consensus and res[0].rounds == 1
     assert not res[1].consensus and res[1].rounds == 3
+
+
+def test_run_tables_sequential_lockstep_matches_single_table_runs(tmp_path):
+    """Lockstep sequential tables == each table run alone (same visibility, same decisions)."""
+    def make(t):
+        sc = {k: [consensus_reply(9 if t == 0 else 4)] * 3 for k in ("Claude", "Gemini", "GPT")}
+        return Orchestrator(config(n=3, max_rounds=3, mode="sequential"), backends(sc), str(tmp_path),
+                            options=RunOptions(shuffle_seed=t))
+    res = run_tables_sequential([make(0), make(1)], ["A", "B"])
+    assert res[0].consensus and res[0].rounds == 1
+    assert not res[1].consensus and res[1].rounds == 3
+    alone = make(1).run("B")
+    assert alone.rounds == res[1].rounds and alone.consensus == res[1].consensus
+
+
+def test_sequential_visibility_within_round(tmp_path):
+    """Sequential mode: the second speaker's prompt contains the first speaker's reply."""
+    seen = {}
+
+    class Spy(FakeBackend):
+        def _run(self, req, timeout_s):
+            seen[self.name] = str(req.prompt)
+            return super()._run(req, timeout_s)
+    sc = {"Claude": ["EERSTE-ANTWOORD-XYZ"], "Gemini": ["tweede"]}
+    bk = {f"fake-{k.lower()}": Spy(name=k, script={k: v}) for k, v in sc.items()}
+    o = Orchestrator(config(n=2, max_rounds=1, mode="sequential"), bk, str(tmp_path))
+    run_tables_sequential([o], ["T"])
+    assert "EERSTE-ANTWOORD-XYZ" in seen["Gemini"] and "EERSTE-ANTWOORD-XYZ" not in seen["Claude"]

@@ -73,11 +73,24 @@ def cmd_init(args, ui: UI) -> int:
     for j in range(extra):
         knights.append({"name": f"Knight{j + 4}", "adapter": f"local-llm-knight{j + 4}",
                         "capabilities": ["code", "logic"]})
+    # local checkpoints (init.ts:361-373 seats detected local models as local-llm-<slug> knights)
+    from .utils.local_detect import detect_local_models
+    local_engine = {}
+    found = detect_local_models(project_root=root)
+    if found:
+        ui.ok(f"  Found {len(found)} local checkpoint(s): " + ", ".join(m.name for m in found))
+    for m in found:
+        if m.preset is None:
+            continue
+        if args.local_models or (not args.yes and confirm(ui, f"  Seat {m.name} ({m.preset}) at the table?", False)):
+            adapter = f"local-llm-{m.adapter_slug()}"
+            knights.append({"name": m.name, "adapter": adapter, "capabilities": ["code", "logic"]})
+            local_engine[adapter] = {"model": m.preset, "weights": m.path, "model_overrides": m.overrides}
     if not knights:
         ui.error("\n  A roundtable with no knights is just a table.")
         return 0
     for i, k in enumerate(knights):
-        eng = {"model": args.model, "tp": args.tp}
+        eng = dict(local_engine.get(k["adapter"], {"model": args.model}), tp=args.tp)
         if gpus:
             g0 = (i * args.tp) % len(gpus)
             eng["gpus"] = [(g0 + t) % len(gpus) for t in range(args.tp)]
@@ -90,7 +103,8 @@ def cmd_init(args, ui: UI) -> int:
                           adapter_engine=adapter_engine)
     for k in knights:
         if k["adapter"].startswith("local-llm"):
-            cfg["adapter_config"][k["adapter"]].update({"endpoint": "engine://local", "model": args.model,
+            model = adapter_engine[k["adapter"]]["model"]
+            cfg["adapter_config"][k["adapter"]].update({"endpoint": "engine://local", "model": model,
                                                         "name": k["name"]})
     os.makedirs(os.path.join(rt, "sessions"), exist_ok=True)
     write_config(root, cfg)
@@ -479,6 +493,8 @@ def build_parser() -> argparse.ArgumentParser:
     i.add_argument("--knights", type=int, default=3)
     i.add_argument("--tp", type=int, default=1)
     i.add_argument("--max-new-tokens", type=int, default=512)
+    i.add_argument("--local-models", action="store_true",
+                   help="seat every detected local checkpoint (ROUNDTABLE_MODELS_DIR, ./models, HF cache)")
     i.set_defaults(fn=cmd_init)
     d = sub.add_parser("discuss", help="Start a discussion between knights")
     d.add_argument("topic")

@@ -73,7 +73,8 @@ class BackendFactory:
                             block_size=int(st.get("kv_block_size", 32)),
                             kv_cache_fraction=float(st.get("kv_cache_fraction", 0.85)),
                             max_kv_tokens=st.get("max_kv_tokens"),
-                            use_graphs=bool(st.get("use_graphs", True)))
+                            use_graphs=bool(st.get("use_graphs", True)),
+                            model_overrides=dict(st.get("model_overrides") or {}))
         if ecfg.device == "cpu":
             ecfg.dtype = "fp32" if st.get("dtype") in (None, "bf16") and st.get("cpu_fp32", True) else ecfg.dtype
             ecfg.use_graphs = False

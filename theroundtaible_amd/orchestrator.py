@@ -310,24 +310,37 @@ class Orchestrator:
             self._record(knight, self.backends[knight.adapter], rnd, out, self.all_rounds, self.latest,
                          self.session_path, self.tool_state)
 
+    def plan_turn(self, rnd: int, knight: KnightConfig) -> Optional[Tuple[KnightConfig, KnightBackend, TurnRequest]]:
+        """One sequential-mode turn: the prompt sees every entry recorded so far (orchestrator.ts:397-425)."""
+        backend = self.backends.get(knight.adapter)
+        if backend is None:
+            self.ui.warn(f"  {knight.name} didn't show up today. Typical.")
+            return None
+        store.update_status(self.session_path, phase="discussing", current_knight=knight.name, round=rnd)
+        prompt = self._prompt(knight, self.ctx, self.all_rounds, rnd, self.cont is not None,
+                              self.tool_state["files"], self.tool_state["commands"])
+        msgs = THINKING.get(knight.name, ["is thinking...", "prepares their response..."])
+        self.ui.print(f"  {knight.name} {msgs[self.rng.randrange(len(msgs))]}", "dim")
+        return knight, backend, TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens)
+
+    def record_turn(self, rnd: int, knight: KnightConfig, backend: KnightBackend,
+                    res: Union[TurnResult, BaseException]) -> None:
+        if isinstance(res, BaseException):
+            self._report_failure(knight, res)   # skip the knight, continue the round
+            return
+        self._record(knight, backend, rnd, res, self.all_rounds, self.latest, self.session_path, self.tool_state)
+
     def run_sequential_round(self, rnd: int, order: Sequence[KnightConfig]) -> None:
         for knight in order:
-            backend = self.backends.get(knight.adapter)
-            if backend is None:
-                self.ui.warn(f"  {knight.name} didn't show up today. Typical.")
+            planned = self.plan_turn(rnd, knight)
+            if planned is None:
                 continue
-            store.update_status(self.session_path, phase="discussing", current_knight=knight.name, round=rnd)
-            prompt = self._prompt(knight, self.ctx, self.all_rounds, rnd, self.cont is not None,
-                                  self.tool_state["files"], self.tool_state["commands"])
-            msgs = THINKING.get(knight.name, ["is thinking...", "prepares their response..."])
-            self.ui.print(f"  {knight.name} {msgs[self.rng.randrange(len(msgs))]}", "dim")
-            req = TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens)
+            _, backend, req = planned
             try:
                 res = self._execute_with_fallback(knight, backend, req, self.timeout_s)
             except Exception as e:  # noqa: BLE001 - skip the knight, continue the round
-                self._report_failure(knight, e)
-                continue
-            self._record(knight, backend, rnd, res, self.all_rounds, self.latest, self.session_path, self.tool_state)
+                res = e
+            self.record_turn(rnd, knight, backend, res)
 
     def execute_plan(self, plan) -> Dict[str, Union[TurnResult, BaseException]]:
         """Run planned turns grouped by backend group (one batched decode per engine), groups concurrently."""
@@ -463,6 +476,46 @@ def run_tables_parallel(tables: Sequence[Orchestrator], topics: Sequence[str],
         results = open_[0].execute_plan(merged)
         for t in open_:
             t.record_parallel(rnd, orders[id(t)], results)
+        ms = (time.perf_counter() - t0) * 1e3
+        still = []
+        for t in open_:
+            if t.end_round(rnd, ms) is None and rnd < t.end:
+                still.append(t)
+            elif t.result is None:
+                t.finish()
+        open_ = still
+        if on_round is not None:
+            on_round(rnd, ms)
+        rnd += 1
+    return [t.finish() for t in tables]
+
+
+def run_tables_sequential(tables: Sequence[Orchestrator], topics: Sequence[str],
+                          on_round: Optional[Callable[[int, float], None]] = None) -> List[SessionResult]:
+    """Several independent tables in reference (sequential) round mode, in lockstep by
+    speaking slot: the k-th speaker of every open table runs in one batch, each seeing its
+    own table's earlier speakers of the round (orchestrator.ts:361-536 visibility)."""
+    for i, (t, topic) in enumerate(zip(tables, topics)):
+        if len(tables) > 1 and not t.table_id:
+            t.table_id = f"t{i}/"
+        t.begin(topic)
+    open_ = list(tables)
+    rnd = min(t.start for t in tables)
+    while open_:
+        t0 = time.perf_counter()
+        orders = {id(t): t.round_order(rnd) for t in open_}
+        for k in range(max(len(o) for o in orders.values())):
+            planned = []
+            for t in open_:
+                if k < len(orders[id(t)]):
+                    item = t.plan_turn(rnd, orders[id(t)][k])
+                    if item is not None:
+                        planned.append((t, item))
+            if not planned:
+                continue
+            results = open_[0].execute_plan([item for _, item in planned])
+            for t, (knight, backend, req) in planned:
+                t.record_turn(rnd, knight, backend, results[req.seq_key])
         ms = (time.perf_counter() - t0) * 1e3
         still = []
         for t in open_:

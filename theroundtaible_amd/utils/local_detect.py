@@ -1,0 +1,148 @@
+"""Local model discovery: find HF-format checkpoints on this machine and map them to engine presets.
+
+The reference discovers *running model servers* (`src/utils/local-detect.ts:103-134`: probe
+LM Studio / Ollama ports, fall back to ``ollama list``) and seats each chat model as a
+``local-llm-<slug>`` knight (`src/commands/init.ts:361-373`). Here the engine itself hosts
+knights, so discovery looks for *weights*: directories holding ``config.json`` plus
+``*.safetensors`` under
+
+* ``$ROUNDTABLE_MODELS_DIR`` (``os.pathsep``-separated),
+* ``./models`` of the project,
+* the Hugging Face hub cache (``$HF_HOME``/``~/.cache/huggingface/hub/models--*/snapshots/*``).
+
+Each hit is read (JSON only — nothing from a checkpoint is executed) and matched to a preset
+(Llama-3-8B/70B, Mistral-7B, GPT-2) or described as a preset plus shape overrides; embedding /
+reranker / speech models are skipped, as the reference's ``isNonChatModel`` does.
+Running servers are still supported from the other side: ``roundtable serve`` speaks the
+LM Studio / Ollama dialects.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Any, Dict, Iterable, List, Optional
+
+from ..models.config import PRESETS
+
+NON_CHAT = re.compile(r"(^|[^a-z])(embed|embedding|tts|whisper|rerank|reranker|clip)([^a-z]|$)", re.I)
+
+
+@dataclass
+class LocalModel:
+    name: str                 # display name, e.g. "Meta Llama 3 8B Instruct"
+    model_id: str             # directory-derived id, e.g. "meta-llama/Meta-Llama-3-8B-Instruct"
+    path: str                 # checkpoint directory (engine ``weights`` spec)
+    preset: Optional[str]     # matching engine preset, or the closest architecture preset
+    overrides: Dict[str, Any] = field(default_factory=dict)   # ModelConfig fields that differ
+    source: str = "checkpoint"
+
+    def adapter_slug(self) -> str:
+        return re.sub(r"[^a-z0-9]+", "-", self.model_id.split("/")[-1].lower()).strip("-")
+
+
+def prettify_model_name(model_id: str) -> str:
+    """``"meta-llama/Meta-Llama-3-8B-instruct"`` -> ``"Meta Llama 3 8B Instruct"``."""
+    raw = model_id.rsplit("/", 1)[-1]
+    words = [w for w in re.split(r"[-_\s]+", raw) if w]
+    out = []
+    for w in words:
+        if re.fullmatch(r"\d+(\.\d+)?[bBmM]", w):
+            out.append(w[:-1] + w[-1].upper())
+        else:
+            out.append(w[:1].upper() + w[1:])
+    return " ".join(out)
+
+
+def is_non_chat_model(model_id: str) -> bool:
+    return bool(NON_CHAT.search(model_id))
+
+
+def _shape_from_hf(hf: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    mt = str(hf.get("model_type", "")).lower()
+    if mt in ("llama", "mistral"):
+        h = int(hf["hidden_size"])
+        nh = int(hf["num_attention_heads"])
+        return {"arch": "llama", "n_layers": int(hf["num_hidden_layers"]), "hidden": h, "n_heads": nh,
+                "n_kv_heads": int(hf.get("num_key_value_heads", nh)), "head_dim": int(hf.get("head_dim", h // nh)),
+                "ffn": int(hf["intermediate_size"]), "vocab": int(hf["vocab_size"]),
+                "max_pos": int(hf.get("max_position_embeddings", 8192)),
+                "rope_theta": float(hf.get("rope_theta", 10000.0)), "norm_eps": float(hf.get("rms_norm_eps", 1e-5)),
+                "tie_embeddings": bool(hf.get("tie_word_embeddings", False))}
+    if mt == "gpt2":
+        h = int(hf["n_embd"])
+        nh = int(hf["n_head"])
+        return {"arch": "gpt2", "n_layers": int(hf["n_layer"]), "hidden": h, "n_heads": nh, "n_kv_heads": nh,
+                "head_dim": h // nh, "ffn": int(hf.get("n_inner") or 4 * h), "vocab": int(hf["vocab_size"]),
+                "max_pos": int(hf.get("n_positions", 1024)), "rope_theta": 0.0,
+                "norm_eps": float(hf.get("layer_norm_epsilon", 1e-5)), "tie_embeddings": True}
+    return None
+
+
+def match_preset(shape: Dict[str, Any]) -> (Optional[str], Dict[str, Any]):
+    """Preset with the same architecture and fewest differing fields, plus those differences."""
+    best, best_diff = None, None
+    for name, cfg in PRESETS.items():
+        if cfg.arch != shape["arch"] or name.startswith("tiny"):
+            continue
+        diff = {k: v for k, v in shape.items() if k != "arch" and getattr(cfg, k) != v}
+        if best_diff is None or len(diff) < len(best_diff):
+            best, best_diff = name, diff
+    return best, (best_diff or {})
+
+
+def _model_id(path: str) -> str:
+    m = re.search(r"models--([^/]+)--([^/]+)/snapshots/", path.replace(os.sep, "/"))
+    if m:
+        return f"{m.group(1)}/{m.group(2)}"
+    return os.path.basename(os.path.normpath(path))
+
+
+def default_search_dirs(project_root: Optional[str] = None) -> List[str]:
+    dirs: List[str] = []
+    env = os.environ.get("ROUNDTABLE_MODELS_DIR")
+    if env:
+        dirs.extend(d for d in env.split(os.pathsep) if d)
+    if project_root:
+        dirs.append(os.path.join(project_root, "models"))
+    hf_home = os.environ.get("HF_HOME") or os.path.join(os.path.expanduser("~"), ".cache", "huggingface")
+    dirs.append(os.path.join(hf_home, "hub"))
+    return dirs
+
+
+def _candidates(root: str) -> Iterable[str]:
+    if not os.path.isdir(root):
+        return []
+    pats = [os.path.join(root, "config.json"), os.path.join(root, "*", "config.json"),
+            os.path.join(root, "*", "*", "config.json"), os.path.join(root, "models--*", "snapshots", "*", "config.json")]
+    seen = set()
+    for pat in pats:
+        for cfg in sorted(glob.glob(pat)):
+            d = os.path.dirname(cfg)
+            if d not in seen and glob.glob(os.path.join(d, "*.safetensors")):
+                seen.add(d)
+                yield d
+
+
+def detect_local_models(search_dirs: Optional[List[str]] = None, project_root: Optional[str] = None) -> List[LocalModel]:
+    out: List[LocalModel] = []
+    seen_ids = set()
+    for root in (search_dirs if search_dirs is not None else default_search_dirs(project_root)):
+        for d in _candidates(root):
+            mid = _model_id(d)
+            if mid in seen_ids or is_non_chat_model(mid):
+                continue
+            try:
+                with open(os.path.join(d, "config.json"), encoding="utf-8") as f:
+                    hf = json.load(f)
+                shape = _shape_from_hf(hf)
+            except (OSError, ValueError, KeyError, TypeError):
+                continue
+            if shape is None:
+                continue
+            preset, diff = match_preset(shape)
+            seen_ids.add(mid)
+            out.append(LocalModel(prettify_model_name(mid), mid, d, preset, diff))
+    return out
