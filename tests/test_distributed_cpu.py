@@ -108,3 +108,36 @@ def test_spmd_bench_two_ranks():
     assert out["n_gpus"] == 2 and out["config"]["knights"] == 6 and out["config"]["tables"] == 2
     assert out["detail"]["decode_tokens"] == 6 * 8 * 2
     assert out["value"] > 0 and out["scaling"] == "weak"
+
+
+def test_cli_discuss_under_torchrun_with_tp_knight(tmp_path):
+    """`torchrun -m theroundtaible_amd discuss` (SPMD): one knight per rank plus a TP=2 knight
+    spanning both ranks; rank 0 writes the session, every knight's turn lands in it."""
+    cfg = {"version": "1.0", "project": "spmd", "language": "nl",
+           "knights": [{"name": "Alfa", "adapter": "local-llm-alfa", "capabilities": ["x"], "priority": 1},
+                       {"name": "Beta", "adapter": "local-llm-beta", "capabilities": ["x"], "priority": 2},
+                       {"name": "Groot", "adapter": "local-llm-groot", "capabilities": ["x"], "priority": 3}],
+           "rules": {"max_rounds": 2, "consensus_threshold": 9, "timeout_per_turn_seconds": 300,
+                     "escalate_to_user_after": 5, "auto_execute": False, "ignore": [".git"],
+                     "round_mode": "sequential"},
+           "chronicle": ".roundtable/chronicle.md",
+           "engine": {"default_model": "tiny-llama", "weights": "random-full:4", "max_new_tokens": 6,
+                      "ignore_eos": True, "temperature": 0.0},
+           "adapter_config": {"local-llm-alfa": {"engine": {"gpus": [0]}},
+                              "local-llm-beta": {"engine": {"gpus": [1]}},
+                              "local-llm-groot": {"engine": {"gpus": [0, 1], "tp": 2}}}}
+    os.makedirs(tmp_path / ".roundtable" / "sessions")
+    (tmp_path / ".roundtable" / "config.json").write_text(json.dumps(cfg))
+    (tmp_path / ".roundtable" / "chronicle.md").write_text("# Chronicle\n")
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", "-m", "theroundtaible_amd", "--quiet",
+           "discuss", "SPMD onderwerp", "--no-read-codebase", "--choice", "4"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    sessions = os.listdir(tmp_path / ".roundtable" / "sessions")
+    assert len(sessions) == 1                                   # only rank 0 wrote into the project
+    disc = (tmp_path / ".roundtable" / "sessions" / sessions[0] / "discussion.md").read_text()
+    for name in ("Alfa", "Beta", "Groot"):
+        assert disc.count(name) >= 2, name                       # both rounds, every knight (TP knight too)

@@ -21,12 +21,33 @@ from .utils.ui import UI
 
 
 # ---- prompts ------------------------------------------------------------------------------------
+_CLUSTER = None   # set when discuss/summon run under torchrun (one process per GPU, SPMD)
+
+
+def spmd_cluster():
+    """The torchrun cluster for SPMD commands (None for a single-process run)."""
+    global _CLUSTER
+    if _CLUSTER is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        from .parallel.cluster import init_cluster
+        _CLUSTER = init_cluster(prefer_gpu=True)
+    return _CLUSTER
+
+
+def is_writer() -> bool:
+    """Only rank 0 writes project files / asks the King in an SPMD run."""
+    return _CLUSTER is None or _CLUSTER.rank == 0
+
+
 def ask(ui: UI, question: str, default: str = "") -> str:
-    ui.print(question)
-    try:
-        line = sys.stdin.readline()
-    except (EOFError, OSError):
-        return default
+    line = None
+    if is_writer():
+        ui.print(question)
+        try:
+            line = sys.stdin.readline()
+        except (EOFError, OSError):
+            line = None
+    if _CLUSTER is not None and _CLUSTER.distributed:
+        line = _CLUSTER.broadcast_object(line, src=0)   # every rank takes the King's answer
     if not line:
         return default
     return line.strip() or default
@@ -153,9 +174,25 @@ def discuss(topic: str, args, ui: UI) -> int:
     from .orchestrator import Orchestrator, RunOptions
     root = os.getcwd()
     config = load_config(root)
+    cl = spmd_cluster()
+    if cl is not None and cl.rank != 0:
+        ui = UI(quiet=True)
     ui.print(f'\n  Topic: "{topic}"\n', "bold")
     ui.dim("  Summoning the knights to the table...\n")
-    backends, factory = _make_backends(config, ui, getattr(args, "device", None))
+    store_root = root
+    if cl is not None and cl.distributed:
+        # SPMD: every rank runs this program; knights run where they are placed (knights/spmd.py)
+        import tempfile
+        from .knights.spmd import build_spmd_backends
+        backends, _pool = build_spmd_backends(config, cl, ui, args.max_new_tokens)
+        factory = None
+        if cl.rank != 0:
+            store_root = tempfile.mkdtemp(prefix=f"roundtable-rank{cl.rank}-")   # mirror writes, discarded
+        if args.seed is None:   # one speaking order for all ranks
+            import random
+            args.seed = cl.broadcast_object(random.SystemRandom().randrange(1 << 31) if cl.rank == 0 else None)
+    else:
+        backends, factory = _make_backends(config, ui, getattr(args, "device", None))
     if not backends:
         raise ConfigError("A roundtable with no knights is just a table.",
                           hint="Configure at least one knight adapter with an engine model.")
@@ -168,7 +205,7 @@ def discuss(topic: str, args, ui: UI) -> int:
         read_src = args.read_codebase
     opts = RunOptions(read_source=read_src, shuffle_seed=args.seed, round_mode=args.round_mode,
                       prompt_layout=args.layout, max_new_tokens=args.max_new_tokens)
-    orch = Orchestrator(config, backends, root, ui, opts, backend_factory=factory)
+    orch = Orchestrator(config, backends, root, ui, opts, backend_factory=factory, store_root=store_root)
     cont = None
     if args.resume:
         cont = _resume_state(root, args.resume)
@@ -220,11 +257,13 @@ def _kings_decree(root, topic, result, args, ui: UI) -> None:
         return
     name = os.path.basename(result.session_path)
     if choice == "later":
-        e = store.add_decree_entry(root, "deferred", name, topic, args.decree_reason)
-        ui.dim(f"  Decree {e['id']}: deferred.")
+        if is_writer():
+            e = store.add_decree_entry(root, "deferred", name, topic, args.decree_reason)
+            ui.dim(f"  Decree {e['id']}: deferred.")
     elif choice == "reject":
-        e = store.add_decree_entry(root, "rejected_no_apply", name, topic, args.decree_reason)
-        ui.dim(f"  Decree {e['id']}: rejected, no apply.")
+        if is_writer():
+            e = store.add_decree_entry(root, "rejected_no_apply", name, topic, args.decree_reason)
+            ui.dim(f"  Decree {e['id']}: rejected, no apply.")
 
 
 def _no_consensus(root, topic, result, args, ui: UI) -> str:

@@ -96,7 +96,14 @@ class Engine:
             weights = materialize(self.cfg, ecfg.weights, self.device, self.dtype, self.tp)
             self.model = build_model(self.cfg, weights, self.device, self.dtype, self.tp)
             if self.on_gpu and hasattr(self.model, "decode_weights") and self.tp.size == 1:
-                self.model.decode_weights()   # shuffled decode copies before sizing the KV pool
+                # shuffled decode copies (+1x weight memory) before sizing the KV pool — only when they
+                # leave room for KV: a 70B knight on one GPU keeps the unfused (hipBLASLt) decode path
+                wbytes = sum(t.numel() * t.element_size() for t in weights.values())
+                total = torch.cuda.get_device_properties(self.device).total_memory
+                if 2 * wbytes <= 0.7 * total:
+                    self.model.decode_weights()
+                else:
+                    self.model.use_fused = False
         self.load_s = time.perf_counter() - t0
         self.kv = self._alloc_kv()
         self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}
