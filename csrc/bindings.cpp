@@ -26,10 +26,11 @@ int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, 
 int sample_workspace_floats(int B);
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, const void* rope, hipStream_t stream);
+                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream);
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
-                            const int64_t* slots, int Hq, int Hkv, int D, int BS, hipStream_t stream);
+                            const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
+                            hipStream_t stream);
 int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
                        const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
                        int64_t vocab, hipStream_t stream);
@@ -209,8 +210,26 @@ void sample(torch::Tensor out, torch::Tensor logits, torch::Tensor temperature, 
                 seeds.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), ws.data_ptr<float>(), cur_stream());
 }
 // Ws: fragment-shuffled weight [N_w, K] (N_w = 2N for SwiGLU); out [M, N] (unused for RESID).
+// PRO_NORM_ADD (pro=2): x2 [M,K] is added to x before the norm; xout (optional) receives x + x2.
+std::pair<const void*, void*> add_operands(const torch::Tensor& x, int64_t pro, const c10::optional<torch::Tensor>& x2,
+                                           const c10::optional<torch::Tensor>& xout) {
+  if (pro != 2) return {nullptr, nullptr};
+  TORCH_CHECK(x2.has_value(), "pro=NORM_ADD needs x2");
+  check_bf16(*x2, "x2");
+  TORCH_CHECK(x2->sizes() == x.sizes(), "x2 must match x");
+  void* xo = nullptr;
+  if (xout.has_value()) {
+    check_bf16(*xout, "xout");
+    TORCH_CHECK(xout->sizes() == x.sizes(), "xout must match x");
+    TORCH_CHECK(xout->data_ptr() != x.data_ptr() && xout->data_ptr() != x2->data_ptr(), "xout must not alias x / x2");
+    xo = xout->data_ptr();
+  }
+  return {x2->data_ptr(), xo};
+}
+
 void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t pro, int64_t epi,
-                 c10::optional<torch::Tensor> res, double eps) {
+                 c10::optional<torch::Tensor> res, double eps, c10::optional<torch::Tensor> x2,
+                 c10::optional<torch::Tensor> xout) {
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
   TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm: x [M,K], Ws [N,K]");
@@ -235,15 +254,18 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
     TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N, "out must be [M, N]");
     ldo = out.stride(0);
   }
+  const auto addo = add_operands(x, pro, x2, xout);
   const int rc = launch_skinny_gemm(epi == 1 ? nullptr : out.data_ptr(), x.data_ptr(), Ws.data_ptr(), rp, (int)M,
-                                    (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, nullptr, cur_stream());
+                                    (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, nullptr, addo.first,
+                                    addo.second, cur_stream());
   TORCH_CHECK(rc == 0, "skinny_gemm: unsupported configuration (rc=", rc, ")");
 }
 
 // qkv decode projection with the RoPE + paged-cache epilogue (Ws built with rope_heads = Hq + Hkv).
 void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, int64_t pro, torch::Tensor positions,
                       torch::Tensor cos_sin, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots,
-                      int64_t Hq, int64_t Hkv, int64_t D, double eps) {
+                      int64_t Hq, int64_t Hkv, int64_t D, double eps, c10::optional<torch::Tensor> x2,
+                      c10::optional<torch::Tensor> xout) {
   check_bf16(q_out, "q_out");
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
@@ -258,10 +280,12 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "positions/slots must cover M rows");
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
   check_caches(k_cache, v_cache, Hkv, D);
+  const auto addo = add_operands(x, pro, x2, xout);
   const int rc = launch_skinny_gemm_rope(q_out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)M, (int)K, (int)pro,
                                          (float)eps, positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                          k_cache.data_ptr(), v_cache.data_ptr(), slots.data_ptr<int64_t>(), (int)Hq,
-                                         (int)Hkv, (int)D, (int)k_cache.size(2), cur_stream());
+                                         (int)Hkv, (int)D, (int)k_cache.size(2), addo.first, addo.second,
+                                         cur_stream());
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
@@ -332,13 +356,16 @@ void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tens
 PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm, "decode GEMM (M<=16), shuffled weights, fused norm / resid / swiglu",
         py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("epi"), py::arg("res") = py::none(),
-        py::arg("eps") = 1e-5);
+        py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none());
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
         py::arg("rope_heads") = 0, py::arg("head_dim") = 0);
   m.def("decode_prep", &decode_prep);
   m.def("decode_advance", &decode_advance);
   m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));
-  m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write");
+  m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write",
+        py::arg("q_out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("positions"), py::arg("cos_sin"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
+        py::arg("eps"), py::arg("x2") = py::none(), py::arg("xout") = py::none());
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);

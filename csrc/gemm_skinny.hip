@@ -39,7 +39,9 @@ using rt::float4_;
 using rt::short8;
 
 
-enum : int { PRO_PLAIN = 0, PRO_NORM = 1 };
+// PRO_NORM_ADD (tensor-parallel decode): the A operand is bf16(x + x2) — the residual plus the
+// all-reduced row-parallel partial — and workgroup 0 writes that sum to `xo` (the next residual).
+enum : int { PRO_PLAIN = 0, PRO_NORM = 1, PRO_NORM_ADD = 2 };
 enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_ROPE = 3 };
 
 struct RopeEpi {
@@ -54,16 +56,18 @@ struct RopeEpi {
 RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
 
 // U = k-steps per wave per pipeline stage (x2 stages in flight)
-template <int EPI, int U>
+template <int PRO, int EPI, int U>
 struct Stage {
   short8 w[U];
   short8 w2[(EPI == EPI_SWIGLU) ? U : 1];
   short8 a[U];
+  short8 b[(PRO == PRO_NORM_ADD) ? U : 1];
 };
 
-template <int EPI, int NW, int U>
-RT_DEVICE void issue(Stage<EPI, U>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2,
-                     const uint16_t* __restrict__ xr, bool row_ok, int s0, int nsteps, int lane) {
+template <int PRO, int EPI, int NW, int U>
+RT_DEVICE void issue(Stage<PRO, EPI, U>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2,
+                     const uint16_t* __restrict__ xr, const uint16_t* __restrict__ xr2, bool row_ok, int s0,
+                     int nsteps, int lane) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int s = s0 + NW * u;
@@ -76,22 +80,32 @@ RT_DEVICE void issue(Stage<EPI, U>& st, const short8* __restrict__ wt, const sho
   for (int u = 0; u < U; ++u) {
     const int s = s0 + NW * u;
     st.a[u] = (row_ok && s < nsteps) ? *reinterpret_cast<const short8*>(xr + s * 32) : short8{0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (PRO == PRO_NORM_ADD)
+      st.b[u] = (row_ok && s < nsteps) ? *reinterpret_cast<const short8*>(xr2 + s * 32) : short8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 }
 
 template <int PRO, int EPI, int NW, int U>
-RT_DEVICE void consume(const Stage<EPI, U>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps) {
+RT_DEVICE void consume(const Stage<PRO, EPI, U>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps,
+                       uint16_t* __restrict__ xo_r) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (s0 + NW * u < nsteps) {
-      const bf16x8 a = __builtin_bit_cast(bf16x8, st.a[u]);
+      short8 av = st.a[u];
+      if constexpr (PRO == PRO_NORM_ADD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          av[j] = (short)rt::f2bf(rt::bf2f((uint16_t)st.a[u][j]) + rt::bf2f((uint16_t)st.b[u][j]));
+        if (xo_r != nullptr) *reinterpret_cast<short8*>(xo_r + (s0 + NW * u) * 32) = av;
+      }
+      const bf16x8 a = __builtin_bit_cast(bf16x8, av);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u]), acc, 0, 0, 0);
       if constexpr (EPI == EPI_SWIGLU)
         acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u]), acc2, 0, 0, 0);
-      if constexpr (PRO == PRO_NORM) {
+      if constexpr (PRO != PRO_PLAIN) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float f = rt::bf2f((uint16_t)st.a[u][j]);
+          const float f = rt::bf2f((uint16_t)av[j]);
           ssq = fmaf(f, f, ssq);
         }
       }
@@ -102,7 +116,8 @@ RT_DEVICE void consume(const Stage<EPI, U>& st, float4_& acc, float4_& acc2, flo
 template <int PRO, int EPI, int NW, int U>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
                                                           const short8* __restrict__ Ws, uint16_t* __restrict__ res,
-                                                          int M, int N, int K, int ldo, float eps, RopeEpi re) {
+                                                          int M, int N, int K, int ldo, float eps, RopeEpi re,
+                                                          const uint16_t* __restrict__ x2, uint16_t* __restrict__ xo) {
   __shared__ float red[NW][(EPI == EPI_SWIGLU) ? 2 : 1][16][17];
   __shared__ float sq[NW][16];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -111,23 +126,27 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restri
   const int nsteps = K / 32;
   const bool row_ok = r < M;
   const uint16_t* xr = x + (size_t)(row_ok ? r : 0) * K + 8 * g;
+  const uint16_t* xr2 = (PRO == PRO_NORM_ADD) ? x2 + (size_t)(row_ok ? r : 0) * K + 8 * g : nullptr;
+  // workgroup 0 publishes the summed residual (rows < M only)
+  uint16_t* xo_r = (PRO == PRO_NORM_ADD && blockIdx.x == 0 && row_ok && xo != nullptr) ? xo + (size_t)r * K + 8 * g
+                                                                                      : nullptr;
   const short8* wt = Ws + (size_t)tile * nsteps * 64;
   const short8* wt2 = (EPI == EPI_SWIGLU) ? Ws + (size_t)(N / 16 + tile) * nsteps * 64 : nullptr;
 
   float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
   float ssq = 0.f;
-  Stage<EPI, U> st0, st1;
+  Stage<PRO, EPI, U> st0, st1;
   int s = wid;
-  issue<EPI, NW, U>(st0, wt, wt2, xr, row_ok, s, nsteps, lane);
+  issue<PRO, EPI, NW, U>(st0, wt, wt2, xr, xr2, row_ok, s, nsteps, lane);
   for (;;) {
     const int sn = s + NW * U;
-    if (sn < nsteps) issue<EPI, NW, U>(st1, wt, wt2, xr, row_ok, sn, nsteps, lane);
-    consume<PRO, EPI, NW, U>(st0, acc, acc2, ssq, s, nsteps);
+    if (sn < nsteps) issue<PRO, EPI, NW, U>(st1, wt, wt2, xr, xr2, row_ok, sn, nsteps, lane);
+    consume<PRO, EPI, NW, U>(st0, acc, acc2, ssq, s, nsteps, xo_r);
     if (sn >= nsteps) break;
     s = sn;
     const int sn2 = s + NW * U;
-    if (sn2 < nsteps) issue<EPI, NW, U>(st0, wt, wt2, xr, row_ok, sn2, nsteps, lane);
-    consume<PRO, EPI, NW, U>(st1, acc, acc2, ssq, s, nsteps);
+    if (sn2 < nsteps) issue<PRO, EPI, NW, U>(st0, wt, wt2, xr, xr2, row_ok, sn2, nsteps, lane);
+    consume<PRO, EPI, NW, U>(st1, acc, acc2, ssq, s, nsteps, xo_r);
     if (sn2 >= nsteps) break;
     s = sn2;
   }
@@ -138,7 +157,7 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restri
     red[wid][0][4 * g + i][r] = acc[i];
     if constexpr (EPI == EPI_SWIGLU) red[wid][(EPI == EPI_SWIGLU) ? 1 : 0][4 * g + i][r] = acc2[i];
   }
-  if constexpr (PRO == PRO_NORM) {
+  if constexpr (PRO != PRO_PLAIN) {
     ssq += __shfl_xor(ssq, 16, 64);
     ssq += __shfl_xor(ssq, 32, 64);
     if (g == 0) sq[wid][r] = ssq;
@@ -150,10 +169,10 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(uint16_t* __restri
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       v += red[w][0][m][n];
-      if constexpr (PRO == PRO_NORM) ss += sq[w][m];
+      if constexpr (PRO != PRO_PLAIN) ss += sq[w][m];
     }
     float inv = 1.f;
-    if constexpr (PRO == PRO_NORM) inv = rsqrtf(ss / (float)K + eps);
+    if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss / (float)K + eps);
     v *= inv;
     const int col = tile * 16 + n;
     if constexpr (EPI == EPI_SWIGLU) {
@@ -226,7 +245,8 @@ __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restri
 }  // namespace
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, const void* rope, hipStream_t stream) {
+                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream) {
+  if (pro == PRO_NORM_ADD && x2 == nullptr) return -5;
   if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
   RopeEpi re{};
   if (epi == EPI_ROPE) {
@@ -258,7 +278,8 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   } while (0)
 #define RT_SGV(P, E, NWV, UV)                                                                                \
   hipLaunchKernelGGL((skinny_gemm_kernel<P, E, NWV, UV>), grid, dim3(NWV * 64), 0, stream, (uint16_t*)out,  \
-                     (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re)
+                     (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo, eps, re,               \
+                     (const uint16_t*)x2, (uint16_t*)xo)
   if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SG(PRO_PLAIN, EPI_STORE);
   else if (pro == PRO_NORM && epi == EPI_STORE) RT_SG(PRO_NORM, EPI_STORE);
   else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_SG(PRO_PLAIN, EPI_RESID);
@@ -266,6 +287,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_SG(PRO_PLAIN, EPI_SWIGLU);
   else if (pro == PRO_NORM && epi == EPI_ROPE) RT_SG(PRO_NORM, EPI_ROPE);
   else if (pro == PRO_PLAIN && epi == EPI_ROPE) RT_SG(PRO_PLAIN, EPI_ROPE);
+  else if (pro == PRO_NORM_ADD && epi == EPI_STORE) RT_SG(PRO_NORM_ADD, EPI_STORE);
+  else if (pro == PRO_NORM_ADD && epi == EPI_SWIGLU) RT_SG(PRO_NORM_ADD, EPI_SWIGLU);
+  else if (pro == PRO_NORM_ADD && epi == EPI_ROPE) RT_SG(PRO_NORM_ADD, EPI_ROPE);
   else return -2;
 #undef RT_SG
 #undef RT_SGV
@@ -285,7 +309,9 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
 
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
-                            const int64_t* slots, int Hq, int Hkv, int D, int BS, hipStream_t stream) {
+                            const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
+                            hipStream_t stream) {
   const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS};
-  return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, stream);
+  return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, x2, xo,
+                            stream);
 }

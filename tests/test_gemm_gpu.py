@@ -116,3 +116,46 @@ def test_skinny_gemm_rope_epilogue(M, hq, hkv, d):
     qkv = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W.cpu(), gam.cpu()), 1, eps=1e-5)
     q2 = ref.rope_and_cache(qkv, positions.cpu(), cos_sin.cpu(), kc2, vc2, slots.cpu(), hq, hkv, d)
     close(q_r, q2, 0.05, 0.02)
+
+
+def test_norm_add_prologue():
+    """TP decode prologue: normalize bf16(x + x2), workgroup 0 publishes the sum."""
+    M, N, K = 3, 512, 4096
+    x, x2 = bf(M, K, seed=71), bf(M, K, seed=72)
+    W = bf(N, K, scale=0.05, seed=73)
+    gam = bf(K, seed=74)
+    xo = torch.zeros_like(x)
+    got = ops.skinny_gemm(x, ops.shuffle_weight(W, gam), ops.PRO_NORM_ADD, eps=1e-5, x2=x2, xout=xo)
+    xo_r = torch.zeros(M, K, dtype=torch.bfloat16)
+    exp = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W.cpu(), gam.cpu()), 2, eps=1e-5, x2=x2.cpu(), xout=xo_r)
+    close(got, exp.to(DEV), 0.05, 0.02)
+    assert torch.equal(xo, xo_r.to(DEV))
+    # SwiGLU epilogue with the same prologue
+    W2 = bf(2 * N, K, scale=0.05, seed=75)
+    got = ops.skinny_gemm(x, ops.shuffle_weight(W2, gam), ops.PRO_NORM_ADD, ops.EPI_SWIGLU, x2=x2)
+    exp = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W2.cpu(), gam.cpu()), 2, 2, x2=x2.cpu())
+    close(got, exp.to(DEV), 0.05, 0.03)
+
+
+def test_tp_fused_decode_path_matches_tp1_fused():
+    """The tensor-parallel fused forward (NORM_ADD prologues, ping-pong residual) at tp=1 equals
+    the single-GPU fused forward (in-place RESID epilogues)."""
+    from theroundtaible_amd.engine import Engine, EngineConfig
+    from theroundtaible_amd.models.llama import AttnMeta
+    e = Engine(EngineConfig(model="tiny-llama-128", weights="random-full:5", device=DEV, num_blocks=64,
+                            use_graphs=False))
+    ids = e.encode_prompt("tensor parallel fused decode " * 4)
+    s = e.kv.seq("a")
+    e.prefill([(s, ids)])
+    e.kv.ensure_capacity(s, s.length + 1)
+    pos = torch.tensor([s.length], device=DEV)
+    slots = torch.tensor([s.blocks[s.length // 32] * 32 + s.length % 32], device=DEV)
+    bt = torch.zeros(1, 8, dtype=torch.int32)
+    bt[0, :len(s.blocks)] = torch.tensor(s.blocks)
+    meta = AttnMeta("decode", slots, bt.to(DEV), (pos + 1).to(torch.int32), num_splits=4)
+    tok = torch.tensor([9], device=DEV)
+    a = e.model.forward(tok, pos, e.kv, meta).float()
+    e.model.force_tp_path = True
+    b = e.model.forward(tok, pos, e.kv, meta).float()
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert float(cos.min()) > 0.999

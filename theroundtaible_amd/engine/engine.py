@@ -95,7 +95,7 @@ class Engine:
         with torch.no_grad():
             weights = materialize(self.cfg, ecfg.weights, self.device, self.dtype, self.tp)
             self.model = build_model(self.cfg, weights, self.device, self.dtype, self.tp)
-            if self.on_gpu and hasattr(self.model, "decode_weights") and self.tp.size == 1:
+            if self.on_gpu and hasattr(self.model, "decode_weights"):
                 # shuffled decode copies (+1x weight memory) before sizing the KV pool — only when they
                 # leave room for KV: a 70B knight on one GPU keeps the unfused (hipBLASLt) decode path
                 wbytes = sum(t.numel() * t.element_size() for t in weights.values())
@@ -327,8 +327,17 @@ class Engine:
         for s, n in zip(seqs, max_new):
             self.kv.ensure_capacity(s, s.length + steps)
         eos = self.tokenizer.eos_id
+        runner = None
         if self.on_gpu and self.ecfg.use_graphs:
-            runner = self._graph_for(B, max(s.length for s in seqs) + steps)
+            try:
+                runner = self._graph_for(B, max(s.length for s in seqs) + steps)
+            except RuntimeError as e:   # e.g. a collective that refuses stream capture: stay eager
+                if self.tp.size == 1:
+                    raise
+                import warnings
+                warnings.warn(f"hipGraph capture failed under tp={self.tp.size} ({e}); decoding eagerly")
+                self.ecfg.use_graphs = False
+        if runner is not None:
             toks = runner.run(self, seqs, turns, first, steps, deadline, eos)
         else:
             toks = self._decode_eager(seqs, turns, first, steps, deadline, eos)

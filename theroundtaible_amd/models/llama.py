@@ -70,11 +70,12 @@ class LlamaModel:
 
     def fused_decode_ok(self, ids: torch.Tensor) -> bool:
         cfg = self.cfg
-        return (ids.is_cuda and self.tp.size == 1 and 1 <= ids.shape[0] <= 16 and self.use_fused
+        return (ids.is_cuda and 1 <= ids.shape[0] <= 16 and self.use_fused
                 and cfg.hidden % 32 == 0 and cfg.ffn % 32 == 0 and (cfg.n_heads * cfg.head_dim) % 32 == 0
                 and self.w["lm_head"].shape[0] % 16 == 0)
 
     use_fused = True
+    force_tp_path = False   # tests: run the tensor-parallel fused path at tp=1 (all-reduces are no-ops)
     _dec = None
 
     def decode_weights(self):
@@ -120,11 +121,48 @@ class LlamaModel:
         logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
         return logits[:, :cfg.vocab]
 
+    def forward_decode_fused_tp(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
+                                hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Tensor-parallel fused decode (Megatron split): o/down are row-parallel,
+        so their outputs are partial sums — stored plainly, all-reduced over RCCL (C2, inside the
+        hipGraph), and added to the residual by the NEXT GEMM's NORM_ADD prologue, whose
+        workgroup 0 also writes the new residual (ping-pong buffers, never in place). The lm_head
+        is vocab-parallel + all-gather (C3). Still 5 kernels + 2 all-reduces per layer."""
+        cfg, tp = self.cfg, self.tp
+        eps = cfg.norm_eps
+        dec = self.decode_weights()
+        res = hidden if hidden is not None else F.embedding(ids, self.w["embed"]).contiguous()
+        bufs = [res, torch.empty_like(res)]
+        cur = 0
+        B = ids.shape[0]
+        h = None
+        for l, lw in enumerate(dec["layers"]):
+            kc, vc = kv.k_layer(l), kv.v_layer(l)
+            if h is None:
+                q = ops.skinny_gemm_rope(bufs[cur], lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kc, vc,
+                                         meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps)
+            else:
+                q = ops.skinny_gemm_rope(bufs[cur], lw["wqkv"], ops.PRO_NORM_ADD, positions, self.cos_sin, kc, vc,
+                                         meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps,
+                                         x2=h, xout=bufs[1 - cur])
+                cur = 1 - cur
+            a = self.attention(q, kc, vc, meta)
+            h = tp.all_reduce(ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_STORE))
+            g = ops.skinny_gemm(bufs[cur], lw["w_gate_up"], ops.PRO_NORM_ADD, ops.EPI_SWIGLU, eps=eps, x2=h,
+                                xout=bufs[1 - cur])
+            cur = 1 - cur
+            h = tp.all_reduce(ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_STORE))
+        logits = ops.skinny_gemm(bufs[cur], dec["lm_head"], ops.PRO_NORM_ADD, ops.EPI_STORE, eps=eps, x2=h)
+        logits = tp.all_gather_last(logits)
+        return logits[:, :cfg.vocab]
+
     def forward(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
                 hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Returns logits [rows, vocab] (all rows for decode, ``meta.last_rows`` for prefill).
         ``hidden``: optional pre-gathered embedding rows (used by the fused decode path only)."""
         if meta.kind == "decode" and self.fused_decode_ok(ids):
+            if self.tp.size > 1 or self.force_tp_path:
+                return self.forward_decode_fused_tp(ids, positions, kv, meta, hidden)
             return self.forward_decode_fused(ids, positions, kv, meta, hidden)
         cfg, tp = self.cfg, self.tp
         T = ids.shape[0]

@@ -159,7 +159,7 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q.cpu(), start_pos.cpu(), scale)
 
 
-PRO_PLAIN, PRO_NORM = 0, 1
+PRO_PLAIN, PRO_NORM, PRO_NORM_ADD = 0, 1, 2
 EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
 
 
@@ -177,30 +177,33 @@ def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None, rope_h
 
 
 def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: int = EPI_STORE,
-                res: Optional[torch.Tensor] = None, eps: float = 1e-5) -> Optional[torch.Tensor]:
+                res: Optional[torch.Tensor] = None, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
+                xout: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """Decode linear (M <= 16) on shuffled weights with fused RMSNorm prologue (gamma pre-folded)
-    and residual / SwiGLU epilogue. Returns the output (None for RESID, which updates ``res``)."""
+    and residual / SwiGLU epilogue. Returns the output (None for RESID, which updates ``res``).
+    ``PRO_NORM_ADD``: normalizes ``bf16(x + x2)`` and writes that sum to ``xout`` (TP decode)."""
     if _use_native(x):
         n = Ws.shape[0] // (2 if epi == EPI_SWIGLU else 1)
         out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device) if epi != EPI_RESID else x
-        native().skinny_gemm(out, x, Ws, pro, epi, res, eps)
+        native().skinny_gemm(out, x, Ws, pro, epi, res, eps, x2, xout)
         return None if epi == EPI_RESID else out
-    return ref.skinny_gemm(x, Ws, pro, epi, res, eps)
+    return ref.skinny_gemm(x, Ws, pro, epi, res, eps, x2, xout)
 
 
 def skinny_gemm_rope(x: torch.Tensor, Ws: torch.Tensor, pro: int, positions: torch.Tensor, cos_sin: torch.Tensor,
                      k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor, n_heads: int,
-                     n_kv_heads: int, head_dim: int, eps: float = 1e-5) -> torch.Tensor:
+                     n_kv_heads: int, head_dim: int, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
+                     xout: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Decode qkv projection (+ optional RMSNorm prologue) with RoPE and the paged K/V cache
     write fused into the epilogue; returns q [M, n_heads, head_dim]. ``Ws`` must come from
     ``shuffle_weight(Wqkv, gamma, rope_heads=n_heads + n_kv_heads, head_dim=head_dim)``."""
     if _use_native(x):
         q = torch.empty(x.shape[0], n_heads, head_dim, dtype=x.dtype, device=x.device)
         native().skinny_gemm_rope(q, x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
-                                  head_dim, eps)
+                                  head_dim, eps, x2, xout)
         return q
     return ref.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
-                                head_dim, eps)
+                                head_dim, eps, x2, xout)
 
 
 def decode_prep(slots: torch.Tensor, offsets: torch.Tensor, res: torch.Tensor, ids: torch.Tensor,

@@ -150,13 +150,18 @@ def fold_gamma(W, gamma=None, rope_heads: int = 0, head_dim: int = 0):
     return out
 
 
-def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5):
+def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5, x2=None, xout=None):
     """Semantics of csrc/gemm_skinny.hip on the (gamma-folded, row-major) weight ``Wf``:
-    y = rsqrt(mean(x^2) + eps)[:, None] * (x @ Wf^T) for the NORM prologue."""
+    y = rsqrt(mean(x^2) + eps)[:, None] * (x @ Wf^T) for the NORM prologue; NORM_ADD (pro=2)
+    first forms x = bf16(x + x2) and stores it to ``xout``."""
+    if pro == 2:
+        x = (x.float() + x2.float()).to(x.dtype)
+        if xout is not None:
+            xout.copy_(x)
     M, K = x.shape
     xf = x.float()
     y = xf @ Wf.float().t()
-    if pro == 1:
+    if pro in (1, 2):
         y = y * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
     if epi == 2:
         n = Wf.shape[0] // 2
@@ -170,10 +175,10 @@ def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5):
 
 
 def skinny_gemm_rope(x, Wp, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads, head_dim,
-                     eps=1e-5):
+                     eps=1e-5, x2=None, xout=None):
     """ROPE-epilogue semantics: fp32 projection on the pair-permuted weight, columns restored
     to natural order, then RoPE + paged K/V scatter with no bf16 rounding in between."""
-    y = skinny_gemm(x, Wp, pro, 3, None, eps)
+    y = skinny_gemm(x, Wp, pro, 3, None, eps, x2, xout)
     perm = rope_row_perm(Wp.shape[0], n_heads + n_kv_heads, head_dim)
     qkv = torch.empty_like(y)
     qkv[:, perm] = y
