@@ -43,7 +43,9 @@ def parse():
     p.add_argument("--steps", type=int, default=3, help="timed rounds")
     p.add_argument("--warmup", type=int, default=1, help="untimed rounds (round 1 includes the initial prefill)")
     p.add_argument("--model", default="llama3-8b")
-    p.add_argument("--knights-per-gpu", type=int, default=3)
+    p.add_argument("--knights-per-gpu", type=int, default=3,
+                   help="knights hosted per GPU (per TP group when --tp > 1)")
+    p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree of every knight (BASELINE config 5: 4)")
     p.add_argument("--knights-per-table", type=int, default=3)
     p.add_argument("--new-tokens", type=int, default=512, help="decode tokens per knight turn")
     p.add_argument("--temperature", type=float, default=0.7)
@@ -73,25 +75,37 @@ def main() -> int:
     N = cl.world
     device = args.device or cl.device
     kpt = args.knights_per_table
-    total_knights = args.knights_per_gpu * N
+    T = max(1, args.tp)
+    if N % T:
+        raise SystemExit(f"--tp {T} must divide the {N} launched GPUs")
+    n_groups = N // T                      # GPU groups; a knight lives on one group (T ranks)
+    total_knights = args.knights_per_gpu * n_groups
     n_tables = max(1, total_knights // kpt)
     base_names = ["Claude", "Gemini", "GPT", "Mistral", "Llama", "Qwen", "Phi", "Falcon"]
+    group_ranks = [list(range(g * T, (g + 1) * T)) for g in range(n_groups)]
     placement = {}
     tables = []
     for t in range(n_tables):
         knights = []
         for j in range(kpt):
             name = f"{base_names[j % len(base_names)]}-{t}"
-            placement[name] = [(kpt * t + j) % N]
+            placement[name] = group_ranks[(kpt * t + j) % n_groups]
             knights.append({"name": name, "adapter": f"local-llm-{name.lower()}", "capabilities": ["architecture"],
                             "priority": j + 1})
         tables.append(knights)
     local_names = [n for n, ranks in placement.items() if cl.rank in ranks]
 
+    tp = None
+    if T > 1:
+        import torch.distributed as dist
+        from theroundtaible_amd.parallel.tp import TPInfo
+        pgs = [dist.new_group(r) for r in group_ranks]   # collective: same order on every rank
+        g = cl.rank // T
+        tp = TPInfo(size=T, rank=cl.rank % T, group=pgs[g])
     t_load = time.perf_counter()
     engine = Engine(EngineConfig(model=args.model, weights=f"random:{1234}", device=device,
                                  use_graphs=not args.no_graphs and device != "cpu",
-                                 dtype="bf16" if device != "cpu" else "fp32"))
+                                 dtype="bf16" if device != "cpu" else "fp32"), tp)
     params = SamplingParams(temperature=args.temperature, top_p=args.top_p, max_new_tokens=args.new_tokens,
                             ignore_eos=True, stop_on_consensus=False, seed=7)
     import threading
@@ -158,7 +172,8 @@ def main() -> int:
                    "knights_per_gpu": args.knights_per_gpu, "new_tokens_per_turn": args.new_tokens,
                    "global_batch": kpt * n_tables, "seq_len": args.new_tokens,
                    "round_mode": args.round_mode, "prompt_layout": args.layout,
-                   "parallelism": f"knight-placement x{N} (tables striped over GPUs), C1 all-gather"},
+                   "parallelism": (f"knight-placement x{N} (tables striped over GPUs), C1 all-gather" if T == 1 else
+                                   f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL")},
         "detail": {"decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),

@@ -141,3 +141,10 @@ def test_cli_discuss_under_torchrun_with_tp_knight(tmp_path):
     disc = (tmp_path / ".roundtable" / "sessions" / sessions[0] / "discussion.md").read_text()
     for name in ("Alfa", "Beta", "Groot"):
         assert disc.count(name) >= 2, name                       # both rounds, every knight (TP knight too)
+
+
+def test_spmd_bench_tp2():
+    """bench.py --tp 2 on 2 gloo ranks: one TP=2 group hosts the table's knights."""
+    out = _bench(2, ("--tp", "2", "--knights-per-table", "2", "--knights-per-gpu", "2"))
+    assert out["config"]["knights"] == 2 and "tp2" in out["config"]["parallelism"]
+    assert out["detail"]["decode_tokens"] == 2 * 8 * 2
