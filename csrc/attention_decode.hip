@@ -1,276 +1,18 @@
 // K3: paged-KV decode attention (one query token per sequence), GQA, MFMA bf16, split-KV.
-//
-// Grid (B * Hkv, num_splits), NW = 8 waves per workgroup. A workgroup owns one (sequence,
-// kv head, key range); its G = Hq/Hkv query heads share every K/V byte it loads (GQA
-// packing: the G queries are the 16 MFMA columns, G <= 16). The split count is chosen so the
-// grid is ~one 8-wave workgroup per CU (ops.decode_splits): decode attention is a pure
-// K/V stream, so what matters is bytes in flight per CU and few round trips per launch.
-//
-// Per 32-key tile (= one cache block, BS = 32) each wave computes
-//   S^T[32 keys x 16 q] = K . Q^T     2 halves x D/32  mfma_f32_16x16x32_bf16
-//   online softmax down each q column (in-register; 2 xor-shuffles per reduction)
-//   O[16 q x D]        += P . V       D/16 mfma_f32_16x16x32_bf16
-// K rows are fed to the MFMA in the order key(h, row) = 8*(row>>2) + 4h + (row&3), so lane
-// (r, g) of the S^T accumulator holds keys 8g..8g+7 of column r — exactly the A-operand
-// fragment of P.V (P never leaves registers) — and the matching B fragment of the
-// transposed value cache ([D][32] per block) is ONE 16-byte load per lane per d-chunk.
-// K rows are read as 64 contiguous bytes per lane (d permuted consistently on K and Q).
-// K/V go straight to VGPRs (cdna_hip_programming App. B "Attention decode") with the next
-// tile's loads in flight while the current tile computes. The 8 waves' softmax states
-// merge through LDS; the splits of one (sequence, kv head) are combined in the same launch
-// by whichever workgroup arrives last (sc1 write-through hand-off, see below).
-#include "common.h"
+// The work-item code is in attn_core.h (shared with the persistent decode-layer kernel); this
+// file holds the grid launch: blockIdx = (sequence x kv head, key split).
+#include "attn_core.h"
 
 namespace {
-using rt::bf16x8;
-using rt::float4_;
-using rt::short8;
-
-constexpr int BS = 32;
-constexpr int NW = 8;
-constexpr int MAXS = 64;  // max splits (combine staging)
-constexpr float LOG2E = 1.4426950408889634f;
+using namespace attn;
 
 template <int D>
-struct Tile {
-  short8 k[2][D / 32];  // [half][chunk]: K row key(h, r), d = (D/4)*g + 8c + j
-  short8 v[D / 16];     // [d-chunk]: V[keys 8g..8g+7][d = 16e + r]
-};
-
-template <int D>
-RT_DEVICE void load_tile(Tile<D>& t, const uint16_t* __restrict__ kblk, const uint16_t* __restrict__ vblk, int r,
-                         int g) {
-  const int krow = 8 * (r >> 2) + (r & 3);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint16_t* kr = kblk + (krow + 4 * h) * D + (D / 4) * g;
-#pragma unroll
-    for (int c = 0; c < D / 32; ++c) t.k[h][c] = *reinterpret_cast<const short8*>(kr + 8 * c);
-  }
-#pragma unroll
-  for (int e = 0; e < D / 16; ++e) t.v[e] = *reinterpret_cast<const short8*>(vblk + (16 * e + r) * BS + 8 * g);
-}
-
-template <int D>
-__global__ void __launch_bounds__(NW * 64) paged_decode_kernel(
-    uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache,
-    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ ctx_lens,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int Hq, int Hkv,
-    int max_blocks, float scale_log2, int num_splits) {
-  __shared__ float s_m[NW][16];
-  __shared__ float s_l[NW][16];
-  __shared__ float s_o[NW][16][D + 4];
-  __shared__ float s_wt[16][MAXS];
-  __shared__ float s_lt[16][MAXS];
-  __shared__ int s_last;
-
-  const int bh = blockIdx.x;
-  const int b = bh / Hkv, hk = bh - (bh / Hkv) * Hkv;
-  const int split = blockIdx.y;
-  const int G = Hq / Hkv;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-
-  const int ctx = ctx_lens[b];
-  const int ntiles = (ctx + BS - 1) / BS;
-  const int tps = (ntiles + num_splits - 1) / num_splits;
-  const int t_begin = split * tps;
-  const int t_end = min(ntiles, t_begin + tps);
-
-  // Q^T fragments: column r = query head hk*G + r (zero for r >= G)
-  short8 qf[D / 32];
-  {
-    const uint16_t* qr = q + ((size_t)b * Hq + hk * G + (r < G ? r : 0)) * D + (D / 4) * g;
-#pragma unroll
-    for (int c = 0; c < D / 32; ++c) {
-      short8 v = *reinterpret_cast<const short8*>(qr + 8 * c);
-      if (r >= G) v = short8{0, 0, 0, 0, 0, 0, 0, 0};
-      qf[c] = v;
-    }
-  }
-
-  float4_ oacc[D / 16];
-#pragma unroll
-  for (int e = 0; e < D / 16; ++e) oacc[e] = float4_{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY;  // running max (log2 domain) of column r
-  float lsum = 0.f;     // lane-partial running sum of column r
-
-  const int* bt = block_tables + (size_t)b * max_blocks;
-  const size_t blk_stride = (size_t)Hkv * BS * D;
-  Tile<D> cur, nxt;
-  int t = t_begin + wid;
-  if (t < t_end) {
-    const size_t base = (size_t)bt[t] * blk_stride + (size_t)hk * BS * D;
-    load_tile<D>(cur, k_cache + base, v_cache + base, r, g);
-  }
-  for (; t < t_end; t += NW) {
-    const int tn = t + NW;
-    if (tn < t_end) {  // keep the next tile's loads in flight during this tile's math
-      const size_t base = (size_t)bt[tn] * blk_stride + (size_t)hk * BS * D;
-      load_tile<D>(nxt, k_cache + base, v_cache + base, r, g);
-    }
-    // ---- S^T = K Q^T ----
-    float4_ s[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      s[h] = float4_{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < D / 32; ++c)
-        s[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur.k[h][c]),
-                                                       __builtin_bit_cast(bf16x8, qf[c]), s[h], 0, 0, 0);
-    }
-    // ---- online softmax down column r: lane holds keys 8g + 4h + i ----
-    const int key0 = t * BS + 8 * g;
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = s[h][i] * scale_log2;
-        v = key0 + 4 * h + i < ctx ? v : -INFINITY;
-        s[h][i] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);  // m=-inf first time -> 0
-    m = mnew;
-    float psum = 0.f;
-    short8 pa;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(s[h][i] - mnew);
-        psum += p;
-        pa[4 * h + i] = (short)rt::f2bf(p);
-      }
-    lsum = lsum * alpha + psum;
-    // rows of O held by this lane are q = 4g + i: fetch their alphas from lanes 4g + i
-    float al[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) al[i] = __shfl(alpha, 4 * g + i, 64);
-    // ---- O += P V ----
-#pragma unroll
-    for (int e = 0; e < D / 16; ++e) {
-      float4_ o = oacc[e];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] *= al[i];
-      oacc[e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pa),
-                                                        __builtin_bit_cast(bf16x8, cur.v[e]), o, 0, 0, 0);
-    }
-    cur = nxt;
-  }
-  // column-complete partial sum for q = r
-  lsum += __shfl_xor(lsum, 16, 64);
-  lsum += __shfl_xor(lsum, 32, 64);
-
-  // ---- merge the waves through LDS (only the G live query rows) ----
-  if (g == 0) {
-    s_m[wid][r] = m;
-    s_l[wid][r] = lsum;
-  }
-#pragma unroll
-  for (int e = 0; e < D / 16; ++e)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (4 * g + i < G) s_o[wid][4 * g + i][16 * e + r] = oacc[e][i];
-  __syncthreads();
-
-  const size_t bh_q0 = (size_t)b * Hq + hk * G;  // first query head of this workgroup
-  const auto po_rsrc = rt::buf_rsrc(part_o + bh_q0 * num_splits * D);
-  const auto pml_rsrc = rt::buf_rsrc(part_ml + bh_q0 * num_splits * 4);
-  for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
-    const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][qi]);
-    float L = 0.f;
-    float4_ O = {0.f, 0.f, 0.f, 0.f};
-    if (M != -INFINITY) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const float f = exp2f(s_m[w][qi] - M);
-        L += f * s_l[w][qi];
-        const float4_ ow = *reinterpret_cast<const float4_*>(&s_o[w][qi][d0]);
-        O += f * ow;
-      }
-    }
-    if (num_splits == 1) {
-      const float inv = L > 0.f ? 1.f / L : 0.f;
-      uint2 pk;
-      pk.x = rt::pack2(O[0] * inv, O[1] * inv);
-      pk.y = rt::pack2(O[2] * inv, O[3] * inv);
-      *reinterpret_cast<uint2*>(out + (bh_q0 + qi) * D + d0) = pk;
-    } else {
-      // partials leave as 16-B write-through (sc1) stores: the combining workgroup, possibly
-      // on another XCD, reads them with sc1 loads and no L2 writeback/invalidate is needed
-      rt::sc1_store4(po_rsrc, ((qi * num_splits + split) * D + d0) * 4, O);
-      if (d0 == 0) rt::sc1_store4(pml_rsrc, (qi * num_splits + split) * 16, float4_{M, L, 0.f, 0.f});
-    }
-  }
-  if (num_splits == 1) return;
-
-  // ---- split-KV combine inside the launch (MI355X_MICROARCH "Valid forms", row 1): every
-  // partial is stored sc1 and drained (vmcnt(0)) by each storing wave before the barrier;
-  // ONE lane then bumps the (sequence, kv head) arrival counter; the workgroup whose add
-  // returns num_splits-1 combines, reading every partial with sc1 loads, and re-arms the
-  // counter for the next launch (hipGraph replays need no memset node). A release/acquire
-  // fence pair instead would write back / invalidate caches per workgroup (measured 2x slower).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == num_splits - 1;
-    if (s_last) __hip_atomic_store(counters + bh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!s_last) return;
-
-  // latency-bound: (m, l) of all (head, split) pairs by distinct threads, weights via LDS,
-  // then 8 independent 16-B partial loads in flight per thread
-  for (int i = threadIdx.x; i < G * num_splits; i += blockDim.x) {
-    const float4_ ml = rt::sc1_load4(pml_rsrc, i * 16);
-    const int qi = i / num_splits, s2 = i - qi * num_splits;
-    s_wt[qi][s2] = ml[1] > 0.f ? ml[0] : -INFINITY;
-    s_lt[qi][s2] = ml[1];
-  }
-  __syncthreads();
-  if (threadIdx.x < G) {
-    const int qi = threadIdx.x;
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, s_wt[qi][s2]);
-    float L = 0.f;
-    for (int s2 = 0; s2 < num_splits; ++s2) {
-      const float f = (M == -INFINITY || s_wt[qi][s2] == -INFINITY) ? 0.f : exp2f(s_wt[qi][s2] - M);
-      s_wt[qi][s2] = f;
-      L += f * s_lt[qi][s2];
-    }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    for (int s2 = 0; s2 < num_splits; ++s2) s_wt[qi][s2] *= inv;
-  }
-  __syncthreads();
-  for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
-    const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
-    float4_ O = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = 0; s0 < num_splits; s0 += 8) {
-      float4_ v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = (s0 + j < num_splits) ? rt::sc1_load4(po_rsrc, ((qi * num_splits + s0 + j) * D + d0) * 4)
-                                     : float4_{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (s0 + j < num_splits) O += s_wt[qi][s0 + j] * v[j];
-    }
-    uint2 pk;
-    pk.x = rt::pack2(O[0], O[1]);
-    pk.y = rt::pack2(O[2], O[3]);
-    *reinterpret_cast<uint2*>(out + (bh_q0 + qi) * D + d0) = pk;
-  }
+__global__ void __launch_bounds__(NW * 64) paged_decode_kernel(AttnArgs p) {
+  __shared__ AttnSmem<D> sm;
+  attn_item<D, false>(p, blockIdx.x, blockIdx.y, sm);
 }
 }  // namespace
+
 
 // q [B, Hq, D]; k_cache [NB, Hkv, 32, D]; v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32;
 // part_o >= B*Hq*splits*D floats, part_ml >= B*Hq*splits*4 floats, counters >= B*Hkv ints (zeroed once).
@@ -283,14 +25,12 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   if (num_splits > MAXS) return -3;
   dim3 grid(B * Hkv, num_splits), block(NW * 64);
   const float sl2 = scale * LOG2E;
+  const AttnArgs args{(uint16_t*)out, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+                      block_tables, ctx_lens, part_o, part_ml, counters, Hq, Hkv, max_blocks, sl2, num_splits};
   if (D == 128)
-    hipLaunchKernelGGL((paged_decode_kernel<128>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)q,
-                       (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, part_o, part_ml,
-                       counters, Hq, Hkv, max_blocks, sl2, num_splits);
+    hipLaunchKernelGGL((paged_decode_kernel<128>), grid, block, 0, stream, args);
   else if (D == 64)
-    hipLaunchKernelGGL((paged_decode_kernel<64>), grid, block, 0, stream, (uint16_t*)out, (const uint16_t*)q,
-                       (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, part_o, part_ml,
-                       counters, Hq, Hkv, max_blocks, sl2, num_splits);
+    hipLaunchKernelGGL((paged_decode_kernel<64>), grid, block, 0, stream, args);
   else
     return -2;
   return 0;

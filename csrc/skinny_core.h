@@ -1,0 +1,294 @@
+// Device core of the decode-path GEMMs (M <= 16 rows): shared by the standalone launches in
+// gemm_skinny.hip and the persistent decode-layer kernel in decode_layer.hip.
+//
+// Weight layout ("fragment-shuffled", built once at load time by `shuffle_weight`):
+//     Ws[N/16][K/32][64 lanes][8]   with  Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j]
+// i.e. exactly the order in which the 64 lanes of a wave hold the B operand of
+// v_mfma_f32_16x16x32_bf16: every wave load instruction reads 1 KiB of contiguous HBM and a
+// workgroup streams its 16-row panel front to back.
+//
+// One tile = 16 output columns (32 W rows for SwiGLU) x all of K; the NW waves of the
+// workgroup take interleaved 32-deep k-steps (adjacent waves -> adjacent KiB), with the next
+// U steps' loads issued before the current steps' MFMAs (register double-buffering). M is
+// padded to the 16 MFMA rows. The waves' partial tiles are summed through LDS.
+//
+// Prologues:  PLAIN | NORM (RMSNorm: gamma folded into W, 1/rms from the same A fragments,
+//             applied after the MFMAs) | NORM_ADD (A = bf16(x + x2): tensor-parallel residual
+//             plus the all-reduced partial; workgroup 0 publishes the sum to `xo`).
+// Epilogues:  STORE | RESID (res += y, in place) | SWIGLU (silu(gate) * up) |
+//             ROPE (qkv: rotate q/k pairs, write q, scatter k/v into the paged caches).
+// SC1 = true (persistent kernel): activations produced inside the same launch are read with
+// sc1 loads and every output is stored sc1 (write-through), MI355X_MICROARCH "Valid forms".
+#pragma once
+#include "common.h"
+
+namespace skinny {
+using rt::bf16x8;
+using rt::float4_;
+using rt::short8;
+
+enum : int { PRO_PLAIN = 0, PRO_NORM = 1, PRO_NORM_ADD = 2 };
+enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_ROPE = 3 };
+
+struct RopeEpi {
+  const int64_t* positions;  // [M]
+  const float* cos_sin;      // [max_pos][D]: cos(D/2) | sin(D/2)
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  const int64_t* slots;      // [M]
+  int Hq, Hkv, D, BS;
+};
+
+struct GemmArgs {
+  uint16_t* out;
+  const uint16_t* x;
+  const short8* Ws;
+  uint16_t* res;
+  int M, N, K, ldo;
+  float eps;
+  RopeEpi re;
+  const uint16_t* x2;  // NORM_ADD
+  uint16_t* xo;        // NORM_ADD: where workgroup `xo_wg` publishes x + x2
+};
+
+template <int NACC, int NW>   // NACC = accumulators per lane (2 for SwiGLU gate + up)
+struct GemmSmem {
+  float red[NW][NACC][16][17];
+  float sq[NW][16];
+};
+template <int EPI>
+constexpr int nacc() { return EPI == EPI_SWIGLU ? 2 : 1; }
+
+RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// 16-bit store, optionally write-through (sc1) for consumers in the same launch
+template <bool SC1>
+RT_DEVICE void st16(uint16_t* p, float v) {
+  if constexpr (SC1)
+    __hip_atomic_store(p, rt::f2bf(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = rt::f2bf(v);
+}
+template <bool SC1>
+RT_DEVICE float ld16(const uint16_t* p) {
+  if constexpr (SC1)
+    return rt::bf2f(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  else
+    return rt::bf2f(*p);
+}
+// Activation fragment loads: SC1 goes through a buffer resource built from the UNIFORM tensor
+// base (a per-lane base would force a readfirstlane waterfall loop) plus a per-lane byte offset.
+struct XSrc {
+  const uint16_t* base;            // plain path: this lane's row pointer
+  __amdgpu_buffer_rsrc_t rsrc;     // SC1 path: whole-tensor resource
+  int off;                         // SC1 path: this lane's byte offset
+};
+template <bool SC1>
+RT_DEVICE XSrc make_xsrc(const uint16_t* tensor, size_t lane_elem) {
+  XSrc x;
+  x.base = tensor + lane_elem;
+  if constexpr (SC1) {
+    x.rsrc = rt::buf_rsrc(tensor);
+    x.off = (int)(lane_elem * 2);
+  } else {
+    x.off = 0;
+  }
+  return x;
+}
+template <bool SC1>
+RT_DEVICE short8 ld_x8(const XSrc& x, int elem) {
+  if constexpr (SC1)
+    return __builtin_bit_cast(short8, rt::sc1_load4(x.rsrc, x.off + elem * 2));
+  else
+    return *reinterpret_cast<const short8*>(x.base + elem);
+}
+
+// U = k-steps per wave per pipeline stage (x2 stages in flight)
+template <int PRO, int EPI, int U>
+struct Stage {
+  short8 w[U];
+  short8 w2[(EPI == EPI_SWIGLU) ? U : 1];
+  short8 a[U];
+  short8 b[(PRO == PRO_NORM_ADD) ? U : 1];
+};
+
+template <int PRO, int EPI, int NW, int U>
+RT_DEVICE void issue_w(Stage<PRO, EPI, U>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2, int s0,
+                       int nsteps, int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int s = s0 + NW * u;
+    if (s < nsteps) {
+      st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * 64 + lane);
+      if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt2 + (size_t)s * 64 + lane);
+    }
+  }
+}
+
+template <int PRO, int EPI, int NW, int U, bool SC1>
+RT_DEVICE void issue_a(Stage<PRO, EPI, U>& st, const XSrc& xr, const XSrc& xr2, bool row_ok, int s0, int nsteps) {
+  const short8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int s = s0 + NW * u;
+    st.a[u] = (row_ok && s < nsteps) ? ld_x8<SC1>(xr, s * 32) : z;
+    if constexpr (PRO == PRO_NORM_ADD) st.b[u] = (row_ok && s < nsteps) ? ld_x8<SC1>(xr2, s * 32) : z;
+  }
+}
+
+template <int PRO, int EPI, int NW, int U, bool SC1>
+RT_DEVICE void consume(const Stage<PRO, EPI, U>& st, float4_& acc, float4_& acc2, float& ssq, int s0, int nsteps,
+                       uint16_t* __restrict__ xo_r, const XSrc& xo_s) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (s0 + NW * u < nsteps) {
+      short8 av = st.a[u];
+      if constexpr (PRO == PRO_NORM_ADD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          av[j] = (short)rt::f2bf(rt::bf2f((uint16_t)st.a[u][j]) + rt::bf2f((uint16_t)st.b[u][j]));
+        if (xo_r != nullptr) {
+          if constexpr (SC1) {
+            rt::sc1_store4(xo_s.rsrc, xo_s.off + (s0 + NW * u) * 64, __builtin_bit_cast(float4_, av));
+          } else {
+            *reinterpret_cast<short8*>(xo_r + (s0 + NW * u) * 32) = av;
+          }
+        }
+      }
+      const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u]), acc, 0, 0, 0);
+      if constexpr (EPI == EPI_SWIGLU)
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u]), acc2, 0, 0, 0);
+      if constexpr (PRO != PRO_PLAIN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = rt::bf2f((uint16_t)av[j]);
+          ssq = fmaf(f, f, ssq);
+        }
+      }
+    }
+  }
+}
+
+// Stage-0 weight prefetch of `tile` for the calling wave (no activation loads): lets a
+// persistent kernel put a tile's first weight bytes in flight before its inputs are ready.
+template <int PRO, int EPI, int NW, int U>
+RT_DEVICE void gemm_prefetch(const GemmArgs& p, int tile, Stage<PRO, EPI, U>& st0) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nsteps = p.K / 32;
+  const short8* wt = p.Ws + (size_t)tile * nsteps * 64;
+  const short8* wt2 = (EPI == EPI_SWIGLU) ? p.Ws + (size_t)(p.N / 16 + tile) * nsteps * 64 : nullptr;
+  issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane);
+}
+
+// One 16-column tile. `st0` may hold this tile's prefetched stage-0 weights (prefetched=true).
+// `publish_xo`: this workgroup writes the NORM_ADD sum to p.xo.
+template <int PRO, int EPI, int NW, int U, bool SC1>
+RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>& sm, Stage<PRO, EPI, U>& st0,
+                         bool prefetched,
+                         bool publish_xo) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nsteps = K / 32;
+  const bool row_ok = r < M;
+  const size_t lane_elem = (size_t)(row_ok ? r : 0) * K + 8 * g;
+  const XSrc xr = make_xsrc<SC1>(p.x, lane_elem);
+  const XSrc xr2 = make_xsrc<SC1>(PRO == PRO_NORM_ADD ? p.x2 : p.x, lane_elem);
+  uint16_t* xo_r =
+      (PRO == PRO_NORM_ADD && publish_xo && row_ok && p.xo != nullptr) ? p.xo + (size_t)r * K + 8 * g : nullptr;
+  const XSrc xo_s = make_xsrc<SC1>(PRO == PRO_NORM_ADD && p.xo != nullptr ? p.xo : p.x, lane_elem);
+  const short8* wt = p.Ws + (size_t)tile * nsteps * 64;
+  const short8* wt2 = (EPI == EPI_SWIGLU) ? p.Ws + (size_t)(N / 16 + tile) * nsteps * 64 : nullptr;
+
+  float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  float ssq = 0.f;
+  Stage<PRO, EPI, U> st1;
+  int s = wid;
+  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s, nsteps, lane);
+  issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s, nsteps);
+  for (;;) {
+    const int sn = s + NW * U;
+    if (sn < nsteps) {
+      issue_w<PRO, EPI, NW, U>(st1, wt, wt2, sn, nsteps, lane);
+      issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, sn, nsteps);
+    }
+    consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
+    if (sn >= nsteps) break;
+    s = sn;
+    const int sn2 = s + NW * U;
+    if (sn2 < nsteps) {
+      issue_w<PRO, EPI, NW, U>(st0, wt, wt2, sn2, nsteps, lane);
+      issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, sn2, nsteps);
+    }
+    consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
+    if (sn2 >= nsteps) break;
+    s = sn2;
+  }
+
+  // C layout: acc[i] = C[m = 4g + i][n = r]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sm.red[wid][0][4 * g + i][r] = acc[i];
+    if constexpr (EPI == EPI_SWIGLU) sm.red[wid][(EPI == EPI_SWIGLU) ? 1 : 0][4 * g + i][r] = acc2[i];
+  }
+  if constexpr (PRO != PRO_PLAIN) {
+    ssq += __shfl_xor(ssq, 16, 64);
+    ssq += __shfl_xor(ssq, 32, 64);
+    if (g == 0) sm.sq[wid][r] = ssq;
+  }
+  __syncthreads();
+  const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
+  if (threadIdx.x < 256 && m < M) {
+    float v = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      v += sm.red[w][0][m][n];
+      if constexpr (PRO != PRO_PLAIN) ss += sm.sq[w][m];
+    }
+    float inv = 1.f;
+    if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss / (float)K + p.eps);
+    v *= inv;
+    const int col = tile * 16 + n;
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int u1 = (EPI == EPI_SWIGLU) ? 1 : 0;
+      float up = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) up += sm.red[w][u1][m][n];
+      up *= inv;
+      st16<SC1>(p.out + (size_t)m * p.ldo + col, silu(v) * up);
+    } else if constexpr (EPI == EPI_RESID) {
+      uint16_t* rp = p.res + (size_t)m * N + col;
+      st16<SC1>(rp, v + ld16<SC1>(rp));
+    } else if constexpr (EPI == EPI_ROPE) {
+      const RopeEpi& re = p.re;
+      const int D = re.D, half = D >> 1;
+      const int h = col / D, pp = col - h * D;
+      const int64_t slot = re.slots[m];
+      const int64_t blk = slot / re.BS;
+      const int off = (int)(slot - blk * re.BS);
+      if (h < re.Hq + re.Hkv) {
+        float partner = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) partner += sm.red[w][0][m][n ^ 1];
+        partner *= inv;
+        const int i = pp >> 1, hi = pp & 1;
+        const float* cs = re.cos_sin + (size_t)re.positions[m] * D;
+        const float c = cs[i], sn = cs[half + i];
+        // pair (x1 = d i, x2 = d i+D/2): y1 = x1 c - x2 s ; y2 = x2 c + x1 s
+        const float y = hi ? fmaf(v, c, partner * sn) : fmaf(v, c, -partner * sn);
+        const int d = i + hi * half;
+        uint16_t* dst = (h < re.Hq) ? p.out + ((size_t)m * re.Hq + h) * D + d
+                                    : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
+        st16<SC1>(dst, y);
+      } else {
+        const int hv = h - re.Hq - re.Hkv;
+        st16<SC1>(re.v_cache + (((size_t)blk * re.Hkv + hv) * D + pp) * re.BS + off, v);
+      }
+    } else {
+      st16<SC1>(p.out + (size_t)m * p.ldo + col, v);
+    }
+  }
+  __syncthreads();  // LDS reduction buffers are reused by the next tile
+}
+}  // namespace skinny

@@ -14,6 +14,7 @@ Per layer (decode and prefill share the code; only the attention op differs):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -75,6 +76,8 @@ class LlamaModel:
                 and self.w["lm_head"].shape[0] % 16 == 0)
 
     use_fused = True
+    # one persistent launch per layer instead of five (csrc/decode_layer.hip)
+    use_persistent = os.environ.get("ROUNDTABLE_PERSISTENT_DECODE", "0") == "1"
     force_tp_path = False   # tests: run the tensor-parallel fused path at tp=1 (all-reduces are no-ops)
     _dec = None
 
@@ -110,6 +113,15 @@ class LlamaModel:
         # the residual stream is updated in place by every RESID epilogue
         res = hidden if hidden is not None else F.embedding(ids, self.w["embed"]).contiguous()
         B = ids.shape[0]
+        if self.use_persistent and self.head_dim == 128 and kv.block_size == 32:
+            ws = meta.workspace or ops.DecodeWorkspace(B, self.n_heads, self.head_dim, max(1, meta.num_splits),
+                                                       res.device)
+            for l, lw in enumerate(dec["layers"]):
+                ops.decode_layer(res, lw, positions, self.cos_sin, kv.k_layer(l), kv.v_layer(l), meta.slot_mapping,
+                                 meta.block_tables, meta.ctx_lens, self.n_heads, self.n_kv_heads, self.head_dim,
+                                 max(1, meta.num_splits), ws, eps, self.scale)
+            logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
+            return logits[:, :cfg.vocab]
         for l, lw in enumerate(dec["layers"]):
             q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kv.k_layer(l),
                                      kv.v_layer(l), meta.slot_mapping, self.n_heads, self.n_kv_heads,

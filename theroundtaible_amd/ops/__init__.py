@@ -105,6 +105,9 @@ class DecodeWorkspace:
         # per-(sequence, kv head) split arrival counters; the kernel re-arms them to 0 itself.
         # Sized by n_heads (>= n_kv_heads) so one workspace serves every GQA ratio.
         self.counters = torch.zeros(max_batch * n_heads, dtype=torch.int32, device=device)
+        # persistent decode-layer kernel: phase counters (self-re-arming) and the poll-expiry flag
+        self.sync = torch.zeros(8, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
 
 
 def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 64) -> int:
@@ -222,6 +225,23 @@ def decode_advance(out: torch.Tensor, ids: torch.Tensor, positions: torch.Tensor
         native().decode_advance(out, ids, positions, ctx_lens, step, nxt)
         return
     ref.decode_advance(out, ids, positions, ctx_lens, step, nxt)
+
+
+def decode_layer(res: torch.Tensor, lw: dict, positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,
+                 v_cache: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor, ctx_lens: torch.Tensor,
+                 n_heads: int, n_kv_heads: int, head_dim: int, num_splits: int, ws: DecodeWorkspace, eps: float,
+                 scale: float, stamps: Optional[torch.Tensor] = None) -> None:
+    """One whole decode layer in ONE persistent launch (csrc/decode_layer.hip); updates ``res``
+    in place. ``lw``: the layer's shuffled weights (wqkv with rope rows, wo, w_gate_up, w_down)."""
+    M = res.shape[0]
+    if not _use_native(res):
+        raise RuntimeError("decode_layer is GPU-only (CPU runs the unfused reference path)")
+    q = torch.empty(M, n_heads, head_dim, dtype=res.dtype, device=res.device)
+    a = torch.empty(M, n_heads * head_dim, dtype=res.dtype, device=res.device)
+    g = torch.empty(M, lw["w_down"].shape[1], dtype=res.dtype, device=res.device)
+    native().decode_layer(res, q, a, g, lw["wqkv"], lw["wo"], lw["w_gate_up"], lw["w_down"], positions, cos_sin,
+                          k_cache, v_cache, slots, block_tables, ctx_lens, ws.partial_o, ws.partial_ml, ws.counters,
+                          ws.sync, ws.err, n_heads, n_kv_heads, int(num_splits), eps, scale, stamps)
 
 
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
