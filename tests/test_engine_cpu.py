@@ -103,3 +103,33 @@ def test_gpt2_small_shapes_cpu():
     out = e.run_turns([Turn("K", "GPT-2 knight", SamplingParams(temperature=0.7, max_new_tokens=4, ignore_eos=True,
                                                                  stop_on_consensus=False))])[0]
     assert len(out.ids) == 4 and all(0 <= i < 50257 for i in out.ids)
+
+
+def test_engine_fault_injection_and_health():
+    """injected faults surface as classified per-turn errors; a device fault marks
+    the engine unhealthy so later turns are refused (the orchestrator then skips / falls back)."""
+    from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+    sp = SamplingParams(temperature=0.0, max_new_tokens=3, ignore_eos=True, stop_on_consensus=False)
+    e = Engine(EngineConfig(model="tiny-llama", device="cpu", dtype="fp32", num_blocks=64,
+                            faults={0: "oom", 1: "timeout", 3: "device"}))
+    r0 = e.run_turns([Turn("a", "x", sp)])[0]
+    assert r0.error is not None and r0.error.kind == "oom"
+    r1 = e.run_turns([Turn("a", "x", sp)])[0]
+    assert r1.error is not None and r1.error.kind == "timeout"
+    r2 = e.run_turns([Turn("a", "x", sp)])[0]
+    assert r2.error is None and len(r2.ids) == 3
+    r3 = e.run_turns([Turn("a", "x", sp)])[0]
+    assert r3.error.kind == "device" and not e.healthy
+    r4 = e.run_turns([Turn("a", "x", sp)])[0]
+    assert r4.error.kind == "device"
+
+
+def test_debug_paging_checks():
+    import pytest as _pt
+    from theroundtaible_amd.engine import Engine, EngineConfig
+    e = Engine(EngineConfig(model="tiny-llama", device="cpu", dtype="fp32", num_blocks=16, debug_checks=True))
+    e.check_paging(torch.tensor([[0, 15]], dtype=torch.int32), [0, 16 * 32 - 1])
+    with _pt.raises(AssertionError):
+        e.check_paging(torch.tensor([[16]], dtype=torch.int32), [])
+    with _pt.raises(AssertionError):
+        e.check_paging(torch.tensor([[0]], dtype=torch.int32), [16 * 32])

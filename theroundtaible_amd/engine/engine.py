@@ -19,6 +19,7 @@ The same class runs on CPU (reference ops, no graphs) for the GPT-2 plumbing con
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -57,6 +58,11 @@ class EngineConfig:
     sync_every: int = 32                    # decode steps between host token readbacks
     max_batch: int = 16
     model_overrides: Dict[str, object] = field(default_factory=dict)
+    # fault injection (tests / chaos runs): run_turns call index -> "raise" | "oom" |
+    # "timeout" | "device". Also from ROUNDTABLE_ENGINE_FAULTS="2:oom,5:device".
+    faults: Dict[int, str] = field(default_factory=dict)
+    # validate paging metadata (block tables / slots in range) before every forward (ROUNDTABLE_DEBUG_CHECKS=1)
+    debug_checks: bool = False
 
 
 @dataclass
@@ -110,6 +116,12 @@ class Engine:
         self._seg_cache: Dict[Tuple[str, str], List[int]] = {}
         self.healthy = True
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0}
+        self._calls = 0
+        self.faults = dict(ecfg.faults)
+        for item in filter(None, os.environ.get("ROUNDTABLE_ENGINE_FAULTS", "").split(",")):
+            k, _, v = item.partition(":")
+            self.faults[int(k)] = v.strip()
+        self.debug_checks = ecfg.debug_checks or os.environ.get("ROUNDTABLE_DEBUG_CHECKS") == "1"
 
     # ---- memory ----------------------------------------------------------------------------
     def _alloc_kv(self) -> PagedKVCache:
@@ -234,6 +246,8 @@ class Engine:
                             cu_q=cu_t.to(dev, non_blocking=True),
                             start_pos=torch.tensor(starts, dtype=torch.int32).to(dev, non_blocking=True),
                             last_rows=torch.tensor(last, dtype=torch.int64).to(dev, non_blocking=True))
+            if self.debug_checks:
+                self.check_paging(bt, slots)
             if self.on_gpu:
                 rows = ops.native().prefill_rows_per_tile(self.model.n_heads // self.model.n_kv_heads)
                 meta.tile_map = ops.prefill_tile_map(cu_t, rows).to(dev, non_blocking=True)
@@ -255,7 +269,10 @@ class Engine:
         if not self.healthy:
             err = AdapterError("engine", "engine unhealthy after a previous device error", kind="device")
             return [TurnOutput("", [], {}, err) for _ in turns]
+        call = self._calls
+        self._calls += 1
         try:
+            self._inject(call)
             return self._run_turns(turns)
         except KVCacheOOM as e:
             for t in turns:  # drop partial state; the knight re-prefills next time
@@ -270,6 +287,29 @@ class Engine:
                 return [TurnOutput("", [], {}, AdapterError("engine", f"HIP error: {msg}", kind="device"))
                         for _ in turns]
             raise
+
+    def _inject(self, call: int) -> None:
+        f = self.faults.get(call)
+        if f is None:
+            return
+        if f == "oom":
+            raise KVCacheOOM(f"injected KV-cache exhaustion at call {call}")
+        if f == "timeout":
+            raise EngineTimeout("engine", f"injected timeout at call {call}")
+        if f == "device":
+            raise RuntimeError(f"HIP error: injected device fault at call {call}")
+        raise AdapterError("engine", f"injected failure at call {call}", kind="unknown")
+
+    def check_paging(self, block_tables: torch.Tensor, slots: Sequence[int]) -> None:
+        """Debug-mode bounds asserts on the paging metadata a kernel is about to dereference."""
+        nb = self.kv.num_blocks
+        bt = block_tables.cpu()
+        if bt.numel() and (int(bt.min()) < 0 or int(bt.max()) >= nb):
+            raise AssertionError(f"block table entry outside [0, {nb}): {int(bt.min())}..{int(bt.max())}")
+        lim = nb * self.kv.block_size
+        bad = [x for x in slots if x < 0 or x >= lim]
+        if bad:
+            raise AssertionError(f"slot mapping outside [0, {lim}): {bad[:4]}")
 
     def _run_turns(self, turns: Sequence[Turn]) -> List[TurnOutput]:
         t_start = time.perf_counter()
@@ -337,10 +377,11 @@ class Engine:
                 import warnings
                 warnings.warn(f"hipGraph capture failed under tp={self.tp.size} ({e}); decoding eagerly")
                 self.ecfg.use_graphs = False
-        if runner is not None:
-            toks = runner.run(self, seqs, turns, first, steps, deadline, eos)
-        else:
-            toks = self._decode_eager(seqs, turns, first, steps, deadline, eos)
+        with trace.range(f"decode B={B} steps={steps}"):
+            if runner is not None:
+                toks = runner.run(self, seqs, turns, first, steps, deadline, eos)
+            else:
+                toks = self._decode_eager(seqs, turns, first, steps, deadline, eos)
         gen: List[List[int]] = []
         for b, (s, t) in enumerate(zip(seqs, turns)):
             g = toks[b][:max_new[b]]

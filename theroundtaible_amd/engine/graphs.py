@@ -108,6 +108,8 @@ class DecodeGraph:
         bt = torch.full((self.B, self.maxb), self.scratch, dtype=torch.int32)
         for j, s in enumerate(seqs):
             bt[j, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+        if engine.debug_checks:
+            engine.check_paging(bt, [])
         self.block_tables.copy_(bt.to(dev, non_blocking=True))
         lens = torch.tensor([s.length for s in seqs] + [0] * (self.B - B), dtype=torch.int64)
         self.positions.copy_(lens.to(dev, non_blocking=True))

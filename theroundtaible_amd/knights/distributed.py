@@ -21,6 +21,7 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union
 from ..errors import AdapterError
 from ..parallel.cluster import Cluster
 from ..parallel.exchange import exchange_token_ids
+from ..utils import trace
 from .base import KnightBackend, TurnRequest, TurnResult
 
 
@@ -69,8 +70,9 @@ class DistributedPool:
                 meta[i] = ("ok", None if has_ids else o.text, o.tokenizer, o.metrics)
                 if has_ids:
                     ids_contrib.append((i, list(o.ids)))
-        all_meta = self.cluster.all_gather_object(meta)
-        all_ids = exchange_token_ids(self.cluster, ids_contrib, self.cluster.device)
+        with trace.range("C1 exchange"):
+            all_meta = self.cluster.all_gather_object(meta)
+            all_ids = exchange_token_ids(self.cluster, ids_contrib, self.cluster.device)
         self.exchange_ms.append((time.perf_counter() - t0) * 1e3)
         merged: Dict[int, tuple] = {}
         for m in all_meta:
