@@ -1,6 +1,7 @@
 """`roundtable serve` on a CPU engine: OpenAI + Ollama dialects, batching, session KV reuse."""
 import json
 import threading
+import time
 import urllib.request
 
 import pytest
@@ -103,3 +104,24 @@ def test_bad_requests(server):
 def test_render_chat():
     s = render_chat([{"role": "system", "content": "S"}, {"role": "user", "content": [{"type": "text", "text": "U"}]}])
     assert s.endswith("### Assistent:\n") and "### Systeem:\nS" in s and "### Gebruiker:\nU" in s
+
+
+def test_continuous_batching_admits_midflight(server):
+    """A short request that arrives while a long generation runs joins the running batch at
+    the next chunk boundary and finishes first."""
+    done = {}
+
+    def go(name, n, delay):
+        time.sleep(delay)
+        _post(server.url + "/v1/chat/completions",
+              {"messages": [{"role": "user", "content": name}], "max_tokens": n, "temperature": 0})
+        done[name] = time.perf_counter()
+    before = server.sched.stats["admitted_midflight"]
+    server.sched.chunk = 4
+    ts = [threading.Thread(target=go, args=("lang", 160, 0.0)), threading.Thread(target=go, args=("kort", 4, 0.15))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert server.sched.stats["admitted_midflight"] > before
+    assert done["kort"] < done["lang"]

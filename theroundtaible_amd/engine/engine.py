@@ -347,6 +347,60 @@ class Engine:
         if self.on_gpu:
             torch.cuda.synchronize(self.device)
 
+    # ---- continuous batching (serve.py): admit / step in chunks / retire ----------------------------
+    @torch.no_grad()
+    def start_turns(self, turns: Sequence[Turn]) -> List[Tuple[SeqState, int, Dict[str, float]]]:
+        """Prefill ``turns`` (LCP reuse, delta only) and sample each first token, WITHOUT decoding:
+        returns (sequence, first token, metrics). The first token's K/V is not in the cache yet —
+        it is the input of the next :meth:`continue_decode`."""
+        targets = [self.encode_prompt(t.prompt) for t in turns]
+        seqs, reused = [], []
+        for t, ids in zip(turns, targets):
+            sq, n = self.sync_prefix(t.seq_key, ids)
+            seqs.append(sq)
+            reused.append(n)
+        deltas = [ids[n:] for ids, n in zip(targets, reused)]
+        t0 = time.perf_counter()
+        logits = self.prefill(list(zip(seqs, deltas)))
+        first = self._sample_host(logits, seqs, turns).tolist()
+        ms = (time.perf_counter() - t0) * 1e3
+        self.stats["prefill_tokens"] += sum(len(d) for d in deltas)
+        self.stats["prefill_s"] += ms / 1e3
+        return [(sq, int(f), {"prompt_tokens": len(d) + n, "prefill_tokens": len(d), "reused_tokens": n,
+                              "prefill_ms": ms}) for sq, f, d, n in zip(seqs, first, deltas, reused)]
+
+    @torch.no_grad()
+    def continue_decode(self, seqs: Sequence[SeqState], turns: Sequence[Turn], last: Sequence[int],
+                        steps: int) -> List[List[int]]:
+        """Decode ``steps`` new tokens for every sequence of a (possibly changing) batch, given each
+        sequence's last sampled token (not yet in the KV cache). Afterwards the cache holds every
+        token except the newest one, so calls chain chunk by chunk while sequences join and leave."""
+        if not seqs:
+            return []
+        first = torch.tensor(list(last), dtype=torch.int64, device=self.device)
+        for sq in seqs:
+            self.kv.ensure_capacity(sq, sq.length + steps + 1)
+        chunk = [Turn(t.seq_key, t.prompt, SamplingParams(**{**t.params.__dict__, "max_new_tokens": steps + 1,
+                                                              "ignore_eos": True, "stop_on_consensus": False}),
+                      t.timeout_s) for t in turns]
+        eos = self.tokenizer.eos_id
+        t0 = time.perf_counter()
+        runner = self._graph_for(len(seqs), max(sq.length for sq in seqs) + steps + 1) \
+            if self.on_gpu and self.ecfg.use_graphs else None
+        with trace.range(f"decode chunk B={len(seqs)} steps={steps}"):
+            if runner is not None:
+                toks = runner.run(self, seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos)
+            else:
+                toks = self._decode_eager(seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos)
+        out = []
+        for sq, tk, f in zip(seqs, toks, last):
+            new = list(tk[1:steps + 1])
+            sq.tokens.extend([int(f)] + new[:-1])     # K/V now covers the old last token + all but the newest
+            out.append(new)
+        self.stats["decode_tokens"] += sum(len(n) for n in out)
+        self.stats["decode_s"] += time.perf_counter() - t0
+        return out
+
     def _sample_host(self, logits: torch.Tensor, seqs: Sequence[SeqState], turns: Sequence[Turn]) -> torch.Tensor:
         B = logits.shape[0]
         dev = logits.device

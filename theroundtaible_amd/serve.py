@@ -12,9 +12,9 @@ Serving model:
 
 * one :class:`~theroundtaible_amd.engine.Engine` per process (one process per GPU; run
   several ``serve`` processes for several GPUs);
-* a batching scheduler thread: every request waiting when the engine becomes free joins
-  the next batch (up to ``max_batch``), so concurrent clients share one hipGraph replay
-  per token — the same batching the round table uses for parallel knights;
+* continuous batching (:class:`Scheduler`): between decode chunks finished requests leave
+  and waiting ones are prefilled and join, so concurrent clients share one hipGraph replay
+  per token (up to ``max_batch``) — the batching the round table uses for parallel knights;
 * conversation KV reuse: a request carrying ``"user"`` (OpenAI) or ``"session"`` keeps
   its KV sequence resident under that key, so the next request of the conversation
   prefills only its new tokens (longest-common-prefix reuse, engine.sync_prefix);
@@ -65,16 +65,33 @@ class _Request:
     error: Optional[BaseException] = None
 
 
-class Scheduler:
-    """Single engine worker; batches whatever is queued when the engine frees up."""
+@dataclass
+class _Active:
+    req: _Request
+    seq: Any
+    turn: Turn
+    gen: List[int]
+    metrics: Dict[str, Any]
+    t0: float
 
-    def __init__(self, engine: Engine, max_batch: int = 16, timeout_s: float = 600.0):
+
+class Scheduler:
+    """Continuous batching over one engine.
+
+    Between decode chunks (``chunk`` tokens, one hipGraph replay per token for the whole
+    batch) finished requests leave and waiting ones join: a newcomer is prefilled (delta only,
+    LCP reuse) and its first token sampled, then it decodes in the same batch as everyone
+    else — so a long generation never blocks a short one behind it for more than a chunk.
+    """
+
+    def __init__(self, engine: Engine, max_batch: int = 16, timeout_s: float = 600.0, chunk: int = 16):
         self.engine = engine
         self.max_batch = max(1, int(max_batch))
         self.timeout_s = timeout_s
+        self.chunk = max(1, int(chunk))
         self.q: "queue.Queue[_Request]" = queue.Queue()
         self.stats = {"requests": 0, "batches": 0, "prompt_tokens": 0, "completion_tokens": 0,
-                      "reused_tokens": 0, "busy_s": 0.0, "errors": 0}
+                      "reused_tokens": 0, "busy_s": 0.0, "errors": 0, "admitted_midflight": 0}
         self._stop = threading.Event()
         self._lock = threading.Lock()
         self.thread = threading.Thread(target=self._loop, name="roundtable-serve", daemon=True)
@@ -89,58 +106,109 @@ class Scheduler:
         self.q.put(None)  # type: ignore[arg-type]
         self.thread.join(timeout=5)
 
-    def _take_batch(self) -> List[_Request]:
-        first = self.q.get()
-        if first is None:
-            return []
-        batch, keys, later = [first], {first.key}, []
-        while len(batch) < self.max_batch:
+    # ---- queue --------------------------------------------------------------------------------
+    def _take(self, room: int, busy_keys: set, block: bool) -> List[_Request]:
+        out: List[_Request] = []
+        later: List[_Request] = []
+        keys = set(busy_keys)
+        while len(out) < room:
             try:
-                r = self.q.get_nowait()
+                r = self.q.get(timeout=0.5) if (block and not out) else self.q.get_nowait()
             except queue.Empty:
                 break
             if r is None:
                 self._stop.set()
                 break
-            (later if r.key in keys else batch).append(r)  # one turn per sequence per batch
+            if r.key in keys:          # one in-flight turn per sequence
+                later.append(r)
+                continue
             keys.add(r.key)
+            out.append(r)
         for r in later:
             self.q.put(r)
-        return batch
+        return out
 
-    def _loop(self) -> None:
-        while not self._stop.is_set():
-            batch = self._take_batch()
-            if not batch:
-                continue
-            t0 = time.perf_counter()
-            turns = [Turn(r.key, r.prompt, r.params, timeout_s=self.timeout_s) for r in batch]
+    # ---- completion ---------------------------------------------------------------------------
+    def _finished(self, a: _Active) -> bool:
+        eos = self.engine.tokenizer.eos_id
+        return len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos and eos in a.gen)
+
+    def _complete(self, a: _Active, error: Optional[BaseException] = None) -> None:
+        r = a.req
+        if error is not None:
+            r.error = error
+            with self._lock:
+                self.stats["errors"] += 1
+        else:
+            gen = a.gen[:a.req.params.max_new_tokens]
+            eos = self.engine.tokenizer.eos_id
+            if eos in gen and not a.req.params.ignore_eos:
+                gen = gen[:gen.index(eos) + 1]
+            m = dict(a.metrics, decode_tokens=len(gen), turn_ms=(time.perf_counter() - a.t0) * 1e3)
+            r.result = _Output(self.engine.tokenizer.decode(gen), gen, m)
+            with self._lock:
+                self.stats["requests"] += 1
+                self.stats["prompt_tokens"] += int(m.get("prompt_tokens", 0))
+                self.stats["completion_tokens"] += len(gen)
+                self.stats["reused_tokens"] += int(m.get("reused_tokens", 0))
+        if not r.persistent:
             try:
-                outs = self.engine.run_turns(turns)
-            except BaseException as e:  # noqa: BLE001 - reported per request
-                outs = [e] * len(batch)
-            dt = time.perf_counter() - t0
+                self.engine.release(r.key)
+            except Exception:  # noqa: BLE001
+                pass
+        r.done.set()
+
+    # ---- engine loop --------------------------------------------------------------------------
+    def _loop(self) -> None:
+        active: List[_Active] = []
+        while not self._stop.is_set():
+            new = self._take(self.max_batch - len(active), {a.req.key for a in active}, block=not active)
+            t_busy = time.perf_counter()
+            if new:
+                turns = [Turn(r.key, r.prompt, r.params, timeout_s=self.timeout_s) for r in new]
+                try:
+                    started = self.engine.start_turns(turns)
+                except BaseException as e:  # noqa: BLE001 - reported per request
+                    for r in new:
+                        self._complete(_Active(r, None, None, [], {}, time.perf_counter()), e)
+                    started = []
+                if active and started:
+                    with self._lock:
+                        self.stats["admitted_midflight"] += len(started)
+                for r, t, (sq, first, m) in zip(new, turns, started):
+                    a = _Active(r, sq, t, [first], dict(m, batch=0), time.perf_counter())
+                    if self._finished(a):
+                        self._complete(a)
+                    else:
+                        active.append(a)
+            if not active:
+                continue
+            steps = min(self.chunk, min(a.req.params.max_new_tokens - len(a.gen) for a in active))
+            try:
+                outs = self.engine.continue_decode([a.seq for a in active], [a.turn for a in active],
+                                                   [a.gen[-1] for a in active], max(1, steps))
+            except BaseException as e:  # noqa: BLE001
+                for a in active:
+                    self._complete(a, e)
+                active = []
+                continue
+            for a, toks in zip(active, outs):
+                a.gen.extend(toks)
+                a.metrics["batch"] = max(a.metrics.get("batch", 0), len(active))
             with self._lock:
                 self.stats["batches"] += 1
-                self.stats["busy_s"] += dt
-            for r, o in zip(batch, outs):
-                if isinstance(o, BaseException) or getattr(o, "error", None) is not None:
-                    r.error = o if isinstance(o, BaseException) else o.error
-                    with self._lock:
-                        self.stats["errors"] += 1
-                else:
-                    r.result = o
-                    with self._lock:
-                        self.stats["requests"] += 1
-                        self.stats["prompt_tokens"] += int(o.metrics.get("prompt_tokens", 0))
-                        self.stats["completion_tokens"] += len(o.ids)
-                        self.stats["reused_tokens"] += int(o.metrics.get("reused_tokens", 0))
-                if not r.persistent:
-                    try:
-                        self.engine.release(r.key)
-                    except Exception:  # noqa: BLE001
-                        pass
-                r.done.set()
+                self.stats["busy_s"] += time.perf_counter() - t_busy
+            still = []
+            for a in active:
+                (self._complete(a) if self._finished(a) else still.append(a))
+            active = still
+
+
+@dataclass
+class _Output:
+    text: str
+    ids: List[int]
+    metrics: Dict[str, Any]
 
 
 class RoundtableServer:
