@@ -18,6 +18,8 @@
 // layout of P.V (no LDS round trip for P), as in the decode kernel.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 using rt::bf16x8;
 using rt::float4_;
@@ -225,7 +227,23 @@ __global__ void __launch_bounds__(256) prefill_kernel(
 }
 }  // namespace
 
-int prefill_rows_per_tile(int G) { return G >= 4 ? 16 : 16 * (4 / G); }
+int prefill32_rows(int G);
+int launch_prefill32(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                     const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv,
+                     int max_blocks, float scale, hipStream_t stream);
+
+// D = 128 with G in {1, 2, 4, 8} runs the 32x32-MFMA kernel (attention_prefill32.hip) unless
+// ROUNDTABLE_PREFILL16=1; everything else this file's 16x16 kernel. The host tile map must use
+// the rows of the kernel that will run, hence one function for both.
+static bool use_prefill32(int G, int D) {
+  static const bool off = getenv("ROUNDTABLE_PREFILL16") != nullptr;
+  return !off && D == 128 && prefill32_rows(G) > 0;
+}
+
+int prefill_rows_per_tile(int G, int D) {
+  if (use_prefill32(G, D)) return prefill32_rows(G);
+  return G >= 4 ? 16 : 16 * (4 / G);
+}
 
 // q [T, Hq, D]; tile_map [n_tiles, 2] int32 (sequence, first row).
 int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -234,7 +252,10 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
   if (n_tiles == 0) return 0;
   const int G = Hq / Hkv;
   if (Hq % Hkv || !(G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) return -1;
-  const int rows = prefill_rows_per_tile(G);
+  if (use_prefill32(G, D))
+    return launch_prefill32(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, tile_map, n_tiles, Hq, Hkv,
+                            max_blocks, scale, stream);
+  const int rows = prefill_rows_per_tile(G, D);
   dim3 grid(n_tiles, Hkv), block(256);
   const float sl2 = scale * LOG2E;
 #define RT_PF(DD, HH)                                                                                            \

@@ -1,0 +1,261 @@
+// K4 (D = 128): varlen causal prefill attention on 32x32x16 MFMAs.
+//
+// Same contract as attention_prefill.hip (queries q[cu_q[s]:cu_q[s+1]] at positions
+// start_pos[s] + i attend to cached keys [0, pos]; K/V already in the paged cache), built for
+// arithmetic intensity: each wave owns 32 query rows of one head and every K or V fragment it
+// reads from LDS feeds a full 32x32x16 MFMA (four times the work per LDS byte of the 16x16
+// kernel).
+//
+// Workgroup = 8 waves: wave w -> head hk*G + w%G, rows row0 + 32*(w/G) .. +31 (256/G rows
+// per workgroup: two waves per SIMD, each K/V tile feeds 8 x 32 query rows). Per 64-key
+// tile (two cache blocks):
+//   S^T[64 keys x 32 q] = K . Q^T      2 key blocks x 8 d-chunks   (A = K rows from LDS, B = Q^T regs)
+//   online softmax down each q column (lane-local + one xor-32 shuffle)
+//   O^T[128 d x 32 q] += V^T . P^T     4 d blocks x 4 key chunks   (A = V^T rows from LDS, B = P^T regs)
+// K rows are read in the order key(rho) = rho with bits 2 and 3 swapped, which makes the S^T
+// accumulator of lane (q, h) hold keys 16c + 8h + 0..7 of each 16-key chunk c — exactly the
+// B-operand fragment of P^T — so P never leaves registers; O^T keeps every value of a query
+// column in one lane, so the softmax rescale and the final 1/l are lane-local. V is cached
+// transposed ([d][32 keys] per block), which is the A-operand order of V^T: one 16-byte LDS
+// read per fragment. K/V tiles are register-staged into double-buffered LDS (one barrier
+// per tile), K rows XOR-swizzled in 16-byte chunks, V^T rows padded to 144 B.
+#include "common.h"
+
+namespace {
+using rt::bf16x8;
+using rt::short8;
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int D = 128;
+constexpr int BS = 32;          // cache block
+constexpr int KT = 64;          // keys per tile
+constexpr int KROW = D * 2;     // 256 B per K row
+constexpr int VROW = KT * 2 + 16;  // 144 B per V^T row (64 keys + pad)
+constexpr int KBYTES = KT * KROW;  // 16 KiB
+constexpr int VBYTES = D * VROW;   // 18 KiB
+constexpr int STAGE = KBYTES + VBYTES;
+constexpr float LOG2E = 1.4426950408889634f;
+
+RT_DEVICE int swap23(int x) { return (x & ~12) | ((x & 4) << 1) | ((x & 8) >> 1); }
+
+template <int NW>
+struct Loader {
+  // per thread: K 16 KiB / (64*NW) and V 16 KiB / (64*NW) bytes, 16 B per load
+  static constexpr int KL = KBYTES / (64 * NW * 16);
+  static constexpr int VL = (D * KT * 2) / (64 * NW * 16);
+  uint4 k[KL], v[VL];
+
+  RT_DEVICE void load(const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache, const int* bt,
+                      int tile, int max_blocks, size_t blk_stride, size_t head_off, int tid) {
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const int ch = tid * KL + i;          // 16-B chunk of the 64x128 K tile
+      const int row = ch >> 4, c = ch & 15;  // key, d-chunk
+      const int bi = 2 * tile + (row >> 5);
+      const int blk = bt[bi < max_blocks ? bi : 0];
+      k[i] = *reinterpret_cast<const uint4*>(k_cache + (size_t)blk * blk_stride + head_off + (row & 31) * D + 8 * c);
+    }
+#pragma unroll
+    for (int i = 0; i < VL; ++i) {
+      const int ch = tid * VL + i;          // 16-B chunk of the two [128 d][32 key] V blocks
+      const int half = ch >> 9;              // 512 chunks per block
+      const int w = ch & 511, d = w >> 2, c = w & 3;
+      const int bi = 2 * tile + half;
+      const int blk = bt[bi < max_blocks ? bi : 0];
+      v[i] = *reinterpret_cast<const uint4*>(v_cache + (size_t)blk * blk_stride + head_off + d * BS + 8 * c);
+    }
+  }
+  RT_DEVICE void store(unsigned char* kb, unsigned char* vb, int tid) const {
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const int ch = tid * KL + i;
+      const int row = ch >> 4, c = ch & 15;
+      *reinterpret_cast<uint4*>(kb + row * KROW + 16 * (c ^ (row & 15))) = k[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VL; ++i) {
+      const int ch = tid * VL + i;
+      const int half = ch >> 9;
+      const int w = ch & 511, d = w >> 2, c = w & 3;
+      *reinterpret_cast<uint4*>(vb + d * VROW + 64 * half + 16 * c) = v[i];
+    }
+  }
+};
+
+template <int G, int NW>
+__global__ void __launch_bounds__(NW * 64) prefill32_kernel(
+    uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ cu_q,
+    const int* __restrict__ start_pos, const int* __restrict__ tile_map, int Hq, int Hkv, int max_blocks,
+    float scale_log2, int rows_per_tile) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];   // 68 KiB: static (> 64 KiB)
+  const int tile = blockIdx.x, hk = blockIdx.y;
+  const int s = tile_map[2 * tile], row0 = tile_map[2 * tile + 1];
+  const int q_begin = cu_q[s], q_end = cu_q[s + 1];
+  const int sp = start_pos[s];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 31, h = lane >> 5;   // MFMA column (query) and k-half
+
+  const int head = hk * G + (wid % G);
+  const int wrow0 = row0 + 32 * (wid / G);
+  const int tile_rows_end = min(row0 + rows_per_tile, q_end);
+  const int kmax = sp + (tile_rows_end - q_begin);  // keys [0, kmax) for the whole workgroup
+  const int ntiles = (kmax + KT - 1) / KT;
+  const int my_row = min(wrow0 + c, q_end - 1);
+  const int my_pos = sp + (my_row - q_begin);
+  // keys this wave can ever see (tiles past it are still loaded cooperatively, math skipped)
+  const int wave_rows_end = min(wrow0 + 32, q_end);
+  const int wave_kmax = sp + (wave_rows_end - q_begin);
+  const int wave_min_pos = sp + (min(wrow0, q_end - 1) - q_begin);   // first row of the wave
+
+  // Q^T B-fragments: lane (q = c, h) holds Q[q][16 dk + 8 h + j]
+  short8 qf[D / 16];
+  {
+    const uint16_t* qr = q + ((size_t)my_row * Hq + head) * D + 8 * h;
+#pragma unroll
+    for (int dk = 0; dk < D / 16; ++dk) qf[dk] = *reinterpret_cast<const short8*>(qr + 16 * dk);
+  }
+  f16v o[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[db][i] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
+
+  const int* bt = block_tables + (size_t)s * max_blocks;
+  const size_t blk_stride = (size_t)Hkv * BS * D;
+  const size_t head_off = (size_t)hk * BS * D;
+  Loader<NW> ld;
+  if (ntiles > 0) {
+    ld.load(k_cache, v_cache, bt, 0, max_blocks, blk_stride, head_off, tid);
+    ld.store(smem, smem + KBYTES, tid);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) ld.load(k_cache, v_cache, bt, t + 1, max_blocks, blk_stride, head_off, tid);
+    const unsigned char* kb = smem + buf * STAGE;
+    const unsigned char* vb = kb + KBYTES;
+    if (t * KT < wave_kmax) {
+      // ---- S^T = K Q^T (two 32-key blocks) ----
+      f16v sc[2];
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[blk][i] = 0.f;
+        const int krow = 32 * blk + swap23(c);
+#pragma unroll
+        for (int dk = 0; dk < D / 16; ++dk) {
+          const int ch = 2 * dk + h;
+          const short8 a = *reinterpret_cast<const short8*>(kb + krow * KROW + 16 * (ch ^ (krow & 15)));
+          sc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                            __builtin_bit_cast(bf16x8, qf[dk]), sc[blk], 0, 0, 0);
+        }
+      }
+      // ---- online softmax down column c: reg i of block blk holds key 64t + 32blk + 16(i>>3) + 8h + (i&7)
+      float tmax = -INFINITY;
+      if ((t + 1) * KT - 1 <= wave_min_pos) {   // whole tile visible to every row of the wave
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float v = sc[blk][i] * scale_log2;
+            sc[blk][i] = v;
+            tmax = fmaxf(tmax, v);
+          }
+      } else {                                  // diagonal tile: causal mask per element
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = t * KT + 32 * blk + 16 * (i >> 3) + 8 * h + (i & 7);
+            float v = sc[blk][i] * scale_log2;
+            v = key <= my_pos ? v : -INFINITY;
+            sc[blk][i] = v;
+            tmax = fmaxf(tmax, v);
+          }
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+      m = mnew;
+      short8 pf[4];   // P^T B-fragments per 16-key chunk
+      float psum = 0.f;
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = (mnew == -INFINITY) ? 0.f : exp2f(sc[kc >> 1][8 * (kc & 1) + j] - mnew);
+          psum += p;
+          pf[kc][j] = (short)rt::f2bf(p);
+        }
+      lsum = lsum * alpha + psum;
+      // ---- O^T = alpha O^T + V^T P^T ----
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        // one d-block's 4 V^T fragments live at a time (16 VGPRs, not 64): keep the scheduler
+        // from hoisting every block's LDS reads to the top
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[db][i] *= alpha;
+        const unsigned char* vr = vb + (32 * db + c) * VROW + 16 * h;
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+          const short8 a = *reinterpret_cast<const short8*>(vr + 32 * kc);
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                          __builtin_bit_cast(bf16x8, pf[kc]), o[db], 0, 0, 0);
+        }
+      }
+    }
+    // buffer buf^1 held tile t-1, which every wave finished before the previous barrier
+    if (t + 1 < ntiles) ld.store(smem + (buf ^ 1) * STAGE, smem + (buf ^ 1) * STAGE + KBYTES, tid);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane (q = c, h) holds O^T[d = 32db + 8b + 4h + j][q], reg i = 4b + j ----
+  lsum += __shfl_xor(lsum, 32, 64);
+  const int row = wrow0 + c;
+  if (row < q_end && row < row0 + rows_per_tile) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    uint16_t* orow = out + ((size_t)row * Hq + head) * D;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        uint2 pk;
+        pk.x = rt::pack2(o[db][4 * b] * inv, o[db][4 * b + 1] * inv);
+        pk.y = rt::pack2(o[db][4 * b + 2] * inv, o[db][4 * b + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * db + 8 * b + 4 * h) = pk;
+      }
+  }
+}
+}  // namespace
+
+// rows of one work tile for group size G (D = 128); 0 = unsupported (use attention_prefill.hip)
+int prefill32_rows(int G) {
+  if (G == 1 || G == 2 || G == 4 || G == 8) return 32 * 8 / G;   // 8 waves x 32 rows over G heads
+  return 0;
+}
+
+int launch_prefill32(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                     const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv,
+                     int max_blocks, float scale, hipStream_t stream) {
+  const int G = Hq / Hkv;
+  const int rows = prefill32_rows(G);
+  if (rows == 0) return -1;
+  const float sl2 = scale * LOG2E;
+  dim3 grid(n_tiles, Hkv);
+#define RT_P32(GG, NWV)                                                                                          \
+  hipLaunchKernelGGL((prefill32_kernel<GG, NWV>), grid, dim3(64 * NWV), 0, stream, (uint16_t*)out,              \
+                     (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, \
+                     start_pos, tile_map, Hq, Hkv, max_blocks, sl2, rows)
+  switch (G) {
+    case 1: RT_P32(1, 8); break;
+    case 2: RT_P32(2, 8); break;
+    case 4: RT_P32(4, 8); break;
+    default: RT_P32(8, 8); break;
+  }
+#undef RT_P32
+  return 0;
+}

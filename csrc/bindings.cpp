@@ -16,7 +16,7 @@ void launch_gelu(void* out, const void* x, int64_t n, hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, hipStream_t stream);
-int prefill_rows_per_tile(int G);
+int prefill_rows_per_tile(int G, int D);
 int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                    const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv, int D,
                    int max_blocks, float scale, hipStream_t stream);
@@ -427,7 +427,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fused_add_layer_norm", &fused_add_layer_norm);
   m.def("rope_and_cache", &rope_and_cache);
   m.def("paged_attention_decode", &paged_attention_decode);
-  m.def("prefill_rows_per_tile", &prefill_rows_per_tile);
+  m.def("prefill_rows_per_tile", &prefill_rows_per_tile, py::arg("G"), py::arg("D") = 128);
   m.def("prefill_attention", &prefill_attention);
   m.def("silu_and_mul", &silu_and_mul);
   m.def("gelu_tanh", &gelu_tanh);

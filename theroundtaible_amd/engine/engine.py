@@ -249,8 +249,9 @@ class Engine:
             if self.debug_checks:
                 self.check_paging(bt, slots)
             if self.on_gpu:
-                rows = ops.native().prefill_rows_per_tile(self.model.n_heads // self.model.n_kv_heads)
-                meta.tile_map = ops.prefill_tile_map(cu_t, rows).to(dev, non_blocking=True)
+                rows = ops.native().prefill_rows_per_tile(self.model.n_heads // self.model.n_kv_heads,
+                                                          self.cfg.head_dim)
+                meta.tile_map = ops.prefill_tile_map(cu_t, rows, torch.tensor(starts)).to(dev, non_blocking=True)
             with trace.range("prefill"):
                 logits = self.model.forward(torch.tensor(tok, dtype=torch.int64).to(dev, non_blocking=True),
                                             torch.tensor(pos, dtype=torch.int64).to(dev, non_blocking=True),

@@ -142,8 +142,8 @@ def bench_prefill(T):
     bt = torch.arange(nblk, device=DEV, dtype=torch.int32)[None]
     cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
     sp = torch.zeros(1, device=DEV, dtype=torch.int32)
-    rows = ops.native().prefill_rows_per_tile(hq // hkv)
-    tm = ops.prefill_tile_map(cu.cpu(), rows).to(DEV)
+    rows = ops.native().prefill_rows_per_tile(hq // hkv, d)
+    tm = ops.prefill_tile_map(cu.cpu(), rows, sp.cpu()).to(DEV)
     flops = 4 * hq * d * T * T / 2
     us = timed(lambda i: ops.prefill_attention(q, kc, vc, bt, cu, sp, 1 / math.sqrt(d), tm), iters=5, reps=3)
     row(f"prefill attn causal T={T}", us, None, flops)
