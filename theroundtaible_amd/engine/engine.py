@@ -93,6 +93,8 @@ class Engine:
         self.cfg: ModelConfig = get_config(ecfg.model, **ecfg.model_overrides)
         self.device = torch.device(ecfg.device)
         self.on_gpu = self.device.type == "cuda"
+        if self.on_gpu and self.tp.size > 1 and self.tp.backend() != "nccl":
+            ecfg.use_graphs = False      # host-staged (gloo) collectives cannot be captured in a hipGraph
         self.dtype = _dtype(ecfg.dtype)
         if not self.on_gpu and self.dtype == torch.float16:
             self.dtype = torch.float32

@@ -22,7 +22,7 @@ class Cluster:
     rank: int = 0
     world: int = 1
     local_rank: int = 0
-    device: str = "cpu"
+    device: str = "cpu"      # this rank's device: cuda:LOCAL_RANK (or shared round-robin in rehearsal mode)
     backend: str = "none"
     cpu_group: Optional[object] = None
 
@@ -83,15 +83,20 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = prefer_gpu and torch.cuda.is_available()
-    device = f"cuda:{local}" if use_gpu else "cpu"
+    # Rehearsal mode (ROUNDTABLE_DIST_BACKEND=gloo): more ranks than GPUs share devices round-robin
+    # and the data plane runs over gloo (RCCL refuses two ranks on one GPU) — lets a 1-GPU box run
+    # the multi-rank GPU path (engines, hipGraphs, C1 exchange, TP collectives) end to end.
+    forced = os.environ.get("ROUNDTABLE_DIST_BACKEND", "").strip().lower()
+    gpu_index = local % max(1, torch.cuda.device_count()) if use_gpu and forced == "gloo" else local
+    device = f"cuda:{gpu_index}" if use_gpu else "cpu"
     if use_gpu:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(gpu_index)
     c = Cluster(rank=rank, world=world, local_rank=local, device=device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if use_gpu else "gloo"
+        backend = forced if forced in ("nccl", "gloo") else ("nccl" if use_gpu else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu:
+        if backend == "nccl":
             kw["device_id"] = torch.device(device)
         dist.init_process_group(**kw)
         c.backend = backend

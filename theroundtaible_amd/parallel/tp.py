@@ -33,18 +33,32 @@ class TPInfo:
             raise ValueError(f"dimension {n} not divisible by tp={self.size}")
         return n // self.size
 
+    def backend(self) -> str:
+        return dist.get_backend(self.group) if self.size > 1 else "none"
+
+    def _host_staged(self, x: torch.Tensor) -> bool:
+        # gloo (CPU CI, or the shared-GPU rehearsal mode of parallel/cluster.py) moves GPU
+        # tensors through host memory explicitly; RCCL works on device memory directly
+        return x.is_cuda and self.backend() == "gloo"
+
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
-            dist.all_reduce(x, group=self.group)
+            if self._host_staged(x):
+                h = x.cpu()
+                dist.all_reduce(h, group=self.group)
+                x.copy_(h)
+            else:
+                dist.all_reduce(x, group=self.group)
         return x
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """Concatenate shards along the last dim (vocab-parallel logits)."""
         if self.size == 1:
             return x
-        parts: List[torch.Tensor] = [torch.empty_like(x) for _ in range(self.size)]
-        dist.all_gather(parts, x.contiguous(), group=self.group)
-        return torch.cat(parts, dim=-1)
+        src = x.contiguous().cpu() if self._host_staged(x) else x.contiguous()
+        parts: List[torch.Tensor] = [torch.empty_like(src) for _ in range(self.size)]
+        dist.all_gather(parts, src, group=self.group)
+        return torch.cat(parts, dim=-1).to(x.device)
 
 
 def shard_rows(w: torch.Tensor, tp: TPInfo) -> torch.Tensor:
