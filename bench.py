@@ -160,6 +160,9 @@ def main() -> int:
                 dec += int(e.metrics.get("decode_tokens", 0))
                 pre += int(e.metrics.get("prefill_tokens", 0))
                 reused += int(e.metrics.get("reused_tokens", 0))
+    failures = [f for o in orchs for f in o.failures]
+    if failures:
+        print(f"[rank {cl.rank}] {len(failures)} failed knight turns; first: {failures[0]}", file=sys.stderr, flush=True)
     exch = sum(pool.exchange_ms[-args.steps:]) / max(1, args.steps) if pool.exchange_ms else 0.0
     ms_round = elapsed / max(1, args.steps) * 1e3
     value = dec / elapsed if elapsed > 0 else 0.0
@@ -177,7 +180,7 @@ def main() -> int:
                    "round_mode": args.round_mode, "prompt_layout": args.layout,
                    "parallelism": (f"knight-placement x{N} (tables striped over GPUs), C1 all-gather" if T == 1 else
                                    f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL")},
-        "detail": {"decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
+        "detail": {"failed_turns": len(failures), "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
                    "kv_capacity_tokens": engine.kv_capacity_tokens},

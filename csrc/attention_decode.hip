@@ -6,10 +6,10 @@
 namespace {
 using namespace attn;
 
-template <int D>
+template <int D, int GM>
 __global__ void __launch_bounds__(NW * 64) paged_decode_kernel(AttnArgs p) {
-  __shared__ AttnSmem<D> sm;
-  attn_item<D, false>(p, blockIdx.x, blockIdx.y, sm);
+  __shared__ AttnSmem<D, GM> sm;
+  attn_item<D, false, GM>(p, blockIdx.x, blockIdx.y, sm);
 }
 }  // namespace
 
@@ -27,11 +27,16 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   const float sl2 = scale * LOG2E;
   const AttnArgs args{(uint16_t*)out, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
                       block_tables, ctx_lens, part_o, part_ml, counters, Hq, Hkv, max_blocks, sl2, num_splits};
-  if (D == 128)
-    hipLaunchKernelGGL((paged_decode_kernel<128>), grid, block, 0, stream, args);
-  else if (D == 64)
-    hipLaunchKernelGGL((paged_decode_kernel<64>), grid, block, 0, stream, args);
-  else
-    return -2;
+  const int G = Hq / Hkv;
+#define RT_PD(DV)                                                                                  \
+  do {                                                                                             \
+    if (G <= 4) hipLaunchKernelGGL((paged_decode_kernel<DV, 4>), grid, block, 0, stream, args);   \
+    else if (G <= 8) hipLaunchKernelGGL((paged_decode_kernel<DV, 8>), grid, block, 0, stream, args); \
+    else hipLaunchKernelGGL((paged_decode_kernel<DV, 16>), grid, block, 0, stream, args);         \
+  } while (0)
+  if (D == 128) RT_PD(128);
+  else if (D == 64) RT_PD(64);
+  else return -2;
+#undef RT_PD
   return 0;
 }

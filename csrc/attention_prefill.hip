@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) prefill_kernel(
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(m[hh], tmax);
-      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m[hh] - mnew);
+      const float alpha = (mnew == -INFINITY) ? 1.f : rt::fast_exp2(m[hh] - mnew);
       m[hh] = mnew;
       float psum = 0.f;
       short8 pa;
@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256) prefill_kernel(
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = (mnew == -INFINITY) ? 0.f : exp2f(sc[h][i] - mnew);
+          const float p = (mnew == -INFINITY) ? 0.f : rt::fast_exp2(sc[h][i] - mnew);
           psum += p;
           pa[4 * h + i] = (short)rt::f2bf(p);
         }

@@ -43,26 +43,37 @@ struct Loader {
   // per thread: K 16 KiB / (64*NW) and V 16 KiB / (64*NW) bytes, 16 B per load
   static constexpr int KL = KBYTES / (64 * NW * 16);
   static constexpr int VL = (D * KT * 2) / (64 * NW * 16);
-  uint4 k[KL], v[VL];
+  rt::u32x4 k[KL], v[VL];   // native vectors: HIP's uint4 class defeats SROA (private-memory spill)
+  int kblk[KL], vblk[VL];   // cache blocks of the NEXT tile to load (fetched one tile ahead)
 
-  RT_DEVICE void load(const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache, const int* bt,
-                      int tile, int max_blocks, size_t blk_stride, size_t head_off, int tid) {
+  // block-table indirection software-pipelined one tile ahead, so a tile's K/V loads never
+  // wait on a dependent block-table load
+  RT_DEVICE void fetch_blocks(const int* bt, int tile, int max_blocks, int tid) {
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const int bi = 2 * tile + (((tid * KL + i) >> 4) >> 5);
+      kblk[i] = bt[bi < max_blocks ? bi : 0];
+    }
+#pragma unroll
+    for (int i = 0; i < VL; ++i) {
+      const int bi = 2 * tile + ((tid * VL + i) >> 9);
+      vblk[i] = bt[bi < max_blocks ? bi : 0];
+    }
+  }
+  RT_DEVICE void load(const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
+                      size_t blk_stride, size_t head_off, int tid) {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
       const int ch = tid * KL + i;          // 16-B chunk of the 64x128 K tile
       const int row = ch >> 4, c = ch & 15;  // key, d-chunk
-      const int bi = 2 * tile + (row >> 5);
-      const int blk = bt[bi < max_blocks ? bi : 0];
-      k[i] = *reinterpret_cast<const uint4*>(k_cache + (size_t)blk * blk_stride + head_off + (row & 31) * D + 8 * c);
+      k[i] = *reinterpret_cast<const rt::u32x4*>(k_cache + (size_t)kblk[i] * blk_stride + head_off + (row & 31) * D +
+                                                 8 * c);
     }
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
       const int ch = tid * VL + i;          // 16-B chunk of the two [128 d][32 key] V blocks
-      const int half = ch >> 9;              // 512 chunks per block
       const int w = ch & 511, d = w >> 2, c = w & 3;
-      const int bi = 2 * tile + half;
-      const int blk = bt[bi < max_blocks ? bi : 0];
-      v[i] = *reinterpret_cast<const uint4*>(v_cache + (size_t)blk * blk_stride + head_off + d * BS + 8 * c);
+      v[i] = *reinterpret_cast<const rt::u32x4*>(v_cache + (size_t)vblk[i] * blk_stride + head_off + d * BS + 8 * c);
     }
   }
   RT_DEVICE void store(unsigned char* kb, unsigned char* vb, int tid) const {
@@ -70,14 +81,14 @@ struct Loader {
     for (int i = 0; i < KL; ++i) {
       const int ch = tid * KL + i;
       const int row = ch >> 4, c = ch & 15;
-      *reinterpret_cast<uint4*>(kb + row * KROW + 16 * (c ^ (row & 15))) = k[i];
+      *reinterpret_cast<rt::u32x4*>(kb + row * KROW + 16 * (c ^ (row & 15))) = k[i];
     }
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
       const int ch = tid * VL + i;
       const int half = ch >> 9;
       const int w = ch & 511, d = w >> 2, c = w & 3;
-      *reinterpret_cast<uint4*>(vb + d * VROW + 64 * half + 16 * c) = v[i];
+      *reinterpret_cast<rt::u32x4*>(vb + d * VROW + 64 * half + 16 * c) = v[i];
     }
   }
 };
@@ -128,13 +139,22 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
   const size_t head_off = (size_t)hk * BS * D;
   Loader<NW> ld;
   if (ntiles > 0) {
-    ld.load(k_cache, v_cache, bt, 0, max_blocks, blk_stride, head_off, tid);
+    ld.fetch_blocks(bt, 0, max_blocks, tid);
+    ld.load(k_cache, v_cache, blk_stride, head_off, tid);
     ld.store(smem, smem + KBYTES, tid);
+    if (ntiles > 1) ld.fetch_blocks(bt, 1, max_blocks, tid);
   }
+  // Q^T and tile 0 landed: without this explicit drain the waitcnt pass, merging the
+  // ntiles == 0 path at the loop header, waits on qf inside the loop with vmcnt(n..0) —
+  // which also drains the next tile's prefetch every iteration (no copy/compute overlap).
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) ld.load(k_cache, v_cache, bt, t + 1, max_blocks, blk_stride, head_off, tid);
+    if (t + 1 < ntiles) {
+      ld.load(k_cache, v_cache, blk_stride, head_off, tid);
+      if (t + 2 < ntiles) ld.fetch_blocks(bt, t + 2, max_blocks, tid);
+    }
     const unsigned char* kb = smem + buf * STAGE;
     const unsigned char* vb = kb + KBYTES;
     if (t * KT < wave_kmax) {
@@ -178,18 +198,23 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
       }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(m, tmax);
-      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+      const float alpha = (mnew == -INFINITY) ? 1.f : rt::fast_exp2(m - mnew);
       m = mnew;
       short8 pf[4];   // P^T B-fragments per 16-key chunk
       float psum = 0.f;
+      const float msub = (mnew == -INFINITY) ? 0.f : mnew;   // all-masked column: exp2(-inf) = 0
 #pragma unroll
-      for (int kc = 0; kc < 4; ++kc)
+      for (int kc = 0; kc < 4; ++kc) {
+        rt::u32x4 w;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float p = (mnew == -INFINITY) ? 0.f : exp2f(sc[kc >> 1][8 * (kc & 1) + j] - mnew);
-          psum += p;
-          pf[kc][j] = (short)rt::f2bf(p);
+        for (int j = 0; j < 4; ++j) {
+          const float p0 = rt::fast_exp2(sc[kc >> 1][8 * (kc & 1) + 2 * j] - msub);
+          const float p1 = rt::fast_exp2(sc[kc >> 1][8 * (kc & 1) + 2 * j + 1] - msub);
+          psum += p0 + p1;
+          w[j] = rt::pack2(p0, p1);
         }
+        pf[kc] = __builtin_bit_cast(short8, w);
+      }
       lsum = lsum * alpha + psum;
       // ---- O^T = alpha O^T + V^T P^T ----
 #pragma unroll

@@ -80,13 +80,15 @@ struct AttnArgs {
   int num_splits;
 };
 
-template <int D>
+// GM = max query heads per kv head the LDS is sized for (G <= GM). GM = 4 (Llama-3-8B,
+// Mistral-7B) keeps the workgroup at ~26 KB so two fit a CU: 16 waves streaming K/V per CU.
+template <int D, int GM = 16>
 struct AttnSmem {
   float s_m[NW][16];
   float s_l[NW][16];
-  float s_o[NW][16][D + 4];
-  float s_wt[16][MAXS];
-  float s_lt[16][MAXS];
+  float s_o[NW][GM][D + 4];
+  float s_wt[GM][MAXS];
+  float s_lt[GM][MAXS];
   int s_last;
 };
 
@@ -103,8 +105,8 @@ RT_DEVICE void store_bf16x4(uint16_t* dst, float a, float b_, float c, float d, 
 
 // One (sequence, kv head, key split) work item. Returns true when this workgroup wrote the
 // item's final output rows (no split, or the last-arriving split that combined them).
-template <int D, bool SC1>
-RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D>& S) {
+template <int D, bool SC1, int GM = 16>
+RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& S) {
   uint16_t* __restrict__ out = P.out;
   const uint16_t* __restrict__ q = P.q;
   const uint16_t* __restrict__ k_cache = P.k_cache;
@@ -195,18 +197,19 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D>& S) {
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mnew);  // m=-inf first time -> 0
+    const float alpha = rt::fast_exp2(m - mnew);  // m=-inf first time -> 0
     m = mnew;
     float psum = 0.f;
-    short8 pa;
+    rt::u32x4 pw;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(s[h][i] - mnew);
-        psum += p;
-        pa[4 * h + i] = (short)rt::f2bf(p);
+      for (int i = 0; i < 2; ++i) {
+        const float p0 = rt::fast_exp2(s[h][2 * i] - mnew), p1 = rt::fast_exp2(s[h][2 * i + 1] - mnew);
+        psum += p0 + p1;
+        pw[2 * h + i] = rt::pack2(p0, p1);
       }
+    const short8 pa = __builtin_bit_cast(short8, pw);
     lsum = lsum * alpha + psum;
     // rows of O held by this lane are q = 4g + i: fetch their alphas from lanes 4g + i
     float al[4];

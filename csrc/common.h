@@ -19,13 +19,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // bf16 <-> f32 by bit manipulation (round-to-nearest-even on the way down; NaN kept NaN).
 RT_DEVICE float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
-RT_DEVICE uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// f32 -> bf16 (RNE, NaN-preserving) on the gfx950 converter: one v_cvt_pk_bf16_f32 per PAIR.
+// (A bit-twiddled RNE costs ~5 VALU + an exec-masked NaN branch per element — in the
+// attention P conversion that was the largest VALU block of the loop.)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+RT_DEVICE uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+RT_DEVICE uint32_t pack2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
-RT_DEVICE uint32_t pack2(float lo, float hi) { return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16); }
+// raw v_exp_f32 (2^x): exp2f adds a denormal-range rescale (cmp, 2 cndmask, add, ldexp) per call;
+// softmax arguments are <= 0 and results below 2^-126 are negligible against the row sum
+RT_DEVICE float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 template <typename T> struct DT;
 template <> struct DT<uint16_t> {  // bf16 storage

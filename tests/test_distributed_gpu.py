@@ -28,18 +28,20 @@ def _bench(extra=()):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
-    return json.loads(line)
+    out = json.loads(line)
+    out["_log"] = r.stdout[-3000:] + r.stderr[-3000:]
+    return out
 
 
 def test_two_rank_bench_on_shared_gpu():
     out = _bench()
     assert out["n_gpus"] == 2 and out["dtype"] == "bf16"
     assert out["config"]["knights"] == 6 and out["config"]["tables"] == 2
-    assert out["detail"]["decode_tokens"] == 6 * 16 * 2
+    assert out["detail"]["decode_tokens"] == 6 * 16 * 2, out["_log"]
     assert out["value"] > 0
 
 
 def test_two_rank_tp2_bench_on_shared_gpu():
     out = _bench(("--tp", "2", "--knights-per-table", "2", "--knights-per-gpu", "2"))
     assert "tp2" in out["config"]["parallelism"]
-    assert out["detail"]["decode_tokens"] == 2 * 16 * 2
+    assert out["detail"]["decode_tokens"] == 2 * 16 * 2, out["_log"]

@@ -125,6 +125,7 @@ class Orchestrator:
         self.opt = options or RunOptions()
         self.backend_factory = backend_factory
         self.rng = random.Random(self.opt.shuffle_seed)
+        self.failures: List[Tuple[str, str, str]] = []   # (knight, error kind, message) per failed turn
         self.round_mode = self.opt.round_mode or config.rules.round_mode
         self.layout = self.opt.prompt_layout or config.rules.prompt_layout
         # append layout: transcript segments shared by every knight (grows append-only)
@@ -212,6 +213,7 @@ class Orchestrator:
 
     def _report_failure(self, knight: KnightConfig, err: BaseException) -> None:
         c = classify_error(err, knight.name)
+        self.failures.append((knight.name, c.kind, c.message))
         self.ui.error(f"  {knight.name} crashed and burned")
         self.ui.error(f"  Error ({c.kind}): {c.message}")
         hint = HINTS.get(c.kind, "").format(adapter=knight.adapter)
