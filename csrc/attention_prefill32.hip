@@ -100,7 +100,10 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
     const int* __restrict__ start_pos, const int* __restrict__ tile_map, int Hq, int Hkv, int max_blocks,
     float scale_log2, int rows_per_tile) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];   // 68 KiB: static (> 64 KiB)
-  const int tile = blockIdx.x, hk = blockIdx.y;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (id mod 8), so with
+  // id = tile * Hkv + hk every workgroup of kv head hk lands on XCD hk (Hkv = 8): that head's
+  // K/V (2 MiB at 4K tokens) stays in one XCD's 4 MiB L2 instead of streaming from MALL/HBM.
+  const int tile = blockIdx.x / Hkv, hk = blockIdx.x - (blockIdx.x / Hkv) * Hkv;
   const int s = tile_map[2 * tile], row0 = tile_map[2 * tile + 1];
   const int q_begin = cu_q[s], q_end = cu_q[s + 1];
   const int sp = start_pos[s];
@@ -270,7 +273,7 @@ int launch_prefill32(void* out, const void* q, const void* k_cache, const void* 
   const int rows = prefill32_rows(G);
   if (rows == 0) return -1;
   const float sl2 = scale * LOG2E;
-  dim3 grid(n_tiles, Hkv);
+  dim3 grid(n_tiles * Hkv);
 #define RT_P32(GG, NWV)                                                                                          \
   hipLaunchKernelGGL((prefill32_kernel<GG, NWV>), grid, dim3(64 * NWV), 0, stream, (uint16_t*)out,              \
                      (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, \
