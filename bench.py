@@ -57,6 +57,7 @@ def parse():
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--kv-fraction", type=float, default=0.85,
                    help="fraction of free HBM for the KV pool (lower it when ranks share a GPU)")
+    p.add_argument("--max-kv-tokens", type=int, default=None, help="cap the KV pool (tokens per engine)")
     p.add_argument("--device", default=None, help="override device (cpu for a plumbing run)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
@@ -108,7 +109,7 @@ def main() -> int:
     engine = Engine(EngineConfig(model=args.model, weights=f"random:{1234}", device=device,
                                  use_graphs=not args.no_graphs and device != "cpu",
                                  dtype="bf16" if device != "cpu" else "fp32",
-                                 kv_cache_fraction=args.kv_fraction), tp)
+                                 kv_cache_fraction=args.kv_fraction, max_kv_tokens=args.max_kv_tokens), tp)
     params = SamplingParams(temperature=args.temperature, top_p=args.top_p, max_new_tokens=args.new_tokens,
                             ignore_eos=True, stop_on_consensus=False, seed=7)
     import threading

@@ -34,6 +34,8 @@ int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, i
 int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
                        const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
                        int64_t vocab, hipStream_t stream);
+int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
+                        int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream);
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
                           const int64_t* next, int B, int max_steps, hipStream_t stream);
 int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, const void* wo, const void* wgu,
@@ -335,6 +337,33 @@ void decode_advance(torch::Tensor out, torch::Tensor ids, torch::Tensor position
                         (int)out.size(0), cur_stream());
 }
 
+// Debug paging guard (csrc/decode_step.hip): err[0] |= violation code; capturable.
+void paging_guard(torch::Tensor block_tables, torch::Tensor ctx_lens, c10::optional<torch::Tensor> positions,
+                  c10::optional<torch::Tensor> slots, torch::Tensor err, int64_t num_blocks, int64_t block_size) {
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_type(ctx_lens, torch::kInt32, "ctx_lens");
+  check_type(err, torch::kInt32, "err");
+  const int64_t B = ctx_lens.numel();
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.is_contiguous(),
+              "paging_guard: block_tables [B, max_blocks]");
+  const int64_t* pp = nullptr;
+  const int64_t* sp = nullptr;
+  if (positions && positions->defined()) {
+    check_type(*positions, torch::kInt64, "positions");
+    TORCH_CHECK(positions->numel() >= B, "paging_guard: positions");
+    pp = positions->data_ptr<int64_t>();
+  }
+  if (slots && slots->defined()) {
+    check_type(*slots, torch::kInt64, "slots");
+    TORCH_CHECK(slots->numel() >= B, "paging_guard: slots");
+    sp = slots->data_ptr<int64_t>();
+  }
+  const int rc = launch_paging_guard(block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), pp, sp,
+                                     err.data_ptr<int>(), (int)B, (int)block_tables.size(1), (int)num_blocks,
+                                     (int)block_size, cur_stream());
+  TORCH_CHECK(rc == 0, "paging_guard: rc=", rc);
+}
+
 // Persistent decode layer (csrc/decode_layer.hip): one launch = qkv -> attention -> o -> gate_up -> down.
 void decode_layer(torch::Tensor res, torch::Tensor q, torch::Tensor a, torch::Tensor g, torch::Tensor wqkv,
                   torch::Tensor wo, torch::Tensor wgu, torch::Tensor wd, torch::Tensor positions, torch::Tensor cos_sin,
@@ -415,6 +444,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Hkv"), py::arg("num_splits"), py::arg("eps"), py::arg("scale"), py::arg("stamps") = py::none());
   m.def("decode_layer_grid", &decode_layer_grid);
   m.def("decode_advance", &decode_advance);
+  m.def("paging_guard", &paging_guard, py::arg("block_tables"), py::arg("ctx_lens"), py::arg("positions"),
+        py::arg("slots"), py::arg("err"), py::arg("num_blocks"), py::arg("block_size"));
   m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));
   m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write",
         py::arg("q_out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("positions"), py::arg("cos_sin"),

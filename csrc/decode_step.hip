@@ -64,3 +64,46 @@ int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* c
                      B, max_steps);
   return 0;
 }
+
+// ---- debug variant: paging guard (ROUNDTABLE_DEBUG_CHECKS=1) ------------------------
+// Validates, on the device and inside the captured step, the paging metadata every later kernel
+// of the step dereferences — host asserts cannot see the slots / lengths the graph advances
+// itself. Violations OR a code into err[0]; the host reads it at its sync points:
+//   1 = ctx_len outside [1, max_blocks * BS]     2 = block-table entry outside [0, num_blocks)
+//   4 = write slot != block_tables[pos / BS] * BS + pos % BS    8 = ctx_len != position + 1
+namespace {
+__global__ void __launch_bounds__(256) paging_guard_kernel(const int* __restrict__ block_tables,
+                                                           const int* __restrict__ ctx_lens,
+                                                           const int64_t* __restrict__ positions,
+                                                           const int64_t* __restrict__ slots, int* __restrict__ err,
+                                                           int max_blocks, int num_blocks, int BS) {
+  const int b = blockIdx.x;
+  const int ctx = ctx_lens[b];
+  const int* bt = block_tables + (size_t)b * max_blocks;
+  int code = 0;
+  if (ctx < 1 || ctx > max_blocks * BS) code |= 1;
+  const int nt = min((max(ctx, 0) + BS - 1) / BS, max_blocks);
+  for (int t = threadIdx.x; t < nt; t += blockDim.x) {
+    const int blk = bt[t];
+    if (blk < 0 || blk >= num_blocks) code |= 2;
+  }
+  if (threadIdx.x == 0 && positions != nullptr) {
+    const int64_t pos = positions[b];
+    if (pos + 1 != ctx) code |= 8;
+    if (slots != nullptr && pos >= 0 && pos / BS < max_blocks) {
+      const int64_t want = (int64_t)bt[pos / BS] * BS + pos % BS;
+      if (slots[b] != want) code |= 4;
+    }
+  }
+  if (code) atomicOr(err, code);
+}
+}  // namespace
+
+int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
+                        int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (max_blocks <= 0 || BS <= 0) return -1;
+  hipLaunchKernelGGL(paging_guard_kernel, dim3(B), dim3(256), 0, stream, block_tables, ctx_lens, positions, slots, err,
+                     max_blocks, num_blocks, BS);
+  return 0;
+}

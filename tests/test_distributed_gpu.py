@@ -6,12 +6,14 @@ engines on the GPU, hipGraph decode (tp=1), the SPMD orchestration, C1 exchange,
 (eager decode) — runs exactly as on an 8-GPU node, so the scaling bench's code path is covered
 by a test that fits a 1-GPU box.
 """
+import gc
 import json
 import os
 import subprocess
 import sys
 
 import pytest
+import torch
 
 from test_distributed_cpu import ROOT, free_port
 
@@ -19,11 +21,14 @@ pytestmark = pytest.mark.gpu
 
 
 def _bench(extra=()):
+    # the ranks size their KV pools from free HBM: return what earlier in-process GPU tests cached
+    gc.collect()
+    torch.cuda.empty_cache()
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "16",
-           "--temperature", "0", "--kv-fraction", "0.1", *extra]
+           "--temperature", "0", "--kv-fraction", "0.1", "--max-kv-tokens", "65536", *extra]
     env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]

@@ -97,3 +97,21 @@ def test_serve_on_gpu_batches_requests():
         assert srv.engine.graphs   # decode ran through captured hipGraphs
     finally:
         srv.close()
+
+
+def test_debug_paging_guard_in_decode_graph():
+    """ROUNDTABLE_DEBUG_CHECKS: the captured step validates its own paging metadata on the device.
+    Normal decoding never trips it; corrupted graph state does, at the next host sync point."""
+    e = eng(use_graphs=True, debug_checks=True)
+    p = "Hallo tafel, wat is het plan voor vandaag?"
+    out = e.run_turns([Turn("K1", p, GREEDY), Turn("K2", p + " Anders.", GREEDY)])
+    assert all(len(t.ids) == GREEDY.max_new_tokens for t in out)
+    g = next(iter(e.graphs.values()))
+    assert int(g.guard_err.item()) == 0
+    # a length one past the position: every kernel still reads valid (allocated or scratch)
+    # blocks, so the replay is safe, but the guard must flag the inconsistency (code 8)
+    g.ctx_lens.add_(1)
+    g.graph.replay()
+    with pytest.raises(AssertionError, match="position"):
+        g.check_guard()
+    assert int(g.guard_err.item()) == 0           # cleared after reporting

@@ -196,3 +196,28 @@ def test_sample_top_p_nucleus():
         hits.add(int(tok))
     assert hits <= {0, 1} and len(hits) == 2
 
+
+
+def test_paging_guard_matches_reference():
+    g = torch.Generator().manual_seed(3)
+    for trial in range(40):
+        B, maxb, nb, bs = 3, 6, 16, 32
+        bt = torch.randint(0, nb, (B, maxb), generator=g, dtype=torch.int32)
+        ctx = torch.randint(1, maxb * bs + 1, (B,), generator=g, dtype=torch.int32)
+        pos = (ctx - 1).to(torch.int64)
+        slots = torch.tensor([int(bt[b, int(p) // bs]) * bs + int(p) % bs for b, p in enumerate(pos)])
+        kind = trial % 5
+        if kind == 1:
+            bt[trial % B, 0] = nb + trial            # out of the pool
+        elif kind == 2:
+            slots[trial % B] += 1                    # wrong write slot
+        elif kind == 3:
+            ctx[trial % B] = maxb * bs + 5           # beyond the table
+        elif kind == 4:
+            pos[trial % B] += 2                      # position / length mismatch
+        want = torch.zeros(1, dtype=torch.int32)
+        ref.paging_guard(bt, ctx, pos, slots, want, nb, bs)
+        got = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ops.paging_guard(bt.to(DEV), ctx.to(DEV), pos.to(DEV), slots.to(DEV), got, nb, bs)
+        assert int(got.item()) == int(want[0]), (trial, kind)
+        assert (kind == 0) == (int(want[0]) == 0)

@@ -75,3 +75,32 @@ def test_decode_prep_and_advance_reference():
     ops.decode_advance(out, ids, pos, ctx, step, torch.tensor([11, 12]))
     assert out[0].tolist() == [11, 12] and ids.tolist() == [11, 12]
     assert pos.tolist() == [34, 65] and ctx.tolist() == [35, 66] and step.item() == 1
+
+
+def _guard_case():
+    bt = torch.tensor([[3, 5, 0], [7, 1, 2]], dtype=torch.int32)
+    ctx = torch.tensor([40, 33], dtype=torch.int32)
+    pos = (ctx - 1).to(torch.int64)
+    slots = torch.tensor([5 * 32 + 7, 1 * 32 + 0], dtype=torch.int64)
+    return bt, ctx, pos, slots
+
+
+def test_paging_guard_reference_codes():
+    bt, ctx, pos, slots = _guard_case()
+    err = torch.zeros(1, dtype=torch.int32)
+    ref.paging_guard(bt, ctx, pos, slots, err, num_blocks=8, block_size=32)
+    assert int(err[0]) == 0
+    bad = bt.clone()
+    bad[1, 1] = 8                                     # outside an 8-block pool
+    ref.paging_guard(bad, ctx, pos, None, err, 8, 32)
+    assert int(err[0]) == 2
+    err.zero_()
+    ref.paging_guard(bt, ctx, pos, slots + 1, err, 8, 32)   # wrong write slot
+    assert int(err[0]) == 4
+    err.zero_()
+    ref.paging_guard(bt, ctx + 1, pos, None, err, 8, 32)    # ctx / position disagree
+    assert int(err[0]) == 8
+    err.zero_()
+    ref.paging_guard(bt, torch.tensor([97, 0], dtype=torch.int32), None, None, err, 8, 32)
+    assert int(err[0]) == 1
+    assert "KV pool" in ops.paging_guard_message(2) and ops.paging_guard_message(0) == "ok"

@@ -50,6 +50,7 @@ class DecodeGraph:
         self.offsets = torch.zeros(B, dtype=torch.int64, device=dev)
         self.hidden = torch.zeros(B, engine.model.cfg.hidden, dtype=engine.model.dtype, device=dev)
         self.ws = ops.DecodeWorkspace(B, engine.model.n_heads, engine.cfg.head_dim, max(1, splits), dev)
+        self.guard_err = torch.zeros(1, dtype=torch.int32, device=dev)   # debug paging guard (captured)
         self.graph = None
         self._capture()
 
@@ -66,6 +67,9 @@ class DecodeGraph:
             blk = self.block_tables.gather(1, (self.positions // bs).unsqueeze(1)).squeeze(1).long()
             slots = blk * bs + self.positions % bs
             offsets, hidden = self.positions + 1, None
+        if e.debug_checks:   # device-side bounds asserts on what this step's kernels dereference
+            ops.paging_guard(self.block_tables, self.ctx_lens, self.positions, slots, self.guard_err,
+                             e.kv.num_blocks, self.bs)
         meta = AttnMeta(kind="decode", slot_mapping=slots, block_tables=self.block_tables, ctx_lens=self.ctx_lens,
                         num_splits=self.splits, workspace=self.ws)
         if hidden is not None:
@@ -76,6 +80,13 @@ class DecodeGraph:
         # one epilogue launch: record ids, advance positions / lengths / step
         ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt)
 
+    def check_guard(self) -> None:
+        code = int(self.guard_err.item())
+        if code:
+            self.guard_err.zero_()
+            raise AssertionError(f"paging guard tripped in the decode graph (code {code}): "
+                                 f"{ops.paging_guard_message(code)}")
+
     def _reset_dummy(self):
         self.positions.zero_()
         self.ctx_lens.fill_(1)
@@ -84,6 +95,7 @@ class DecodeGraph:
 
     def _capture(self):
         dev = self.engine.device
+        self.guard_err.zero_()
         self._reset_dummy()
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -128,6 +140,8 @@ class DecodeGraph:
         for i in range(1, steps):
             self.graph.replay()
             if i % sync_every == 0:
+                if engine.debug_checks:
+                    self.check_guard()
                 if time.perf_counter() > deadline:
                     engine._sync()
                     raise EngineTimeout("engine", "turn exceeded timeout_per_turn_seconds")
@@ -137,6 +151,8 @@ class DecodeGraph:
                     if all(_finished(o, t.params, eos, engine.tokenizer) for o, t in zip(outs, turns)):
                         done_at = i + 1
                         break
+        if engine.debug_checks:
+            self.check_guard()
         n = done_at - 1
         got = self.out[:n, :B].t().tolist() if n > 0 else [[] for _ in range(B)]
         return [[f] + g for f, g in zip(first_host, got)]

@@ -224,6 +224,22 @@ def decode_prep(slots: torch.Tensor, offsets: torch.Tensor, res: torch.Tensor, i
     ref.decode_prep(slots, offsets, res, ids, positions, block_tables, embed, block_size)
 
 
+def paging_guard(block_tables: torch.Tensor, ctx_lens: torch.Tensor, positions: Optional[torch.Tensor],
+                 slots: Optional[torch.Tensor], err: torch.Tensor, num_blocks: int, block_size: int) -> None:
+    """Debug-mode device guard of the paging metadata (err[0] |= ref.PAGING_GUARD_CODES bits).
+
+    Capturable: placed inside the decode hipGraph it validates the slots / lengths the graph
+    advances on the device, which host-side asserts never see."""
+    if _use_native(ctx_lens):
+        native().paging_guard(block_tables, ctx_lens, positions, slots, err, int(num_blocks), int(block_size))
+        return
+    ref.paging_guard(block_tables, ctx_lens, positions, slots, err, num_blocks, block_size)
+
+
+def paging_guard_message(code: int) -> str:
+    return "; ".join(msg for bit, msg in ref.PAGING_GUARD_CODES.items() if code & bit) or "ok"
+
+
 def decode_advance(out: torch.Tensor, ids: torch.Tensor, positions: torch.Tensor, ctx_lens: torch.Tensor,
                    step: torch.Tensor, nxt: torch.Tensor) -> None:
     """Captured-step epilogue: record the sampled ids and advance positions / lengths / step."""

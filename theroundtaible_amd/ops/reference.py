@@ -288,3 +288,31 @@ def decode_advance(out, ids, positions, ctx_lens, step, nxt):
     positions.add_(1)
     ctx_lens.add_(1)
     step.add_(1)
+
+
+PAGING_GUARD_CODES = {1: "ctx_len outside [1, max_blocks*block_size]", 2: "block-table entry outside the KV pool",
+                      4: "K/V write slot does not match block_tables[pos // block_size]",
+                      8: "ctx_len != position + 1"}
+
+
+def paging_guard(block_tables, ctx_lens, positions, slots, err, num_blocks, block_size):
+    """Semantics of csrc/decode_step.hip::paging_guard (err[0] |= violation bits, in place)."""
+    code = 0
+    maxb = block_tables.shape[1]
+    for b in range(ctx_lens.numel()):
+        ctx = int(ctx_lens[b])
+        if ctx < 1 or ctx > maxb * block_size:
+            code |= 1
+        nt = min((max(ctx, 0) + block_size - 1) // block_size, maxb)
+        row = block_tables[b, :nt]
+        if nt and (int(row.min()) < 0 or int(row.max()) >= num_blocks):
+            code |= 2
+        if positions is not None:
+            pos = int(positions[b])
+            if pos + 1 != ctx:
+                code |= 8
+            if slots is not None and pos >= 0 and pos // block_size < maxb:
+                want = int(block_tables[b, pos // block_size]) * block_size + pos % block_size
+                if int(slots[b]) != want:
+                    code |= 4
+    err[0] = int(err[0]) | code
