@@ -65,6 +65,9 @@ def parse():
 
 def main() -> int:
     args = parse()
+    from theroundtaible_amd.utils.debug import apply_debug_env
+    if apply_debug_env():
+        print("bench: ROUNDTABLE_DEBUG=1 — kernels serialized, numbers are NOT performance data", file=sys.stderr)
     import torch
     from theroundtaible_amd.engine.engine import Engine, EngineConfig
     from theroundtaible_amd.engine.sampler import SamplingParams

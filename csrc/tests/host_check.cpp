@@ -1,0 +1,64 @@
+// Host-side argument validation of the HIP launchers, built with AddressSanitizer +
+// UndefinedBehaviorSanitizer on the HOST code only (GPU ASan / xnack+ is not
+// available on the MI355X pool). Every case below must be rejected BEFORE any HIP call, so
+// the binary runs on a machine without a GPU. Build + run: tests/test_native_host_sanitizers.py.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
+                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream);
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
+                          hipStream_t stream);
+int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                        const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
+                        int D, int max_blocks, float scale, int num_splits, hipStream_t stream);
+int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
+                        int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream);
+int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
+                          const int64_t* next, int B, int max_steps, hipStream_t stream);
+int prefill32_rows(int G);
+
+static int failures = 0;
+#define EXPECT(cond)                                                   \
+  do {                                                                 \
+    if (!(cond)) {                                                     \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                      \
+    }                                                                  \
+  } while (0)
+
+int main() {
+  // decode GEMM: M outside [1, 16], K not a multiple of 32, N not a multiple of 16, missing operands
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 0, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
+                            nullptr, nullptr) == -1);
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 17, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
+                            nullptr, nullptr) == -1);
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 48, 16, 1e-5f, 0, 0, nullptr, nullptr,
+                            nullptr, nullptr) == -1);
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 24, 64, 24, 1e-5f, 0, 0, nullptr, nullptr,
+                            nullptr, nullptr) == -1);
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 2, 0, nullptr, nullptr,
+                            nullptr, nullptr) == -5);   // NORM_ADD without its second operand
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 0, 3, nullptr, nullptr,
+                            nullptr, nullptr) == -3);   // ROPE epilogue without its parameters
+  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 16, 48, 0, 0, nullptr) == -1);
+  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 32, 64, 64, 128, nullptr) == -1);   // rope rows > N
+  // decode attention: group size, head dim, split range
+  EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 30, 8,
+                             128, 4, 0.1f, 4, nullptr) == -1);
+  EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 64, 2,
+                             128, 4, 0.1f, 4, nullptr) == -1);   // G = 32 > 16
+  EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 32, 8,
+                             128, 4, 0.1f, 65, nullptr) == -3);  // splits > MAXS
+  EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 32, 8,
+                             128, 4, 0.1f, 4, nullptr) == 0);    // empty batch: no launch
+  EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 2, 0, 16, 32, nullptr) == -1);
+  EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 0, 4, 16, 32, nullptr) == 0);
+  EXPECT(launch_decode_advance(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 8, nullptr) == 0);
+  // prefill tile geometry
+  EXPECT(prefill32_rows(4) == 64 && prefill32_rows(8) == 32 && prefill32_rows(1) == 256 && prefill32_rows(3) == 0);
+  std::printf("host_check: %d failure(s)\n", failures);
+  return failures ? 1 : 0;
+}

@@ -104,3 +104,12 @@ def test_paging_guard_reference_codes():
     ref.paging_guard(bt, torch.tensor([97, 0], dtype=torch.int32), None, None, err, 8, 32)
     assert int(err[0]) == 1
     assert "KV pool" in ops.paging_guard_message(2) and ops.paging_guard_message(0) == "ok"
+
+
+def test_debug_env_mode():
+    from theroundtaible_amd.utils.debug import apply_debug_env
+    env = {"ROUNDTABLE_DEBUG": "1", "HIP_LAUNCH_BLOCKING": "0"}
+    assert apply_debug_env(env)
+    assert env["AMD_SERIALIZE_KERNEL"] == "3" and env["ROUNDTABLE_DEBUG_CHECKS"] == "1"
+    assert env["HIP_LAUNCH_BLOCKING"] == "0"          # explicit settings win
+    assert not apply_debug_env({})

@@ -593,6 +593,8 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv: Optional[List[str]] = None) -> int:
+    from .utils.debug import apply_debug_env
+    apply_debug_env()          # ROUNDTABLE_DEBUG=1: serialized kernels + paging guards (before any HIP call)
     args = build_parser().parse_args(argv)
     ui = UI(quiet=args.quiet)
     try:
