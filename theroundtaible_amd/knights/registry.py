@@ -3,6 +3,8 @@
 Reference semantics kept: the backend map is keyed by *adapter id* (two knights on
 one adapter share a backend); an unavailable primary with an available fallback is
 stored under the primary's key. Unknown adapter ids are reported and skipped.
+Seats configured with ``backend: "external"`` (or reference-shaped ``local-llm`` entries
+with an ``endpoint``) use the reference's transports (:mod:`.external`).
 """
 from __future__ import annotations
 
@@ -15,6 +17,7 @@ from ..types import RoundtableConfig
 from ..utils.ui import NULL_UI, UI
 from .base import KnightBackend
 from .engine_backend import ADAPTER_DISPLAY_NAMES, EngineBackend, EnginePool
+from .external import create_external, wants_external
 from .fake import FakeBackend
 
 KNOWN_PREFIXES = ("claude-", "gemini-", "openai-", "local-llm", "engine", "fake")
@@ -68,6 +71,9 @@ class BackendFactory:
         name = display_name(adapter_id, self.config)
         if st.get("backend") == "fake" or adapter_id.startswith("fake"):
             return FakeBackend(name=name, adapter_id=adapter_id)
+        ac = self.config.adapter_config.get(adapter_id) or {}
+        if isinstance(ac, dict) and wants_external(adapter_id, ac):
+            return create_external(adapter_id, ac, name)
         ecfg = EngineConfig(model=st["model"], weights=str(st.get("weights", "random:0")),
                             dtype=str(st.get("dtype", "bf16")), device=self._device_for(adapter_id, st),
                             block_size=int(st.get("kv_block_size", 32)),
