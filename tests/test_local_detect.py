@@ -60,3 +60,56 @@ def test_init_seats_local_checkpoints(tmp_path, monkeypatch):
     assert "local-llm-meta-llama-3-8b" in adapters
     eng = cfg["adapter_config"]["local-llm-meta-llama-3-8b"]["engine"]
     assert eng["model"] == "llama3-8b" and eng["weights"].endswith("Meta-Llama-3-8B")
+
+
+def test_detect_local_servers_and_cli_fallback():
+    from theroundtaible_amd.knights.external import HttpResponse
+    from theroundtaible_amd.utils.local_detect import detect_local_servers, fetch_models_from_ollama_cli
+
+    def http(method, url, body, headers, timeout):
+        assert timeout == 3.0 and url.endswith("/v1/models")
+        if ":1234" in url:
+            return HttpResponse(200, json.dumps({"data": [{"id": "qwen2.5-coder-14b"}, {"id": "nomic-embed-text"}]}))
+        raise OSError("connection refused")
+
+    listing = "NAME              ID      SIZE\nllama3.1:8b   abc  4.7 GB\nmistral:latest def 4 GB\n"
+    found = detect_local_servers(http=http, ollama_cli=lambda: listing)
+    assert [(m.model_id, m.source) for m in found] == [("qwen2.5-coder-14b", "LM Studio"), ("llama3.1:8b", "Ollama"),
+                                                     ("mistral", "Ollama")]
+    assert found[0].adapter_config() == {"endpoint": "http://localhost:1234", "model": "qwen2.5-coder-14b",
+                                         "name": "Qwen2.5 Coder 14B", "source": "LM Studio"}
+    assert found[1].adapter_slug() == "llama3-1-8b" and found[2].name == "Mistral"
+    assert fetch_models_from_ollama_cli(run=lambda: (_ for _ in ()).throw(OSError("no ollama"))) == []
+
+
+def test_init_seats_running_server(tmp_path, monkeypatch):
+    from theroundtaible_amd import cli
+    from theroundtaible_amd.utils import local_detect
+    from theroundtaible_amd.knights.registry import BackendFactory
+    from theroundtaible_amd.knights.external import LocalLlmHttpBackend
+    from theroundtaible_amd.config import load_config
+    sm = local_detect.ServerModel("Llama3.1 8B", "llama3.1:8b", "http://127.0.0.1:11434", "Ollama")
+    monkeypatch.setattr(local_detect, "detect_local_servers", lambda: [sm])
+    monkeypatch.setattr(cli, "detect_tools", lambda: {"claude": True, "gemini": False, "codex": False})
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("HF_HOME", str(tmp_path / "nohf"))
+    assert cli.main(["--quiet", "init", "--yes", "--knights", "2", "--servers", "--external-clis"]) == 0
+    raw = json.load(open(tmp_path / ".roundtable" / "config.json"))
+    assert raw["adapter_config"]["local-llm-llama3-1-8b"]["endpoint"] == "http://127.0.0.1:11434"
+    assert "engine" not in raw["adapter_config"]["local-llm-llama3-1-8b"]
+    assert raw["adapter_config"]["claude-cli"]["backend"] == "external"
+    assert "backend" not in raw["adapter_config"]["gemini-cli"]
+    cfg = load_config(str(tmp_path))
+    b = BackendFactory(cfg).create("local-llm-llama3-1-8b")
+    assert isinstance(b, LocalLlmHttpBackend) and b.source == "Ollama"
+
+
+def test_update_check():
+    from theroundtaible_amd.knights.external import HttpResponse
+    from theroundtaible_amd.utils.update_check import check_for_update, is_newer
+    assert is_newer("0.2.0", "0.1.9") and not is_newer("0.1.0", "0.1.0") and is_newer("1.0", "0.9.9")
+    assert check_for_update(url=None) is None or os.environ.get("ROUNDTABLE_UPDATE_URL")
+    ok = lambda *a: HttpResponse(200, json.dumps({"info": {"version": "9.0.0"}}))
+    assert check_for_update("http://pypi/x", "0.1.0", http=ok) == "9.0.0"
+    assert check_for_update("http://pypi/x", "9.0.0", http=ok) is None
+    assert check_for_update("http://pypi/x", "0.1.0", http=lambda *a: (_ for _ in ()).throw(OSError())) is None

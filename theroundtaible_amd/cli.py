@@ -70,6 +70,59 @@ def gpu_inventory() -> List[dict]:
     return [{"index": i} for i in range(n)]
 
 
+CLI_TOOLS = {"claude-cli": "claude", "gemini-cli": "gemini", "openai-cli": "codex"}
+API_FALLBACKS = (("claude-api", "ANTHROPIC_API_KEY", "Anthropic"), ("gemini-api", "GEMINI_API_KEY", "Gemini"),
+                 ("openai-api", "OPENAI_API_KEY", "OpenAI"))
+
+
+def detect_tools(commands=("claude", "gemini", "codex")) -> dict:
+    """``<cmd> --version`` for every vendor CLI, in parallel (init.ts:96-113)."""
+    import subprocess
+    from concurrent.futures import ThreadPoolExecutor
+
+    def probe(cmd):
+        try:
+            return subprocess.run([cmd, "--version"], capture_output=True, timeout=10).returncode == 0
+        except (OSError, subprocess.SubprocessError):
+            return False
+    with ThreadPoolExecutor(max_workers=len(commands)) as ex:
+        return dict(zip(commands, ex.map(probe, commands)))
+
+
+def ask_secret(ui: UI, question: str) -> str:
+    """Masked input (init.ts:49-91 raw-mode reader); empty when stdin is not a terminal."""
+    import getpass
+    if not sys.stdin.isatty():
+        return ""
+    try:
+        return getpass.getpass(question + " ").strip()
+    except (EOFError, KeyboardInterrupt):
+        return ""
+
+
+def _ask_fallback_key(ui: UI, knights, external) -> None:
+    from .store.keys import save_key
+    for i, (aid, var, label) in enumerate(API_FALLBACKS, start=1):
+        ui.print(f"    {i}. {label} ({aid})")
+    raw = ask(ui, f"  Which provider? [1-{len(API_FALLBACKS)}]", "")
+    if not raw.isdigit() or not 1 <= int(raw) <= len(API_FALLBACKS):
+        return
+    aid, var, label = API_FALLBACKS[int(raw) - 1]
+    key = ask_secret(ui, f"  {label} API key:")
+    if not key:
+        ui.dim("  No key entered; no fallback added.")
+        return
+    save_key(var, key)
+    names = ", ".join(k["name"] for k in knights)
+    who = ask(ui, f"  Fallback for which knight? ({names})", knights[0]["name"])
+    for k in knights:
+        if k["name"].lower() == who.lower():
+            k["fallback"] = aid
+            external[aid] = {"backend": "external"}
+            ui.ok(f"  {k['name']} falls back to {aid}; key saved to ~/.theroundtaible/keys.json")
+            return
+
+
 def cmd_init(args, ui: UI) -> int:
     root = os.getcwd()
     rt = os.path.join(root, ".roundtable")
@@ -107,6 +160,27 @@ def cmd_init(args, ui: UI) -> int:
             adapter = f"local-llm-{m.adapter_slug()}"
             knights.append({"name": m.name, "adapter": adapter, "capabilities": ["code", "logic"]})
             local_engine[adapter] = {"model": m.preset, "weights": m.path, "model_overrides": m.overrides}
+    # running LM Studio / Ollama servers (init.ts:255,361-373): external local-llm seats over HTTP
+    external = {}
+    if args.servers:
+        from .utils.local_detect import detect_local_servers
+        for sm in detect_local_servers():
+            adapter = f"local-llm-{sm.adapter_slug()}"
+            if any(k["adapter"] == adapter for k in knights):
+                continue
+            knights.append({"name": sm.name, "adapter": adapter, "capabilities": ["code", "logic"]})
+            external[adapter] = sm.adapter_config()
+            ui.ok(f"  Found {sm.name} on {sm.source} ({sm.endpoint})")
+    # installed vendor CLIs (init.ts:96-113): seat them on their own transport instead of the engine
+    if args.external_clis:
+        tools = detect_tools()
+        for k in knights:
+            if k["adapter"] in CLI_TOOLS and tools.get(CLI_TOOLS[k["adapter"]]):
+                external[k["adapter"]] = {"backend": "external"}
+                ui.ok(f"  {k['name']}: {CLI_TOOLS[k['adapter']]} CLI found, seated on its own transport")
+    # API-key fallback (init.ts:306-323): masked input, stored in ~/.theroundtaible/keys.json
+    if not args.yes and knights and confirm(ui, "  Add an API key as fallback for a knight?", False):
+        _ask_fallback_key(ui, knights, external)
     if not knights:
         ui.error("\n  A roundtable with no knights is just a table.")
         return 0
@@ -122,8 +196,12 @@ def cmd_init(args, ui: UI) -> int:
                           engine={"default_model": args.model, "weights": args.weights, "dtype": "bf16",
                                   "max_new_tokens": args.max_new_tokens},
                           adapter_engine=adapter_engine)
+    for aid, ac in external.items():
+        cfg["adapter_config"].setdefault(aid, {}).update(ac)
+        if aid in adapter_engine and "endpoint" in ac:
+            cfg["adapter_config"][aid].pop("engine", None)
     for k in knights:
-        if k["adapter"].startswith("local-llm"):
+        if k["adapter"].startswith("local-llm") and k["adapter"] not in external:
             model = adapter_engine[k["adapter"]]["model"]
             cfg["adapter_config"][k["adapter"]].update({"endpoint": "engine://local", "model": model,
                                                         "name": k["name"]})
@@ -534,6 +612,10 @@ def build_parser() -> argparse.ArgumentParser:
     i.add_argument("--max-new-tokens", type=int, default=512)
     i.add_argument("--local-models", action="store_true",
                    help="seat every detected local checkpoint (ROUNDTABLE_MODELS_DIR, ./models, HF cache)")
+    i.add_argument("--servers", action="store_true",
+                   help="seat models of running LM Studio (:1234) / Ollama (:11434) servers over HTTP")
+    i.add_argument("--external-clis", action="store_true",
+                   help="seat installed claude/gemini/codex CLIs on their own transport instead of the engine")
     i.set_defaults(fn=cmd_init)
     d = sub.add_parser("discuss", help="Start a discussion between knights")
     d.add_argument("topic")
@@ -592,13 +674,23 @@ def build_parser() -> argparse.ArgumentParser:
     return p
 
 
+def _update_notice(ui: UI) -> None:
+    """index.ts:185: print a notice when a newer version exists (opt-in, utils/update_check.py)."""
+    from .utils.update_check import check_for_update
+    latest = check_for_update()
+    if latest:
+        ui.warn(f"\n  Update available: {__version__} -> {latest}")
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     from .utils.debug import apply_debug_env
     apply_debug_env()          # ROUNDTABLE_DEBUG=1: serialized kernels + paging guards (before any HIP call)
     args = build_parser().parse_args(argv)
     ui = UI(quiet=args.quiet)
     try:
-        return int(args.fn(args, ui) or 0)
+        rc = int(args.fn(args, ui) or 0)
+        _update_notice(ui)
+        return rc
     except RoundtableError as e:
         print(format_error(e), file=sys.stderr)
         return int(e.exit_code)

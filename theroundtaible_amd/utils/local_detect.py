@@ -146,3 +146,74 @@ def detect_local_models(search_dirs: Optional[List[str]] = None, project_root: O
             seen_ids.add(mid)
             out.append(LocalModel(prettify_model_name(mid), mid, d, preset, diff))
     return out
+
+
+# ---- running model servers (reference behaviour, `src/utils/local-detect.ts:43-134`) ------------
+LOCAL_SERVERS = (("LM Studio", "http://localhost:1234"), ("Ollama", "http://localhost:11434"))
+
+
+@dataclass
+class ServerModel:
+    name: str                 # prettified display name
+    model_id: str             # id the server reports
+    endpoint: str
+    source: str               # "LM Studio" | "Ollama"
+
+    def adapter_slug(self) -> str:
+        return re.sub(r"[^a-z0-9]+", "-", self.model_id.split("/")[-1].lower()).strip("-")
+
+    def adapter_config(self) -> Dict[str, Any]:
+        """``adapter_config`` entry for an external local-llm seat (knights/external.py)."""
+        return {"endpoint": self.endpoint, "model": self.model_id, "name": self.name, "source": self.source}
+
+
+def fetch_models_from_endpoint(endpoint: str, source: str, timeout_s: float = 3.0, http=None) -> List[ServerModel]:
+    """``GET <endpoint>/v1/models`` (local-detect.ts:43-71); chat models only, [] on any failure."""
+    from ..knights.external import http_request
+    try:
+        r = (http or http_request)("GET", f"{endpoint}/v1/models", None, {}, timeout_s)
+        if not r.ok:
+            return []
+        data = r.json().get("data") or []
+    except Exception:  # noqa: BLE001 - server absent / not JSON
+        return []
+    out = []
+    for m in data:
+        mid = m.get("id") if isinstance(m, dict) else None
+        if isinstance(mid, str) and mid and not is_non_chat_model(mid):
+            out.append(ServerModel(prettify_model_name(mid), mid, endpoint, source))
+    return out
+
+
+def fetch_models_from_ollama_cli(endpoint: str = "http://localhost:11434", run=None) -> List[ServerModel]:
+    """Parse ``ollama list`` (local-detect.ts:77-97): first column after the header, ``:latest`` stripped."""
+    import subprocess
+    try:
+        if run is None:
+            proc = subprocess.run(["ollama", "list"], capture_output=True, text=True, timeout=5)
+            if proc.returncode != 0:
+                return []
+            text = proc.stdout
+        else:
+            text = run()
+    except (OSError, subprocess.SubprocessError):
+        return []
+    out = []
+    for line in text.splitlines()[1:]:
+        cols = line.split()
+        if cols:
+            mid = re.sub(r":latest$", "", cols[0])
+            out.append(ServerModel(prettify_model_name(mid), mid, endpoint, "Ollama"))
+    return out
+
+
+def detect_local_servers(servers=LOCAL_SERVERS, http=None, ollama_cli=None) -> List[ServerModel]:
+    """Probe LM Studio and Ollama concurrently; fall back to ``ollama list`` (local-detect.ts:103-134)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=max(1, len(servers))) as ex:
+        results = list(ex.map(lambda s: fetch_models_from_endpoint(s[1], s[0], http=http), servers))
+    found: List[ServerModel] = [m for r in results for m in r]
+    if not any(m.source == "Ollama" for m in found) and any(src == "Ollama" for src, _ in servers):
+        ep = next(e for src, e in servers if src == "Ollama")
+        found.extend(fetch_models_from_ollama_cli(ep, run=ollama_cli))
+    return found
