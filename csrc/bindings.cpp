@@ -45,6 +45,12 @@ int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, 
                         int I, int Hq, int Hkv, int head_dim, int BS, int max_blocks, int num_splits, float eps,
                         float scale, hipStream_t stream);
 int decode_layer_grid();
+int oneshot_create(int world, int rank, int cap_elems, char* handles);
+int oneshot_open(int id, const char* all_handles);
+int oneshot_capacity(int id);
+int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream);
+int oneshot_error(int id);
+void oneshot_destroy(int id);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
                           hipStream_t stream);
@@ -298,6 +304,26 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
+// K9 one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot_ar.hip).
+py::tuple py_oneshot_create(int64_t world, int64_t rank, int64_t cap_elems) {
+  char h[128] = {0};
+  const int id = oneshot_create((int)world, (int)rank, (int)cap_elems, h);
+  TORCH_CHECK(id >= 0, "oneshot_create failed (rc=", id, ")");
+  return py::make_tuple(id, py::bytes(h, 128));
+}
+void py_oneshot_open(int64_t id, py::bytes all_handles, int64_t world) {
+  const std::string hs = all_handles;
+  TORCH_CHECK((int64_t)hs.size() == world * 128, "oneshot_open: need world x 128 handle bytes");
+  const int rc = oneshot_open((int)id, hs.data());
+  TORCH_CHECK(rc == 0, "oneshot_open: hipIpcOpenMemHandle failed (rc=", rc, ")");
+}
+void py_oneshot_allreduce(int64_t id, torch::Tensor x) {
+  check_bf16(x, "oneshot_allreduce input");
+  TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= oneshot_capacity((int)id), "oneshot_allreduce: size");
+  const int rc = oneshot_allreduce((int)id, x.data_ptr(), (int)x.numel(), cur_stream());
+  TORCH_CHECK(rc == 0, "oneshot_allreduce failed (rc=", rc, ")");
+}
+
 // Decode-step bookkeeping (csrc/decode_step.hip).
 void decode_prep(torch::Tensor slots, torch::Tensor offsets, torch::Tensor res, torch::Tensor ids,
                  torch::Tensor positions, torch::Tensor block_tables, torch::Tensor embed, int64_t block_size) {
@@ -443,6 +469,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("part_ml"), py::arg("split_counters"), py::arg("sync"), py::arg("err"), py::arg("Hq"),
         py::arg("Hkv"), py::arg("num_splits"), py::arg("eps"), py::arg("scale"), py::arg("stamps") = py::none());
   m.def("decode_layer_grid", &decode_layer_grid);
+  m.def("oneshot_create", &py_oneshot_create, py::arg("world"), py::arg("rank"), py::arg("cap_elems"));
+  m.def("oneshot_open", &py_oneshot_open, py::arg("id"), py::arg("all_handles"), py::arg("world"));
+  m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
+  m.def("oneshot_capacity", [](int64_t id) { return oneshot_capacity((int)id); });
+  m.def("oneshot_error", [](int64_t id) { return oneshot_error((int)id); });
+  m.def("oneshot_destroy", [](int64_t id) { oneshot_destroy((int)id); });
   m.def("decode_advance", &decode_advance);
   m.def("paging_guard", &paging_guard, py::arg("block_tables"), py::arg("ctx_lens"), py::arg("positions"),
         py::arg("slots"), py::arg("err"), py::arg("num_blocks"), py::arg("block_size"));

@@ -1,0 +1,228 @@
+// K9: one-shot all-reduce for tensor-parallel decode over xGMI.
+//
+// A decode all-reduce is tiny ([B, hidden] bf16: 16 KB at B = 1 on Llama-3-70B) and there are
+// two per layer (160 per token at TP = 4). RCCL's ring spends world-1 dependent steps per call;
+// on MI355X every GPU has a dedicated xGMI link to each peer, so one step suffices: every rank
+// PUSHES its slice straight into every peer's receive buffer (posted remote writes, one link per
+// peer, all links at once), raises one flag per (peer, workgroup), waits for the peers' flags in
+// its own memory, and sums the world copies locally in rank order (bit-identical results on
+// every rank, like RCCL).
+//
+// Memory: receive buffers and flags are hipDeviceMallocUncached (fine-grained, never cached in a
+// GPU's L2/MALL, so a remote write is what the next local load sees) and exported to the peers
+// with hipIpcGetMemHandle (dmabuf) / hipIpcOpenMemHandle. Two slots alternate by call parity:
+// before rank r writes slot s again (call e), it has seen every peer's flag of call e-1, which
+// each peer raised only after its call e-2 — the last reader of slot s — had finished.
+// The call counter (`epoch`) lives on the device and is advanced by the last workgroup out, so
+// the launch is hipGraph-capturable and replays with no host involvement.
+// Every flag wait is bounded: on expiry *err is set and the kernel proceeds (never a hang).
+#include "common.h"
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace {
+constexpr int MAXW = 8;    // ranks per all-reduce group (one xGMI hop to every peer)
+constexpr int MAXB = 64;   // workgroups per call (flags per (slot, source rank))
+constexpr long long FLAG_POLL_LIMIT = 1ll << 26;
+
+struct Peers {
+  uint16_t* data[MAXW];    // rank p's receive buffer: [2 slots][world][cap] bf16
+  uint32_t* flags[MAXW];   // rank p's flags: [2 slots][world][MAXB]
+};
+
+__global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ inout, int n, int rank, int world,
+                                                         int cap, Peers P, uint32_t* epoch_ctr, uint32_t* done_ctr,
+                                                         int* err) {
+  const uint32_t epoch = __hip_atomic_load(epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int slot = (int)(epoch & 1u);
+  const int nb = gridDim.x, blk = blockIdx.x;
+  const int nvec = n >> 3;                              // 16-byte vectors
+  const int per = (nvec + nb - 1) / nb;
+  const int v0 = blk * per, v1 = min(nvec, v0 + per);
+  using rt::float4_;
+  using vec = uint4;
+
+  // 1. push this workgroup's slice into every rank's receive buffer (own rank included)
+  for (int v = v0 + (int)threadIdx.x; v < v1; v += blockDim.x) {
+    const vec x = reinterpret_cast<const vec*>(inout)[v];
+    for (int p = 0; p < world; ++p)
+      reinterpret_cast<vec*>(P.data[p] + ((size_t)slot * world + rank) * cap)[v] = x;
+  }
+  // 2. release: every thread's remote stores complete before any flag is raised
+  __threadfence_system();
+  __syncthreads();
+  if ((int)threadIdx.x < world)
+    __hip_atomic_store(P.flags[threadIdx.x] + ((size_t)slot * world + rank) * MAXB + blk, epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  // 3. wait for every rank's copy of this slice in our own memory
+  if ((int)threadIdx.x < world) {
+    const uint32_t* f = P.flags[rank] + ((size_t)slot * world + threadIdx.x) * MAXB + blk;
+    long long it = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > FLAG_POLL_LIMIT) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();
+  // 4. sum the world copies in rank order (fp32), write the result in place
+  const uint16_t* mine = P.data[rank] + (size_t)slot * world * cap;
+  for (int v = v0 + (int)threadIdx.x; v < v1; v += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {
+      const vec x = reinterpret_cast<const vec*>(mine + (size_t)r * cap)[v];
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += rt::bf2f((uint16_t)(w[j] & 0xffffu));
+        acc[2 * j + 1] += rt::bf2f((uint16_t)(w[j] >> 16));
+      }
+    }
+    vec o;
+    o.x = rt::pack2(acc[0], acc[1]);
+    o.y = rt::pack2(acc[2], acc[3]);
+    o.z = rt::pack2(acc[4], acc[5]);
+    o.w = rt::pack2(acc[6], acc[7]);
+    reinterpret_cast<vec*>(inout)[v] = o;
+  }
+  // 5. the last workgroup out advances the call counter (every workgroup has read it)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (uint32_t)nb - 1u) {
+      __hip_atomic_store(done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(epoch_ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+struct Comm {
+  int world = 0, rank = 0, cap = 0;       // cap: max elements per call
+  int device = 0;
+  uint16_t* data = nullptr;               // own receive buffer
+  uint32_t* flags = nullptr;              // own flags
+  uint32_t* ctr = nullptr;                // [epoch, done] (plain device memory, local only)
+  int* err = nullptr;
+  Peers peers{};
+  std::vector<void*> opened;              // IPC mappings to close
+};
+std::mutex g_mu;
+std::vector<Comm*> g_comms;
+
+Comm* get(int id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return (id >= 0 && id < (int)g_comms.size()) ? g_comms[id] : nullptr;
+}
+size_t data_bytes(const Comm& c) { return (size_t)2 * c.world * c.cap * sizeof(uint16_t); }
+size_t flag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXB * sizeof(uint32_t); }
+}  // namespace
+
+// Allocates this rank's IPC buffers. Returns a comm id (>= 0) or a negative error; the two
+// 64-byte IPC handles (data, flags) are written to `handles` (128 bytes).
+int oneshot_create(int world, int rank, int cap_elems, char* handles) {
+  if (world < 2 || world > MAXW || rank < 0 || rank >= world || cap_elems < 8 || cap_elems % 8) return -1;
+  Comm* c = new Comm;
+  c->world = world;
+  c->rank = rank;
+  c->cap = cap_elems;
+  if (hipGetDevice(&c->device) != hipSuccess) { delete c; return -2; }
+  if (hipExtMallocWithFlags((void**)&c->data, data_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags((void**)&c->flags, flag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
+      hipMalloc((void**)&c->ctr, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc((void**)&c->err, sizeof(int)) != hipSuccess) {
+    delete c;
+    return -3;
+  }
+  if (hipMemset(c->flags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->ctr, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(c->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    delete c;
+    return -4;
+  }
+  hipIpcMemHandle_t hd, hf;
+  if (hipIpcGetMemHandle(&hd, c->data) != hipSuccess || hipIpcGetMemHandle(&hf, c->flags) != hipSuccess) {
+    delete c;
+    return -5;
+  }
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+  memcpy(handles, &hd, 64);
+  memcpy(handles + 64, &hf, 64);
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms.push_back(c);
+  return (int)g_comms.size() - 1;
+}
+
+// Maps every peer's buffers: `all_handles` = world x 128 bytes, in rank order.
+int oneshot_open(int id, const char* all_handles) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  for (int p = 0; p < c->world; ++p) {
+    if (p == c->rank) {
+      c->peers.data[p] = c->data;
+      c->peers.flags[p] = c->flags;
+      continue;
+    }
+    hipIpcMemHandle_t hd, hf;
+    memcpy(&hd, all_handles + (size_t)p * 128, 64);
+    memcpy(&hf, all_handles + (size_t)p * 128 + 64, 64);
+    void* pd = nullptr;
+    void* pf = nullptr;
+    if (hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -2;
+    c->opened.push_back(pd);
+    if (hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -3;
+    c->opened.push_back(pf);
+    c->peers.data[p] = (uint16_t*)pd;
+    c->peers.flags[p] = (uint32_t*)pf;
+  }
+  return 0;
+}
+
+int oneshot_capacity(int id) {
+  Comm* c = get(id);
+  return c ? c->cap : -1;
+}
+
+// In-place sum over the group of `n` bf16 elements at `inout` (device pointer, 16-B aligned).
+int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  if (n <= 0 || n % 8 || n > c->cap || ((uintptr_t)inout & 15)) return -2;
+  for (int p = 0; p < c->world; ++p)
+    if (c->peers.data[p] == nullptr) return -3;   // oneshot_open not called
+  int nb = n / 2048;                                // ~4 KB of slice per workgroup
+  nb = nb < 1 ? 1 : (nb > MAXB ? MAXB : nb);
+  hipLaunchKernelGGL(oneshot_ar_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
+                     c->cap, c->peers, c->ctr, c->ctr + 1, c->err);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// Poll-expiry flag (1 = a peer's flag never arrived: results of that call are wrong).
+int oneshot_error(int id) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  int e = 0;
+  if (hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  return e;
+}
+
+void oneshot_destroy(int id) {
+  Comm* c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (id < 0 || id >= (int)g_comms.size()) return;
+    c = g_comms[id];
+    g_comms[id] = nullptr;
+  }
+  if (c == nullptr) return;
+  (void)hipDeviceSynchronize();
+  for (void* p : c->opened) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(c->data);
+  (void)hipFree(c->flags);
+  (void)hipFree(c->ctr);
+  (void)hipFree(c->err);
+  delete c;
+}

@@ -1,0 +1,22 @@
+"""K9 one-shot all-reduce (csrc/oneshot_ar.hip) across processes sharing the GPU via IPC."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from test_distributed_cpu import ROOT, free_port
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_oneshot_allreduce_ranks_on_one_gpu(world):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "tools", "oneshot_check.py")]
+    env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == world and all(o["checks"] == 6 + 15 for o in lines)

@@ -112,6 +112,8 @@ class Engine:
                     self.model.decode_weights()
                 else:
                     self.model.use_fused = False
+        if self.on_gpu and self.tp.size > 1:
+            self.tp.setup_oneshot()      # K9: collective over the TP group; RCCL stays the fallback
         self.load_s = time.perf_counter() - t0
         self.kv = self._alloc_kv()
         self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}

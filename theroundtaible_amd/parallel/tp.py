@@ -7,7 +7,9 @@ GPU; ``torch.distributed`` backend ``nccl`` is RCCL on ROCm, ``gloo`` on CPU tes
 
 Decode all-reduces are tiny (``[B, hidden]`` bf16 = 16 KB at B=1, 70B): they are
 latency-bound on xGMI, so they are issued on the compute stream inside the captured
-hipGraph (RCCL supports graph capture) rather than bucketed.
+hipGraph rather than bucketed, and go through the one-shot IPC all-reduce (K9,
+``parallel/oneshot.py``: one push step over the dedicated xGMI links instead of a ring)
+when every rank could map its peers; larger messages (prefill) use RCCL.
 """
 from __future__ import annotations
 
@@ -23,6 +25,7 @@ class TPInfo:
     size: int = 1
     rank: int = 0
     group: Optional[object] = None   # torch.distributed ProcessGroup
+    oneshot: Optional[object] = None  # parallel.oneshot.OneShotAllReduce (decode-size messages)
 
     @property
     def enabled(self) -> bool:
@@ -41,8 +44,16 @@ class TPInfo:
         # tensors through host memory explicitly; RCCL works on device memory directly
         return x.is_cuda and self.backend() == "gloo"
 
+    def setup_oneshot(self) -> None:
+        """Collective over the group (every rank calls it at the same point)."""
+        from .oneshot import enabled_by_env, try_create
+        if self.size > 1 and self.oneshot is None and enabled_by_env():
+            self.oneshot = try_create(self.group, self.rank, self.size)
+
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
+            if self.oneshot is not None and self.oneshot.accepts(x):
+                return self.oneshot(x)
             if self._host_staged(x):
                 h = x.cpu()
                 dist.all_reduce(h, group=self.group)

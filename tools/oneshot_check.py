@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""K9 one-shot all-reduce check + microbenchmark, one process per rank (torchrun).
+
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/oneshot_check.py [--bench]
+
+Ranks may share a GPU (the 1-GPU rehearsal: IPC mappings of the same device) or own one each
+(xGMI). Checks eager calls over several sizes, then a captured hipGraph replayed repeatedly,
+against the fp32 sum of every rank's (regenerated) input; ``--bench`` also times one-shot vs
+the process group's all_reduce for decode-size messages. Exit code 0 = all checks passed.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def data(rank: int, n: int, tag: int, dev) -> torch.Tensor:
+    g = torch.Generator().manual_seed(1000 * tag + 17 * rank + n)
+    return torch.randn(n, generator=g).to(torch.bfloat16).to(dev)
+
+
+def expect(world: int, n: int, tag: int) -> torch.Tensor:
+    acc = torch.zeros(n)
+    for r in range(world):
+        acc += data(r, n, tag, "cpu").float()
+    return acc.to(torch.bfloat16).float()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bench", action="store_true")
+    a = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    ndev = torch.cuda.device_count()
+    dev = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', rank)) % ndev}")
+    torch.cuda.set_device(dev)
+    backend = "nccl" if ndev >= world and os.environ.get("ROUNDTABLE_DIST_BACKEND") != "gloo" else "gloo"
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    from theroundtaible_amd.parallel.oneshot import try_create
+    ar = try_create(dist.group.WORLD, rank, world)
+    assert ar is not None, "one-shot all-reduce could not be set up"
+    out = {"rank": rank, "world": world, "backend": backend, "checks": 0}
+    for tag, n in enumerate([8, 1024, 4096, 8192, 3 * 8192, 16 * 8192]):
+        x = data(rank, n, tag, dev)
+        ar(x)
+        torch.cuda.synchronize()
+        err = (x.float().cpu() - expect(world, n, tag)).abs().max().item()
+        assert err <= 0.0625, f"n={n}: max err {err}"
+        out["checks"] += 1
+    # hipGraph: three calls captured, replayed; inputs refreshed in place before each replay
+    n = 8192
+    bufs = [torch.empty(n, dtype=torch.bfloat16, device=dev) for _ in range(3)]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for b in bufs:
+                ar(b)
+    for rep in range(5):
+        for i, b in enumerate(bufs):
+            b.copy_(data(rank, n, 100 + 10 * rep + i, dev))
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        for i, b in enumerate(bufs):
+            err = (b.float().cpu() - expect(world, n, 100 + 10 * rep + i)).abs().max().item()
+            assert err <= 0.0625, f"graph replay {rep} buf {i}: max err {err}"
+            out["checks"] += 1
+    assert ar.error() == 0, "a flag poll expired"
+    if a.bench:
+        for n in (8192, 16 * 8192):
+            x = data(rank, n, 7, dev)
+            gg = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(gg, stream=s):
+                    for _ in range(20):
+                        ar(x)
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                gg.replay()
+            torch.cuda.synchronize()
+            out[f"oneshot_us_n{n}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+            if backend == "nccl":
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(200):
+                    dist.all_reduce(x)
+                torch.cuda.synchronize()
+                out[f"rccl_eager_us_n{n}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+    ar.close()
+    print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
