@@ -21,14 +21,15 @@ def free_port():
     return p
 
 
-def _tp_worker(rank, world, port, model, q):
+def _tp_worker(rank, world, port, model, q, overrides=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
         from theroundtaible_amd.parallel.tp import TPInfo
         tp = TPInfo(size=world, rank=rank, group=dist.group.WORLD)
-        e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9"), tp)
+        e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9",
+                                model_overrides=dict(overrides or {})), tp)
         ids = e.encode_prompt("tensor parallel knight over xGMI")
         logits = e.prefill([(e.kv.seq("k"), ids)])
         out = e.run_turns([Turn("k2", "tensor parallel", SamplingParams(temperature=0, max_new_tokens=6,
@@ -39,10 +40,13 @@ def _tp_worker(rank, world, port, model, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", ["tiny-llama", "tiny-gpt2"])
-def test_tp2_matches_tp1(model):
+@pytest.mark.parametrize("model,tp,overrides", [("tiny-llama", 2, None), ("tiny-gpt2", 2, None),
+                                                 ("tiny-llama", 4, {"n_kv_heads": 4})])
+def test_tp_matches_tp1(model, tp, overrides):
+    """TP=2/4 forward + greedy decode equal TP=1."""
     from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
-    e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9"))
+    e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9",
+                            model_overrides=dict(overrides or {})))
     ids = e.encode_prompt("tensor parallel knight over xGMI")
     ref_logits = e.prefill([(e.kv.seq("k"), ids)])
     ref_ids = e.run_turns([Turn("k2", "tensor parallel", SamplingParams(temperature=0, max_new_tokens=6,
@@ -50,7 +54,7 @@ def test_tp2_matches_tp1(model):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, model, q)) for r in range(2)]
+    procs = [ctx.Process(target=_tp_worker, args=(r, tp, port, model, q, overrides)) for r in range(tp)]
     for p in procs:
         p.start()
     logits, got_ids = q.get(timeout=180)
@@ -108,6 +112,15 @@ def test_spmd_bench_two_ranks():
     assert out["n_gpus"] == 2 and out["config"]["knights"] == 6 and out["config"]["tables"] == 2
     assert out["detail"]["decode_tokens"] == 6 * 8 * 2
     assert out["value"] > 0 and out["scaling"] == "weak"
+
+
+@pytest.mark.parametrize("nproc", [4, 8])
+def test_spmd_bench_scaling_world_sizes(nproc):
+    """The driver's scaling run (N = 4, 8 ranks) on the gloo/CPU path: 3 knights per rank,
+    tables striped over ranks, every response crossing ranks in the C1 exchange."""
+    out = _bench(nproc)
+    assert out["n_gpus"] == nproc and out["config"]["tables"] == nproc and out["config"]["knights"] == 3 * nproc
+    assert out["detail"]["decode_tokens"] == 3 * nproc * 8 * 2 and out["detail"]["failed_turns"] == 0
 
 
 def test_cli_discuss_under_torchrun_with_tp_knight(tmp_path):
