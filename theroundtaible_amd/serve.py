@@ -91,7 +91,8 @@ class Scheduler:
         self.chunk = max(1, int(chunk))
         self.q: "queue.Queue[_Request]" = queue.Queue()
         self.stats = {"requests": 0, "batches": 0, "prompt_tokens": 0, "completion_tokens": 0,
-                      "reused_tokens": 0, "busy_s": 0.0, "errors": 0, "admitted_midflight": 0}
+                      "reused_tokens": 0, "busy_s": 0.0, "errors": 0, "admitted_midflight": 0,
+                      "decode_steps": 0, "decode_rows": 0, "prefill_s": 0.0}
         self._stop = threading.Event()
         self._lock = threading.Lock()
         self.thread = threading.Thread(target=self._loop, name="roundtable-serve", daemon=True)
@@ -166,14 +167,16 @@ class Scheduler:
             t_busy = time.perf_counter()
             if new:
                 turns = [Turn(r.key, r.prompt, r.params, timeout_s=self.timeout_s) for r in new]
+                t_pf = time.perf_counter()
                 try:
                     started = self.engine.start_turns(turns)
                 except BaseException as e:  # noqa: BLE001 - reported per request
                     for r in new:
                         self._complete(_Active(r, None, None, [], {}, time.perf_counter()), e)
                     started = []
-                if active and started:
-                    with self._lock:
+                with self._lock:
+                    self.stats["prefill_s"] += time.perf_counter() - t_pf
+                    if active and started:
                         self.stats["admitted_midflight"] += len(started)
                 for r, t, (sq, first, m) in zip(new, turns, started):
                     a = _Active(r, sq, t, [first], dict(m, batch=0), time.perf_counter())
@@ -197,6 +200,8 @@ class Scheduler:
                 a.metrics["batch"] = max(a.metrics.get("batch", 0), len(active))
             with self._lock:
                 self.stats["batches"] += 1
+                self.stats["decode_steps"] += max(1, steps)
+                self.stats["decode_rows"] += max(1, steps) * len(active)
                 self.stats["busy_s"] += time.perf_counter() - t_busy
             still = []
             for a in active:
@@ -348,7 +353,8 @@ class RoundtableServer:
             raise ValueError("max_tokens must be >= 1")
         return SamplingParams(temperature=num("temperature", 0.7, float), top_p=num("top_p", 1.0, float),
                               top_k=num("top_k", 0, int), seed=num("seed", 0, int),
-                              max_new_tokens=min(max_tokens, 8192), ignore_eos=False, stop_on_consensus=False)
+                              max_new_tokens=min(max_tokens, 8192), ignore_eos=bool(body.get("ignore_eos", False)),
+                              stop_on_consensus=False)
 
     def generate(self, prompt: str, body: Dict[str, Any], session: Optional[str]) -> Tuple[Any, _Request]:
         params = self.sampling(body)
@@ -388,6 +394,8 @@ class RoundtableServer:
             f"roundtable_completion_tokens_total {st['completion_tokens']}",
             "# TYPE roundtable_reused_kv_tokens_total counter", f"roundtable_reused_kv_tokens_total {st['reused_tokens']}",
             "# TYPE roundtable_engine_busy_seconds_total counter", f"roundtable_engine_busy_seconds_total {st['busy_s']:.6f}",
+            "# TYPE roundtable_decode_steps_total counter", f"roundtable_decode_steps_total {st['decode_steps']}",
+            "# TYPE roundtable_decode_rows_total counter", f"roundtable_decode_rows_total {st['decode_rows']}",
             "# TYPE roundtable_decode_tokens_total counter", f"roundtable_decode_tokens_total {e['decode_tokens']}",
             "# TYPE roundtable_kv_capacity_tokens gauge", f"roundtable_kv_capacity_tokens {self.engine.kv_capacity_tokens}",
             "# TYPE roundtable_engine_healthy gauge", f"roundtable_engine_healthy {int(bool(self.engine.healthy))}",

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Load test of ``roundtable serve`` (OpenAI dialect) on one GPU: aggregate completion tokens/s
+and request latency under N concurrent clients (continuous batching, hipGraph decode).
+
+    python tools/serve_bench.py [--model llama3-8b] [--clients 16] [--requests 32] [--prompt-words 400]
+                                [--max-tokens 256] [--max-batch 16]
+
+Synthetic prompts, random-init weights, ``ignore_eos`` so every request generates exactly
+``--max-tokens``. Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+import threading
+import time
+import urllib.request
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+WORDS = ("ridder tafel consensus voorstel kernel geheugen rooster latency bandbreedte wachtrij graaf "
+         "decoder prefill cache blok splitsing rangorde beslissing koning ronde").split()
+
+
+def post(url, body, timeout=900):
+    req = urllib.request.Request(url, data=json.dumps(body).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    with urllib.request.urlopen(req, timeout=timeout) as r:
+        return json.loads(r.read().decode())
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--clients", type=int, default=16)
+    ap.add_argument("--requests", type=int, default=32)
+    ap.add_argument("--prompt-words", type=int, default=400)
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--max-batch", type=int, default=16)
+    ap.add_argument("--num-blocks", type=int, default=None)
+    a = ap.parse_args()
+    from theroundtaible_amd.serve import build_server
+    t_load = time.perf_counter()
+    srv = build_server(a.model, weights="random:0", device=a.device, port=0, max_batch=a.max_batch,
+                       max_tokens=a.max_tokens, num_blocks=a.num_blocks).start()
+    load_s = time.perf_counter() - t_load
+    rng = random.Random(0)
+    prompts = [" ".join(rng.choice(WORDS) for _ in range(a.prompt_words)) for _ in range(a.requests)]
+    url = srv.url + "/v1/chat/completions"
+
+    def one(i):
+        body = {"model": a.model, "messages": [{"role": "user", "content": prompts[i]}],
+                "max_tokens": a.max_tokens, "ignore_eos": True, "temperature": 0.7, "top_p": 0.95}
+        t0 = time.perf_counter()
+        d = post(url, body)
+        return time.perf_counter() - t0, d["usage"]
+
+    # warm-up: compiles/captures the decode graphs of the batch buckets used below
+    post(url, {"messages": [{"role": "user", "content": "warm"}], "max_tokens": 8, "ignore_eos": True})
+    lat, usage = [], []
+    lock = threading.Lock()
+    nxt = iter(range(a.requests))
+
+    def client():
+        while True:
+            with lock:
+                i = next(nxt, None)
+            if i is None:
+                return
+            dt, u = one(i)
+            with lock:
+                lat.append(dt)
+                usage.append(u)
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=client) for _ in range(a.clients)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    comp = sum(u["completion_tokens"] for u in usage)
+    prompt = sum(u["prompt_tokens"] for u in usage)
+    lat.sort()
+    out = {"metric": "serve aggregate completion tokens/s", "value": round(comp / wall, 1), "unit": "tokens/s",
+           "model": a.model, "dtype": "bf16", "data": "synthetic prompts, random-init weights",
+           "clients": a.clients, "requests": a.requests, "max_batch": a.max_batch, "max_tokens": a.max_tokens,
+           "prompt_tokens_total": prompt, "completion_tokens_total": comp, "wall_s": round(wall, 2),
+           "latency_s_p50": round(statistics.median(lat), 2), "latency_s_p99": round(lat[int(0.99 * (len(lat) - 1))], 2),
+           "engine_load_s": round(load_s, 2), "scheduler": dict(srv.sched.stats) if hasattr(srv, "sched") else None}
+    srv.close()
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
