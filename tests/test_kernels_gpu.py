@@ -108,6 +108,32 @@ def test_paged_decode(hq, hkv, d, splits):
     assert int(ws.counters.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("splits", [1, 2, 5])
+def test_paged_decode_long_context(splits):
+    """Contexts of 20K / 33K keys: at splits=1 a wave walks > 64 tiles, exercising the per-lane
+    block-id refill; block tables are a random permutation over the whole pool."""
+    hq, hkv, d = 32, 8, 128
+    lens = [20000, 33000, 40]
+    B = len(lens)
+    nb = sum((l + 31) // 32 for l in lens) + 2
+    kc, vc = make_cache(nb, hkv, d, seed=21)
+    perm = torch.randperm(nb, generator=torch.Generator().manual_seed(5)).tolist()
+    maxb = max((l + 31) // 32 for l in lens)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    i = 0
+    for b, l in enumerate(lens):
+        n = (l + 31) // 32
+        bt[b, :n] = torch.tensor(perm[i:i + n], dtype=torch.int32)
+        i += n
+    q = bf(B, hq, d, seed=22)
+    cl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(d)
+    ws = ops.DecodeWorkspace(B, hq, d, splits, DEV)
+    out = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws)
+    exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, cl, scale)
+    close(out, exp.to(DEV), 0.02, 0.02)
+
+
 def test_paged_decode_spike():
     """Force the online-softmax rescale path: a key that dominates late in the sequence."""
     hq, hkv, d, L = 32, 8, 128, 700
@@ -146,6 +172,32 @@ def test_prefill_varlen(hq, hkv, d):
     cu_t = torch.tensor(cu, dtype=torch.int32)
     st = torch.tensor([sp for sp, _ in specs], dtype=torch.int32)
     q = bf(cu[-1], hq, d, seed=22)
+    scale = 1 / math.sqrt(d)
+    out = ops.prefill_attention(q, kc, vc, bt.to(DEV), cu_t.to(DEV), st.to(DEV), scale)
+    exp = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt, cu_t, st, scale)
+    close(out, exp.to(DEV), 0.02, 0.02)
+
+
+def test_prefill_long_prefix():
+    """Delta chunks over long paged prefixes (30K / 12K keys) mixed with a fresh sequence."""
+    hq, hkv, d = 32, 8, 128
+    specs = [(30000, 200), (0, 300), (12345, 129)]
+    S = len(specs)
+    nb_each = [(sp + n + 31) // 32 for sp, n in specs]
+    nb = sum(nb_each) + 2
+    kc, vc = make_cache(nb, hkv, d, seed=41)
+    perm = torch.randperm(nb, generator=torch.Generator().manual_seed(6)).tolist()
+    bt = torch.zeros(S, max(nb_each), dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(nb_each):
+        bt[s, :n] = torch.tensor(perm[i:i + n], dtype=torch.int32)
+        i += n
+    cu = [0]
+    for _, n in specs:
+        cu.append(cu[-1] + n)
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    st = torch.tensor([sp for sp, _ in specs], dtype=torch.int32)
+    q = bf(cu[-1], hq, d, seed=42)
     scale = 1 / math.sqrt(d)
     out = ops.prefill_attention(q, kc, vc, bt.to(DEV), cu_t.to(DEV), st.to(DEV), scale)
     exp = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt, cu_t, st, scale)
