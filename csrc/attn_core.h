@@ -29,7 +29,7 @@ using rt::short8;
 
 constexpr int BS = 32;
 constexpr int NW = 8;
-constexpr int MAXS = 64;  // max splits (combine staging)
+constexpr int MAXS = 64;  // max splits per (sequence, kv head)
 constexpr float LOG2E = 1.4426950408889634f;
 
 template <int D>
@@ -87,8 +87,6 @@ struct AttnSmem {
   float s_m[NW][16];
   float s_l[NW][16];
   float s_o[NW][GM][D + 4];
-  float s_wt[GM][MAXS];
-  float s_lt[GM][MAXS];
   int s_last;
 };
 
@@ -121,8 +119,6 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   auto& s_m = S.s_m;
   auto& s_l = S.s_l;
   auto& s_o = S.s_o;
-  auto& s_wt = S.s_wt;
-  auto& s_lt = S.s_lt;
   int& s_last = S.s_last;
 
   const int b = bh / Hkv, hk = bh - (bh / Hkv) * Hkv;
@@ -304,43 +300,40 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   __syncthreads();
   if (!s_last) return false;
 
-  // latency-bound: (m, l) of all (head, split) pairs by distinct threads, weights via LDS,
-  // then 8 independent 16-B partial loads in flight per thread
-  for (int i = threadIdx.x; i < G * num_splits; i += blockDim.x) {
-    const float4_ ml = rt::sc1_load4(pml_rsrc, i * 16);
-    const int qi = i / num_splits, s2 = i - qi * num_splits;
-    s_wt[qi][s2] = ml[1] > 0.f ? ml[0] : -INFINITY;
-    s_lt[qi][s2] = ml[1];
-  }
-  __syncthreads();
-  if (threadIdx.x < G) {
-    const int qi = threadIdx.x;
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, s_wt[qi][s2]);
-    float L = 0.f;
-    for (int s2 = 0; s2 < num_splits; ++s2) {
-      const float f = (M == -INFINITY || s_wt[qi][s2] == -INFINITY) ? 0.f : exp2f(s_wt[qi][s2] - M);
-      s_wt[qi][s2] = f;
-      L += f * s_lt[qi][s2];
-    }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    for (int s2 = 0; s2 < num_splits; ++s2) s_wt[qi][s2] *= inv;
-  }
-  __syncthreads();
+  // latency-bound: each output thread issues the (m, l) AND partial-O loads of up to 16 splits
+  // at once (one round trip for <= 16 splits, no LDS weight pass) and merges them online
   for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
     const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
     float4_ O = {0.f, 0.f, 0.f, 0.f};
-    for (int s0 = 0; s0 < num_splits; s0 += 8) {
-      float4_ v[8];
+    float Mr = -INFINITY, Lr = 0.f;
+    for (int s0 = 0; s0 < num_splits; s0 += 16) {
+      float4_ v[16], ml[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = (s0 + j < num_splits) ? rt::sc1_load4(po_rsrc, ((qi * num_splits + s0 + j) * D + d0) * 4)
-                                     : float4_{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 16; ++j) {
+        const bool ok = s0 + j < num_splits;
+        ml[j] = ok ? rt::sc1_load4(pml_rsrc, (qi * num_splits + s0 + j) * 16) : float4_{-INFINITY, 0.f, 0.f, 0.f};
+        v[j] = ok ? rt::sc1_load4(po_rsrc, ((qi * num_splits + s0 + j) * D + d0) * 4) : float4_{0.f, 0.f, 0.f, 0.f};
+      }
+      float Mc = Mr;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (s0 + j < num_splits) O += s_wt[qi][s0 + j] * v[j];
+      for (int j = 0; j < 16; ++j)
+        if (ml[j][1] > 0.f) Mc = fmaxf(Mc, ml[j][0]);
+      if (Mc == -INFINITY) continue;                 // every split of this chunk was empty
+      const float a = Mr == -INFINITY ? 0.f : exp2f(Mr - Mc);
+      O *= a;
+      Lr *= a;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (ml[j][1] > 0.f) {
+          const float f = exp2f(ml[j][0] - Mc);
+          O += f * v[j];
+          Lr += f * ml[j][1];
+        }
+      }
+      Mr = Mc;
     }
-    store_bf16x4(out + (bh_q0 + qi) * D + d0, O[0], O[1], O[2], O[3], SC1);
+    const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
+    store_bf16x4(out + (bh_q0 + qi) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
   }
   __syncthreads();
   return true;
