@@ -52,7 +52,7 @@ int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream);
 int oneshot_error(int id);
 void oneshot_destroy(int id);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
-int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
 
 
@@ -439,7 +439,7 @@ void prefetch(torch::Tensor t, int64_t nwg, torch::Tensor sink) {
 }
 
 void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tensor> gamma, int64_t rope_heads,
-                    int64_t head_dim) {
+                    int64_t head_dim, bool swiglu) {
   check_bf16(Ws, "Ws");
   check_bf16(W, "W");
   TORCH_CHECK(W.dim() == 2 && Ws.sizes() == W.sizes(), "shuffle_weight shapes");
@@ -451,7 +451,7 @@ void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tens
     gp = gamma->data_ptr();
   }
   const int rc = launch_shuffle_weight(Ws.data_ptr(), W.data_ptr(), gp, (int)W.size(0), (int)W.size(1),
-                                       (int)(rope_heads * head_dim), (int)head_dim, cur_stream());
+                                       (int)(rope_heads * head_dim), (int)head_dim, swiglu ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "shuffle_weight: unsupported configuration (rc=", rc, ")");
 }
 }  // namespace
@@ -461,7 +461,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("epi"), py::arg("res") = py::none(),
         py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none());
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
-        py::arg("rope_heads") = 0, py::arg("head_dim") = 0);
+        py::arg("rope_heads") = 0, py::arg("head_dim") = 0, py::arg("swiglu") = false);
   m.def("decode_prep", &decode_prep);
   m.def("decode_layer", &decode_layer, py::arg("res"), py::arg("q"), py::arg("a"), py::arg("g"), py::arg("wqkv"),
         py::arg("wo"), py::arg("wgu"), py::arg("wd"), py::arg("positions"), py::arg("cos_sin"), py::arg("k_cache"),

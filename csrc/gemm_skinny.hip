@@ -35,16 +35,22 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(GemmArgs p) {
 // Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j] (optionally W * gamma[k] folded in)
 // If rope_rows > 0, output row r < rope_rows takes source row h*D + (p>>1) + (p&1)*D/2
 // (r = h*D + p): the pair-interleaved q/k order the ROPE epilogue expects.
+// swiglu: N = 2I rows [gate; up], stored k-step-paired: Ws[t][s][h][l][j] = W[h*I + 16t + (l&15)][...]
 __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restrict__ W,
-                               const uint16_t* __restrict__ gamma, int N, int K, int rope_rows, int D) {
+                               const uint16_t* __restrict__ gamma, int N, int K, int rope_rows, int D, int swiglu) {
   const int nsteps = K / 32;
   const int64_t total = (int64_t)(N / 16) * nsteps * 64;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int l = (int)(i & 63);
-    const int64_t ts = i >> 6;
+    int64_t ts = i >> 6;
+    int h = 0;
+    if (swiglu) {
+      h = (int)(ts & 1);
+      ts >>= 1;
+    }
     const int s = (int)(ts % nsteps);
     const int64_t t = ts / nsteps;
-    int row = (int)(16 * t + (l & 15));
+    int row = (int)(16 * t + (l & 15)) + h * (N / 2);
     if (row < rope_rows) {
       const int h = row / D, p = row - h * D;
       row = h * D + (p >> 1) + (p & 1) * (D >> 1);
@@ -113,14 +119,15 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   return 0;
 }
 
-int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream) {
   if (K % 32 || N % 16 || rope_rows > N || (rope_rows > 0 && (D <= 0 || D % 2 || rope_rows % D))) return -1;
+  if (swiglu && (N % 32 || rope_rows > 0)) return -1;
   const int64_t total = (int64_t)N * K / 8;
   int64_t grid = (total + 255) / 256;
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(shuffle_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (short8*)Ws, (const uint16_t*)W,
-                     (const uint16_t*)gamma, N, K, rope_rows, D);
+                     (const uint16_t*)gamma, N, K, rope_rows, D, swiglu);
   return 0;
 }
 

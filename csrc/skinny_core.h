@@ -3,6 +3,8 @@
 //
 // Weight layout ("fragment-shuffled", built once at load time by `shuffle_weight`):
 //     Ws[N/16][K/32][64 lanes][8]   with  Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j]
+// and for SwiGLU (W = [gate(I); up(I)], `swiglu=True`) the two halves paired per k-step:
+//     Ws[I/16][K/32][2][64][8]      with  Ws[t][s][h][l][j] = W[h*I + 16t + (l&15)][32s + 8(l>>4) + j]
 // i.e. exactly the order in which the 64 lanes of a wave hold the B operand of
 // v_mfma_f32_16x16x32_bf16: every wave load instruction reads 1 KiB of contiguous HBM and a
 // workgroup streams its 16-row panel front to back.
@@ -115,12 +117,15 @@ struct Stage {
 template <int PRO, int EPI, int NW, int U>
 RT_DEVICE void issue_w(Stage<PRO, EPI, U>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2, int s0,
                        int nsteps, int lane) {
+  // SwiGLU weights are stored k-step-paired ([tile][step][gate|up][64 lanes][8]): one wave streams
+  // 2 KiB contiguous per step instead of two 1-KiB streams 117 MB apart (`wt2` unused)
+  constexpr size_t kStride = (EPI == EPI_SWIGLU) ? 128 : 64;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int s = s0 + NW * u;
     if (s < nsteps) {
-      st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * 64 + lane);
-      if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt2 + (size_t)s * 64 + lane);
+      st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + lane);
+      if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + 64 + lane);
     }
   }
 }
@@ -176,8 +181,8 @@ template <int PRO, int EPI, int NW, int U>
 RT_DEVICE void gemm_prefetch(const GemmArgs& p, int tile, Stage<PRO, EPI, U>& st0) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nsteps = p.K / 32;
-  const short8* wt = p.Ws + (size_t)tile * nsteps * 64;
-  const short8* wt2 = (EPI == EPI_SWIGLU) ? p.Ws + (size_t)(p.N / 16 + tile) * nsteps * 64 : nullptr;
+  const short8* wt = p.Ws + (size_t)tile * nsteps * ((EPI == EPI_SWIGLU) ? 128 : 64);
+  const short8* wt2 = nullptr;
   issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane);
 }
 
@@ -198,8 +203,8 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   uint16_t* xo_r =
       (PRO == PRO_NORM_ADD && publish_xo && row_ok && p.xo != nullptr) ? p.xo + (size_t)r * K + 8 * g : nullptr;
   const XSrc xo_s = make_xsrc<SC1>(PRO == PRO_NORM_ADD && p.xo != nullptr ? p.xo : p.x, lane_elem);
-  const short8* wt = p.Ws + (size_t)tile * nsteps * 64;
-  const short8* wt2 = (EPI == EPI_SWIGLU) ? p.Ws + (size_t)(N / 16 + tile) * nsteps * 64 : nullptr;
+  const short8* wt = p.Ws + (size_t)tile * nsteps * ((EPI == EPI_SWIGLU) ? 128 : 64);
+  const short8* wt2 = nullptr;
 
   float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
   float ssq = 0.f;

@@ -40,7 +40,7 @@ def test_skinny_gemm_modes(M, N, K):
     close(res, res_ref.to(DEV), 0.06, 0.02)
     # SwiGLU epilogue over [gate; up]
     W2 = bf(2 * N, K, scale=0.05, seed=55)
-    got = ops.skinny_gemm(x, ops.shuffle_weight(W2, gam), ops.PRO_NORM, ops.EPI_SWIGLU)
+    got = ops.skinny_gemm(x, ops.shuffle_weight(W2, gam, swiglu=True), ops.PRO_NORM, ops.EPI_SWIGLU)
     exp = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W2.cpu(), gam.cpu()), 1, 2)
     close(got, exp.to(DEV), 0.05, 0.03)
 
@@ -132,7 +132,7 @@ def test_norm_add_prologue():
     assert torch.equal(xo, xo_r.to(DEV))
     # SwiGLU epilogue with the same prologue
     W2 = bf(2 * N, K, scale=0.05, seed=75)
-    got = ops.skinny_gemm(x, ops.shuffle_weight(W2, gam), ops.PRO_NORM_ADD, ops.EPI_SWIGLU, x2=x2)
+    got = ops.skinny_gemm(x, ops.shuffle_weight(W2, gam, swiglu=True), ops.PRO_NORM_ADD, ops.EPI_SWIGLU, x2=x2)
     exp = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W2.cpu(), gam.cpu()), 2, 2, x2=x2.cpu())
     close(got, exp.to(DEV), 0.05, 0.03)
 

@@ -93,7 +93,7 @@ class LlamaModel:
                                                    rope_heads=self.n_heads + self.n_kv_heads,
                                                    head_dim=self.head_dim),
                         "wo": ops.shuffle_weight(lw["wo"]),
-                        "w_gate_up": ops.shuffle_weight(lw["w_gate_up"], lw["ffn_norm"]),
+                        "w_gate_up": ops.shuffle_weight(lw["w_gate_up"], lw["ffn_norm"], swiglu=True),
                         "w_down": ops.shuffle_weight(lw["w_down"]),
                     })
                 self._dec = {"layers": layers, "lm_head": ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])}

@@ -173,14 +173,15 @@ EPI_STORE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
 
 
 def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None, rope_heads: int = 0,
-                   head_dim: int = 0) -> torch.Tensor:
+                   head_dim: int = 0, swiglu: bool = False) -> torch.Tensor:
     """Decode-weight copy in the MFMA fragment order of csrc/gemm_skinny.hip, with an RMSNorm
     weight ``gamma`` (over K) optionally folded in and, for a qkv weight used with
-    :func:`skinny_gemm_rope`, the first ``rope_heads`` heads' rows pair-interleaved.
-    On CPU: the row-major ``W * gamma`` (rows permuted the same way)."""
+    :func:`skinny_gemm_rope`, the first ``rope_heads`` heads' rows pair-interleaved. ``swiglu``:
+    W = [gate; up] for the SWIGLU epilogue, stored k-step-paired (one contiguous stream per wave).
+    On CPU: the row-major ``W * gamma`` (rows permuted the same way; ``swiglu`` changes nothing)."""
     if _use_native(W):
         Ws = torch.empty_like(W)
-        native().shuffle_weight(Ws, W.contiguous(), gamma, int(rope_heads), int(head_dim))
+        native().shuffle_weight(Ws, W.contiguous(), gamma, int(rope_heads), int(head_dim), bool(swiglu))
         return Ws
     return ref.fold_gamma(W, gamma, rope_heads, head_dim)
 

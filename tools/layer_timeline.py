@@ -39,7 +39,7 @@ def main():
     gam = torch.ones(H, dtype=torch.bfloat16, device=DEV)
     lw = {"wqkv": ops.shuffle_weight(bf((hq + 2 * hkv) * D, H, scale=0.02), gam, rope_heads=hq + hkv, head_dim=D),
           "wo": ops.shuffle_weight(bf(H, hq * D, scale=0.02)),
-          "w_gate_up": ops.shuffle_weight(bf(2 * I, H, scale=0.02), gam),
+          "w_gate_up": ops.shuffle_weight(bf(2 * I, H, scale=0.02), gam, swiglu=True),
           "w_down": ops.shuffle_weight(bf(H, I, scale=0.02))}
     nblk = (ctx + 32) // 32 + 1
     kc, vc = bf(B * nblk, hkv, 32, D), bf(B * nblk, hkv, D, 32)

@@ -83,7 +83,7 @@ def bench_gemm(M):
     for name, N, K in shapes:
         nbytes = N * K * 2
         copies = max(2, math.ceil(2**30 / nbytes))
-        Ws = [ops.shuffle_weight(bf(N, K, scale=0.02)) for _ in range(copies)]
+        Ws = [ops.shuffle_weight(bf(N, K, scale=0.02), swiglu=name.startswith("gate_up")) for _ in range(copies)]
         # (the launcher reads RT_SKINNY_CFG once: compare variants from separate processes)
         if name.startswith("qkv"):
             fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d)
