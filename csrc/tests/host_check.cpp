@@ -9,7 +9,7 @@
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
                        int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream);
-int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D,
+int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
@@ -43,8 +43,9 @@ int main() {
                             nullptr, nullptr) == -5);   // NORM_ADD without its second operand
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 0, 3, nullptr, nullptr,
                             nullptr, nullptr) == -3);   // ROPE epilogue without its parameters
-  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 16, 48, 0, 0, nullptr) == -1);
-  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 32, 64, 64, 128, nullptr) == -1);   // rope rows > N
+  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 16, 48, 0, 0, 0, nullptr) == -1);
+  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 32, 64, 64, 128, 0, nullptr) == -1);   // rope rows > N
+  EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 48, 64, 0, 0, 1, nullptr) == -1);      // SwiGLU halves of 24 rows
   // decode attention: group size, head dim, split range
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 30, 8,
                              128, 4, 0.1f, 4, nullptr) == -1);

@@ -22,9 +22,23 @@ def test_allowed(cmd):
     ("cat < a", "forbidden pattern: input redirect (<)"), ("rm x", "forbidden command: rm"),
     ("echo hi", "command not whitelisted: echo"), ("ls | ", "empty pipe segment"),
     ("ls | python3 -c 1", "forbidden command: python3"),
+    # deliberate fixes over the reference: other bash command separators
+    ("ls\nrm -rf x", "forbidden pattern: newline (command separator)"),
+    ("ls\r\nrm x", "forbidden pattern: newline (command separator)"),
+    ("ls & rm x", "forbidden pattern: & (background / separator)"),
+    ("cat a &", "forbidden pattern: & (background / separator)"),
 ])
 def test_denied(cmd, why):
     assert validate_command(cmd) == why
+
+
+def test_apply_paths_stay_inside_project(tmp_path):
+    from theroundtaible_amd.apply.apply import inside_project
+    (tmp_path / "src").mkdir()
+    os.symlink("/etc", tmp_path / "escape")
+    assert inside_project(str(tmp_path), "src/a.py") and inside_project(str(tmp_path), "new/dir/b.py")
+    for bad in ("../x.py", "src/../../x.py", "/etc/passwd", "~/x", "escape/passwd", "", "."):
+        assert not inside_project(str(tmp_path), bad), bad
 
 
 def test_execute(tmp_path, monkeypatch):

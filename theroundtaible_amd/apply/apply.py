@@ -67,6 +67,17 @@ def sha256(text: str) -> str:
     return hashlib.sha256(text.encode("utf-8")).hexdigest()
 
 
+def inside_project(root: str, rel: str) -> bool:
+    """A knight-proposed path stays inside the project: relative, no '..' escape, no symlink
+    escape (checked on the resolved path). Applies even when no scope was recorded, and even
+    with --override-scope (which widens the scope, never the project)."""
+    if not rel or os.path.isabs(rel) or rel.startswith("~"):
+        return False
+    base = os.path.realpath(root)
+    full = os.path.realpath(os.path.join(base, rel))
+    return full != base and full.startswith(base + os.sep)
+
+
 def scope_sets(allowed: Optional[List[str]]) -> Tuple[Optional[set], set]:
     if allowed is None:
         return None, set()
@@ -191,6 +202,10 @@ def apply_command(args, ui: UI) -> int:
     plan: List[Tuple[str, Optional[str], str]] = []
     skipped: List[str] = []
     for fe in edits:
+        if not inside_project(root, fe.path):
+            ui.error(f"  ✗ {fe.path} is outside the project (absolute or '..' path) — never written")
+            skipped.append(fe.path)
+            continue
         if fe.path in blocked and override_reason is None:
             skipped.append(fe.path)
             continue

@@ -40,7 +40,9 @@ from .kv_cache import KVCacheOOM, PagedKVCache, SeqState
 from .sampler import SamplingParams
 from .tokenizer import EngineTokenizer, get_tokenizer
 
-BATCH_BUCKETS = (1, 2, 4, 8, 16, 32)
+# decode-graph batch buckets: exact sizes for the common knight counts (3-knight tables, 6 = two
+# tables) so no padded row takes split-KV workgroups from the real ones (B=3: 240 vs 192 live)
+BATCH_BUCKETS = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
 
 
 @dataclass

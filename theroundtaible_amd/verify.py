@@ -37,13 +37,21 @@ MAX_OUTPUT = 5000
 
 
 def validate_command(command: str) -> Optional[str]:
-    """None if allowed, else the rejection reason."""
+    """None if allowed, else the rejection reason.
+
+    Deliberate fix over the reference (`src/utils/verify.ts:55-98`): a newline / carriage return
+    or a lone ``&`` also separates commands under ``bash -c``, so both are rejected too (the
+    reference passes ``"ls\\nrm -rf x"`` and ``"ls & rm x"``)."""
     cmd = command.strip()
     if not cmd:
         return "empty command"
     for pat, src in FORBIDDEN_PATTERNS:
         if pat.search(cmd):
             return f"forbidden pattern: {src}"
+    if "\n" in cmd or "\r" in cmd:
+        return "forbidden pattern: newline (command separator)"
+    if re.search(r"(?<![&>])&(?!&|1)", cmd.replace("2>&1", "")):
+        return "forbidden pattern: & (background / separator)"
     rest = re.sub(r"2>\s*/dev/null", "", cmd).replace("2>&1", "")
     if ">>" in rest:
         return "forbidden pattern: append redirect (>>)"
