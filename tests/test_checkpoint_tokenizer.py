@@ -1,0 +1,81 @@
+"""Checkpoint tokenizers: a weights directory that ships ``tokenizer.json`` (+ chat template and
+end ids) is tokenized with its own vocabulary, every turn wrapped as one user message, and
+generation stops at the checkpoint's end-of-turn ids (engine/tokenizer.py::HFTokenizer)."""
+import json
+
+import pytest
+import torch
+
+transformers = pytest.importorskip("transformers")
+tokenizers = pytest.importorskip("tokenizers")
+
+from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn  # noqa: E402
+from theroundtaible_amd.engine.engine import cut_at_stop  # noqa: E402
+from theroundtaible_amd.engine.tokenizer import HFTokenizer  # noqa: E402
+
+SPECIAL = ["<|begin_of_text|>", "<|end_of_text|>", "<|start_header_id|>", "<|end_header_id|>", "<|eot_id|>"]
+LLAMA3_TEMPLATE = (
+    "{% for message in messages %}{% set content = '<|start_header_id|>' + message['role'] + "
+    "'<|end_header_id|>\\n\\n' + message['content'] | trim + '<|eot_id|>' %}{% if loop.index0 == 0 %}"
+    "{% set content = bos_token + content %}{% endif %}{{ content }}{% endfor %}{% if add_generation_prompt %}"
+    "{{ '<|start_header_id|>assistant<|end_header_id|>\\n\\n' }}{% endif %}")
+
+
+def _checkpoint(d, template=LLAMA3_TEMPLATE):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    corpus = ["De ridders van de ronde tafel bespreken de kernel en de cache.",
+              "Consensus score negen: het voorstel wordt aangenomen door de koning."] * 20
+    tok.train_from_iterator(corpus, trainers.BpeTrainer(vocab_size=400, special_tokens=SPECIAL,
+                                                        initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    tok.save(str(d / "tokenizer.json"))
+    V = tok.get_vocab_size()
+    bos, end, eot = (tok.token_to_id(s) for s in ("<|begin_of_text|>", "<|end_of_text|>", "<|eot_id|>"))
+    torch.manual_seed(0)
+    m = transformers.LlamaForCausalLM(transformers.LlamaConfig(
+        hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
+        vocab_size=V, max_position_embeddings=4096, rope_theta=10000.0, rms_norm_eps=1e-5, tie_word_embeddings=False,
+        bos_token_id=bos, eos_token_id=end))
+    m.save_pretrained(str(d), safe_serialization=True)   # writes config.json + generation_config.json
+    cfg = {"bos_token": "<|begin_of_text|>", "eos_token": "<|eot_id|>"}
+    if template:
+        cfg["chat_template"] = template
+    (d / "tokenizer_config.json").write_text(json.dumps(cfg))
+    (d / "generation_config.json").write_text(json.dumps({"bos_token_id": bos, "eos_token_id": [end, eot]}))
+    return tok, V
+
+
+def _engine(d, V):
+    return Engine(EngineConfig(model="tiny-llama", weights=str(d), device="cpu", dtype="fp32", num_blocks=64,
+                               model_overrides={"vocab": V}))
+
+
+def test_checkpoint_tokenizer_chat_wrap_and_stops(tmp_path):
+    tok, V = _checkpoint(tmp_path)
+    e = _engine(tmp_path, V)
+    t = e.tokenizer
+    assert isinstance(t, HFTokenizer) and t.family.startswith("hf:")
+    assert t.stop_ids == {tok.token_to_id("<|end_of_text|>"), tok.token_to_id("<|eot_id|>")}
+    text = "De ridders bespreken de cache."
+    ids = e.encode_prompt(text)
+    want = tok.encode("<|begin_of_text|><|start_header_id|>user<|end_header_id|>\n\n" + text +
+                      "<|eot_id|><|start_header_id|>assistant<|end_header_id|>\n\n").ids
+    assert ids == want
+    assert t.decode(t.encode(text)) == text
+    # the wrap is constant: a longer prompt re-prefills only the suffix + the new content
+    sp = SamplingParams(temperature=0.0, max_new_tokens=5, ignore_eos=True, stop_on_consensus=False)
+    r1 = e.run_turns([Turn("K", text, sp)])[0]
+    r2 = e.run_turns([Turn("K", text + " Het voorstel wordt aangenomen.", sp)])[0]
+    assert r1.error is None and r2.error is None and len(r2.ids) == 5
+    assert r2.metrics["reused_tokens"] >= len(t.chat_prefix) + len(t.encode(text)) - 1
+    eot = tok.token_to_id("<|eot_id|>")
+    assert cut_at_stop([5, 6, eot, 7], t.stop_ids) == [5, 6, eot]
+
+
+def test_checkpoint_without_template_gets_bos_only(tmp_path):
+    tok, V = _checkpoint(tmp_path, template=None)
+    e = _engine(tmp_path, V)
+    assert e.tokenizer.chat_prefix == (tok.token_to_id("<|begin_of_text|>"),) and e.tokenizer.chat_suffix == ()
+    assert e.encode_prompt("kernel")[0] == tok.token_to_id("<|begin_of_text|>")

@@ -65,6 +65,8 @@ class EngineConfig:
     faults: Dict[int, str] = field(default_factory=dict)
     # validate paging metadata (block tables / slots in range) before every forward (ROUNDTABLE_DEBUG_CHECKS=1)
     debug_checks: bool = False
+    # wrap each turn as one user message with the checkpoint's chat template (checkpoint tokenizers only)
+    chat_template: bool = True
 
 
 @dataclass
@@ -100,7 +102,8 @@ class Engine:
         self.dtype = _dtype(ecfg.dtype)
         if not self.on_gpu and self.dtype == torch.float16:
             self.dtype = torch.float32
-        self.tokenizer: EngineTokenizer = get_tokenizer(self.cfg.vocab)
+        # the checkpoint's own tokenizer + chat template when `weights` ships one, else the bundled BPE
+        self.tokenizer: EngineTokenizer = get_tokenizer(self.cfg.vocab, ecfg.weights, ecfg.chat_template)
         t0 = time.perf_counter()
         with torch.no_grad():
             weights = materialize(self.cfg, ecfg.weights, self.device, self.dtype, self.tp)
@@ -175,6 +178,9 @@ class Engine:
                     self._seg_cache.clear()
                 self._seg_cache[key] = ids
             out.extend(ids)
+        pre, suf = self.tokenizer.chat_prefix, self.tokenizer.chat_suffix
+        if pre or suf:           # constant wrap: the LCP reuse of the content is unaffected
+            return list(pre) + out + list(suf)
         if not out:
             out = [self.tokenizer.bos_id]
         return out
@@ -390,7 +396,7 @@ class Engine:
         chunk = [Turn(t.seq_key, t.prompt, SamplingParams(**{**t.params.__dict__, "max_new_tokens": steps + 1,
                                                               "ignore_eos": True, "stop_on_consensus": False}),
                       t.timeout_s) for t in turns]
-        eos = self.tokenizer.eos_id
+        eos = self.tokenizer.stop_ids
         t0 = time.perf_counter()
         runner = self._graph_for(len(seqs), max(sq.length for sq in seqs) + steps + 1) \
             if self.on_gpu and self.ecfg.use_graphs else None
@@ -427,7 +433,7 @@ class Engine:
         # every sequence: the first sampled token is "generated", then steps-1 decode forwards
         for s, n in zip(seqs, max_new):
             self.kv.ensure_capacity(s, s.length + steps)
-        eos = self.tokenizer.eos_id
+        eos = self.tokenizer.stop_ids
         runner = None
         if self.on_gpu and self.ecfg.use_graphs:
             try:
@@ -446,8 +452,8 @@ class Engine:
         gen: List[List[int]] = []
         for b, (s, t) in enumerate(zip(seqs, turns)):
             g = toks[b][:max_new[b]]
-            if not t.params.ignore_eos and eos in g:
-                g = g[:g.index(eos) + 1]
+            if not t.params.ignore_eos:
+                g = cut_at_stop(g, eos)
             if t.params.stop_on_consensus:
                 g = _cut_at_consensus(self.tokenizer, g)
             gen.append(g)
@@ -514,10 +520,19 @@ class Engine:
         return g
 
 
-def _finished(out: List[int], params: SamplingParams, eos: int, tok: EngineTokenizer) -> bool:
+def cut_at_stop(ids: List[int], stops: frozenset) -> List[int]:
+    """Keep ``ids`` up to and including the first end-of-turn id (``tokenizer.stop_ids``)."""
+    for j, i in enumerate(ids):
+        if i in stops:
+            return ids[:j + 1]
+    return ids
+
+
+def _finished(out: List[int], params: SamplingParams, eos: frozenset, tok: EngineTokenizer) -> bool:
+    """``eos``: the tokenizer's stop-id set."""
     if len(out) >= params.max_new_tokens:
         return True
-    if not params.ignore_eos and eos in out:
+    if not params.ignore_eos and not eos.isdisjoint(out):
         return True
     if params.stop_on_consensus and len(out) > 8:
         return _consensus_closed(tok, out)

@@ -102,7 +102,8 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         from ..engine.tokenizer import get_tokenizer
         from ..models.config import get_config
         st = engine_settings(config, config.knights[0].adapter)
-        tokenizer = get_tokenizer(get_config(st["model"]).vocab)
+        tokenizer = get_tokenizer(get_config(st["model"], **dict(st.get("model_overrides") or {})).vocab,
+                                  str(st.get("weights", "random:0")))
     pool = DistributedPool(cluster, placement, local, tokenizer)
     backends = {aid: RemoteKnight(pool, aid, display_name(aid, config), aid) for aid in placement}
     return backends, pool

@@ -36,6 +36,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional, Tuple
 
 from .engine import Engine, EngineConfig, SamplingParams, Turn
+from .engine.engine import cut_at_stop
 
 ROLE_TAGS = {"system": "Systeem", "user": "Gebruiker", "assistant": "Assistent"}
 
@@ -131,8 +132,9 @@ class Scheduler:
 
     # ---- completion ---------------------------------------------------------------------------
     def _finished(self, a: _Active) -> bool:
-        eos = self.engine.tokenizer.eos_id
-        return len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos and eos in a.gen)
+        stops = self.engine.tokenizer.stop_ids
+        return len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos
+                                                              and not stops.isdisjoint(a.gen))
 
     def _complete(self, a: _Active, error: Optional[BaseException] = None) -> None:
         r = a.req
@@ -142,9 +144,8 @@ class Scheduler:
                 self.stats["errors"] += 1
         else:
             gen = a.gen[:a.req.params.max_new_tokens]
-            eos = self.engine.tokenizer.eos_id
-            if eos in gen and not a.req.params.ignore_eos:
-                gen = gen[:gen.index(eos) + 1]
+            if not a.req.params.ignore_eos:
+                gen = cut_at_stop(gen, self.engine.tokenizer.stop_ids)
             m = dict(a.metrics, decode_tokens=len(gen), turn_ms=(time.perf_counter() - a.t0) * 1e3)
             r.result = _Output(self.engine.tokenizer.decode(gen), gen, m)
             with self._lock:
