@@ -79,3 +79,27 @@ def test_checkpoint_without_template_gets_bos_only(tmp_path):
     e = _engine(tmp_path, V)
     assert e.tokenizer.chat_prefix == (tok.token_to_id("<|begin_of_text|>"),) and e.tokenizer.chat_suffix == ()
     assert e.encode_prompt("kernel")[0] == tok.token_to_id("<|begin_of_text|>")
+
+
+def test_serve_checkpoint_dir_uses_its_template(tmp_path):
+    """`roundtable serve --weights <checkpoint>`: architecture from config.json, conversation
+    rendered by the checkpoint's chat template (all messages, one generation prompt)."""
+    import urllib.request
+    from theroundtaible_amd.serve import build_server
+    tok, V = _checkpoint(tmp_path)
+    srv = build_server("llama3-8b", weights=str(tmp_path), device="cpu", port=0, max_batch=2, max_tokens=6,
+                       num_blocks=64).start()
+    try:
+        msgs = [{"role": "system", "content": "Wees kort."}, {"role": "user", "content": "Wat zegt de koning?"}]
+        req = urllib.request.Request(srv.url + "/v1/chat/completions", method="POST",
+                                     data=json.dumps({"messages": msgs, "max_tokens": 4, "ignore_eos": True}).encode(),
+                                     headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=120) as r:
+            d = json.loads(r.read().decode())
+        rendered = ("<|begin_of_text|><|start_header_id|>system<|end_header_id|>\n\nWees kort.<|eot_id|>"
+                    "<|start_header_id|>user<|end_header_id|>\n\nWat zegt de koning?<|eot_id|>"
+                    "<|start_header_id|>assistant<|end_header_id|>\n\n")
+        assert d["usage"]["prompt_tokens"] == len(tok.encode(rendered).ids)
+        assert d["usage"]["completion_tokens"] == 4
+    finally:
+        srv.close()

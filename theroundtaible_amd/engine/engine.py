@@ -179,7 +179,8 @@ class Engine:
                 self._seg_cache[key] = ids
             out.extend(ids)
         pre, suf = self.tokenizer.chat_prefix, self.tokenizer.chat_suffix
-        if pre or suf:           # constant wrap: the LCP reuse of the content is unaffected
+        if (pre or suf) and not getattr(prompt, "templated", False):
+            # constant wrap: the LCP reuse of the content is unaffected
             return list(pre) + out + list(suf)
         if not out:
             out = [self.tokenizer.bos_id]

@@ -145,6 +145,7 @@ class HFTokenizer:
         tmpl = tc.get("chat_template")
         if isinstance(tmpl, list):   # named templates: use "default"
             tmpl = next((t.get("template") for t in tmpl if isinstance(t, dict) and t.get("name") == "default"), None)
+        self._template = None
         if not isinstance(tmpl, str):
             return (), ()
         import jinja2
@@ -155,15 +156,28 @@ class HFTokenizer:
         env = ImmutableSandboxedEnvironment(trim_blocks=True, lstrip_blocks=True)
         env.globals["raise_exception"] = raise_exception
         try:
-            text = env.from_string(tmpl).render(messages=[{"role": "user", "content": self._MARK}],
-                                                add_generation_prompt=True, bos_token=bos or "", eos_token=eos or "")
+            compiled = env.from_string(tmpl)
+            text = compiled.render(messages=[{"role": "user", "content": self._MARK}],
+                                   add_generation_prompt=True, bos_token=bos or "", eos_token=eos or "")
         except Exception:  # noqa: BLE001 - a template we cannot render: plain prompt
             return (), ()
+        self._template = (compiled, bos or "", eos or "")
         if self._MARK not in text:
             return (), ()
         pre, suf = text.split(self._MARK, 1)
         enc = lambda s: tuple(self._tok.encode(s, add_special_tokens=False).ids) if s else ()
         return enc(pre), enc(suf)
+
+    def render_chat(self, messages: List[dict]) -> Optional[str]:
+        """A whole conversation through the checkpoint's chat template (ends in an open assistant
+        turn); None when the checkpoint has no renderable template."""
+        if getattr(self, "_template", None) is None:
+            return None
+        compiled, bos, eos = self._template
+        try:
+            return compiled.render(messages=messages, add_generation_prompt=True, bos_token=bos, eos_token=eos)
+        except Exception:  # noqa: BLE001 - e.g. a template that rejects this role order
+            return None
 
     def encode(self, text: str) -> List[int]:
         return self._tok.encode(text, add_special_tokens=False).ids if text else []

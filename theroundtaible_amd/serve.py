@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import itertools
 import json
+import os
 import queue
 import threading
 import time
@@ -39,6 +40,12 @@ from .engine import Engine, EngineConfig, SamplingParams, Turn
 from .engine.engine import cut_at_stop
 
 ROLE_TAGS = {"system": "Systeem", "user": "Gebruiker", "assistant": "Assistent"}
+
+
+def _content_text(content: Any) -> str:
+    if isinstance(content, list):  # OpenAI content parts
+        return "".join(p.get("text", "") for p in content if isinstance(p, dict))
+    return str(content)
 
 
 def render_chat(messages: List[Dict[str, Any]]) -> str:
@@ -293,7 +300,7 @@ class RoundtableServer:
                 msgs = body.get("messages")
                 if not isinstance(msgs, list) or not msgs:
                     raise ValueError("'messages' must be a non-empty list")
-                out, r = server.generate(render_chat(msgs), body, body.get("user") or body.get("session"))
+                out, r = server.generate(server.chat_prompt(msgs), body, body.get("user") or body.get("session"))
                 rid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
                 usage = server.usage(out)
                 if body.get("stream"):
@@ -331,7 +338,7 @@ class RoundtableServer:
                 params = {"temperature": opts.get("temperature"), "top_p": opts.get("top_p"),
                           "top_k": opts.get("top_k"), "seed": opts.get("seed"),
                           "max_tokens": opts.get("num_predict")}
-                out, _ = server.generate(render_chat(msgs), params, body.get("session"))
+                out, _ = server.generate(server.chat_prompt(msgs), params, body.get("session"))
                 self._send(200, {"model": server.model_name, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ"),
                                  "message": {"role": "assistant", "content": out.text}, "done": True,
                                  "prompt_eval_count": int(out.metrics.get("prompt_tokens", 0)),
@@ -343,6 +350,19 @@ class RoundtableServer:
         self._thread: Optional[threading.Thread] = None
 
     # ---- request plumbing -----------------------------------------------------------------
+    def chat_prompt(self, messages: List[Dict[str, Any]]):
+        """The conversation through the checkpoint's own chat template when the engine has one
+        (marked templated: no extra wrap), else the plain role-tagged transcript."""
+        from .prompt import Prompt, Segment
+        render = getattr(self.engine.tokenizer, "render_chat", None)
+        if render is not None:
+            norm = [{"role": str(m.get("role", "user")), "content": _content_text(m.get("content", ""))}
+                    for m in messages]
+            text = render(norm)
+            if text is not None:
+                return Prompt([Segment(text)], templated=True)
+        return render_chat(messages)
+
     def sampling(self, body: Dict[str, Any]) -> SamplingParams:
         def num(key, default, cast):
             v = body.get(key)
@@ -425,8 +445,15 @@ class RoundtableServer:
 def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", dtype: str = "bf16",
                  host: str = "127.0.0.1", port: int = 8000, max_batch: int = 16, max_tokens: int = 512,
                  use_graphs: bool = True, num_blocks: Optional[int] = None) -> RoundtableServer:
+    overrides = {}
+    if os.path.isdir(weights):
+        # a checkpoint directory defines the architecture: preset + shape overrides from config.json
+        from .utils.local_detect import checkpoint_model
+        found = checkpoint_model(weights)
+        if found is not None:
+            model, overrides = found[0], dict(found[1])
     ecfg = EngineConfig(model=model, weights=weights, device=device, dtype=dtype, use_graphs=use_graphs,
-                        max_batch=max_batch, num_blocks=num_blocks)
+                        max_batch=max_batch, num_blocks=num_blocks, model_overrides=overrides)
     if ecfg.device == "cpu":
         ecfg.dtype = "fp32" if dtype == "bf16" else dtype
         ecfg.use_graphs = False

@@ -93,6 +93,20 @@ def match_preset(shape: Dict[str, Any]) -> (Optional[str], Dict[str, Any]):
     return best, (best_diff or {})
 
 
+def checkpoint_model(path: str) -> Optional[tuple]:
+    """(engine preset, ModelConfig overrides) for an HF checkpoint directory, from its
+    ``config.json`` alone; None if it is not a recognised Llama / Mistral / GPT-2 checkpoint."""
+    try:
+        with open(os.path.join(path, "config.json"), encoding="utf-8") as f:
+            shape = _shape_from_hf(json.load(f))
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    if shape is None:
+        return None
+    preset, diff = match_preset(shape)
+    return (preset, diff) if preset else None
+
+
 def _model_id(path: str) -> str:
     m = re.search(r"models--([^/]+)--([^/]+)/snapshots/", path.replace(os.sep, "/"))
     if m:
