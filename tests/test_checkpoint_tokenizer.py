@@ -103,3 +103,21 @@ def test_serve_checkpoint_dir_uses_its_template(tmp_path):
         assert d["usage"]["completion_tokens"] == 4
     finally:
         srv.close()
+
+
+def test_knight_on_checkpoint_dir_without_overrides(tmp_path):
+    """A config seat that only names the checkpoint directory: preset + shape come from config.json."""
+    from theroundtaible_amd.knights.registry import BackendFactory
+    from theroundtaible_amd.types import RoundtableConfig
+    (tmp_path / "ckpt").mkdir()
+    tok, V = _checkpoint(tmp_path / "ckpt")
+    cfg = RoundtableConfig.from_dict({
+        "version": "1.0", "project": "t", "knights": [{"name": "Local", "adapter": "local-llm-ckpt",
+                                                       "capabilities": [], "priority": 1}],
+        "rules": {}, "chronicle": ".roundtable/chronicle.md",
+        "adapter_config": {"local-llm-ckpt": {"engine": {"model": "llama3-8b", "weights": str(tmp_path / "ckpt"),
+                                                         "device": "cpu", "max_new_tokens": 3}}}})
+    b = BackendFactory(cfg).create("local-llm-ckpt")
+    assert b.engine.cfg.vocab == V and b.engine.cfg.hidden == 256
+    res = b.execute("De koning spreekt.", 60.0, seq_key="Local")
+    assert isinstance(res.text, str) and len(res.ids) == 3

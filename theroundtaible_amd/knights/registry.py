@@ -14,6 +14,7 @@ from ..config import engine_settings
 from ..engine.engine import EngineConfig
 from ..engine.sampler import SamplingParams
 from ..types import RoundtableConfig
+from ..utils.local_detect import resolve_model
 from ..utils.ui import NULL_UI, UI
 from .base import KnightBackend
 from .engine_backend import ADAPTER_DISPLAY_NAMES, EngineBackend, EnginePool
@@ -74,13 +75,15 @@ class BackendFactory:
         ac = self.config.adapter_config.get(adapter_id) or {}
         if isinstance(ac, dict) and wants_external(adapter_id, ac):
             return create_external(adapter_id, ac, name)
-        ecfg = EngineConfig(model=st["model"], weights=str(st.get("weights", "random:0")),
+        weights = str(st.get("weights", "random:0"))
+        model, overrides = resolve_model(st["model"], weights, st.get("model_overrides"))
+        ecfg = EngineConfig(model=model, weights=weights,
                             dtype=str(st.get("dtype", "bf16")), device=self._device_for(adapter_id, st),
                             block_size=int(st.get("kv_block_size", 32)),
                             kv_cache_fraction=float(st.get("kv_cache_fraction", 0.85)),
                             max_kv_tokens=st.get("max_kv_tokens"),
                             use_graphs=bool(st.get("use_graphs", True)),
-                            model_overrides=dict(st.get("model_overrides") or {}))
+                            model_overrides=overrides)
         if ecfg.device == "cpu":
             ecfg.dtype = "fp32" if st.get("dtype") in (None, "bf16") and st.get("cpu_fp32", True) else ecfg.dtype
             ecfg.use_graphs = False

@@ -27,6 +27,7 @@ from ..engine.sampler import SamplingParams
 from ..parallel.cluster import Cluster
 from ..parallel.tp import TPInfo
 from ..types import RoundtableConfig
+from ..utils.local_detect import resolve_model
 from ..utils.ui import NULL_UI, UI
 from .distributed import DistributedPool, RemoteKnight
 from .engine_backend import EngineBackend
@@ -79,13 +80,14 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         tp = TPInfo(size=len(ranks), rank=ranks.index(cluster.rank), group=groups.get(tuple(ranks)))
         ekey = (st["model"], str(st.get("weights", "random:0")), str(st.get("dtype", "bf16")), tuple(ranks))
         if ekey not in engines:
-            ecfg = EngineConfig(model=st["model"], weights=str(st.get("weights", "random:0")),
+            model, overrides = resolve_model(st["model"], str(st.get("weights", "random:0")), st.get("model_overrides"))
+            ecfg = EngineConfig(model=model, weights=str(st.get("weights", "random:0")),
                                 dtype=str(st.get("dtype", "bf16")), device=cluster.device,
                                 block_size=int(st.get("kv_block_size", 32)),
                                 kv_cache_fraction=float(st.get("kv_cache_fraction", 0.85)),
                                 max_kv_tokens=st.get("max_kv_tokens"),
                                 use_graphs=bool(st.get("use_graphs", True)) and cluster.device.startswith("cuda"),
-                                model_overrides=dict(st.get("model_overrides") or {}))
+                                model_overrides=overrides)
             if not ecfg.device.startswith("cuda"):
                 ecfg.dtype = "fp32"
             engines[ekey] = (Engine(ecfg, tp), threading.Lock())
@@ -102,8 +104,8 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         from ..engine.tokenizer import get_tokenizer
         from ..models.config import get_config
         st = engine_settings(config, config.knights[0].adapter)
-        tokenizer = get_tokenizer(get_config(st["model"], **dict(st.get("model_overrides") or {})).vocab,
-                                  str(st.get("weights", "random:0")))
+        model, overrides = resolve_model(st["model"], str(st.get("weights", "random:0")), st.get("model_overrides"))
+        tokenizer = get_tokenizer(get_config(model, **overrides).vocab, str(st.get("weights", "random:0")))
     pool = DistributedPool(cluster, placement, local, tokenizer)
     backends = {aid: RemoteKnight(pool, aid, display_name(aid, config), aid) for aid in placement}
     return backends, pool

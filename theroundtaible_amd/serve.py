@@ -445,13 +445,9 @@ class RoundtableServer:
 def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", dtype: str = "bf16",
                  host: str = "127.0.0.1", port: int = 8000, max_batch: int = 16, max_tokens: int = 512,
                  use_graphs: bool = True, num_blocks: Optional[int] = None) -> RoundtableServer:
-    overrides = {}
-    if os.path.isdir(weights):
-        # a checkpoint directory defines the architecture: preset + shape overrides from config.json
-        from .utils.local_detect import checkpoint_model
-        found = checkpoint_model(weights)
-        if found is not None:
-            model, overrides = found[0], dict(found[1])
+    # a checkpoint directory defines the architecture: preset + shape overrides from config.json
+    from .utils.local_detect import resolve_model
+    model, overrides = resolve_model(model, weights)
     ecfg = EngineConfig(model=model, weights=weights, device=device, dtype=dtype, use_graphs=use_graphs,
                         max_batch=max_batch, num_blocks=num_blocks, model_overrides=overrides)
     if ecfg.device == "cpu":

@@ -107,6 +107,18 @@ def checkpoint_model(path: str) -> Optional[tuple]:
     return (preset, diff) if preset else None
 
 
+def resolve_model(model: str, weights: str, overrides: Optional[Dict[str, Any]] = None) -> tuple:
+    """(preset, overrides) to build an engine for ``weights``: a checkpoint directory defines the
+    architecture unless the config pins ``model_overrides`` explicitly."""
+    if overrides:
+        return model, dict(overrides)
+    if weights and os.path.isdir(weights):
+        found = checkpoint_model(weights)
+        if found is not None:
+            return found[0], dict(found[1])
+    return model, {}
+
+
 def _model_id(path: str) -> str:
     m = re.search(r"models--([^/]+)--([^/]+)/snapshots/", path.replace(os.sep, "/"))
     if m:
