@@ -45,6 +45,8 @@ int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, 
                         int I, int Hq, int Hkv, int head_dim, int BS, int max_blocks, int num_splits, float eps,
                         float scale, hipStream_t stream);
 int decode_layer_grid();
+int launch_ring_gemm(void* out, const void* x, const void* Ws, int M, int N, int K, int grid, int variant,
+                     hipStream_t stream);
 int oneshot_create(int world, int rank, int cap_elems, char* handles);
 int oneshot_open(int id, const char* all_handles);
 int oneshot_capacity(int id);
@@ -304,6 +306,19 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
+// EXPERIMENT: loader-wave + LDS-ring decode GEMM (csrc/ring_gemm.hip), microbenchmarks only.
+void ring_gemm_exp(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t grid, int64_t variant) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  check_bf16(Ws, "Ws");
+  TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1) && out.size(0) == x.size(0) &&
+                  out.size(1) == Ws.size(0),
+              "ring_gemm_exp: shapes");
+  const int rc = launch_ring_gemm(out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)x.size(0), (int)Ws.size(0),
+                                  (int)x.size(1), (int)grid, (int)variant, cur_stream());
+  TORCH_CHECK(rc == 0, "ring_gemm_exp: unsupported configuration (rc=", rc, ")");
+}
+
 // K9 one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot_ar.hip).
 py::tuple py_oneshot_create(int64_t world, int64_t rank, int64_t cap_elems) {
   char h[128] = {0};
@@ -469,6 +484,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("part_ml"), py::arg("split_counters"), py::arg("sync"), py::arg("err"), py::arg("Hq"),
         py::arg("Hkv"), py::arg("num_splits"), py::arg("eps"), py::arg("scale"), py::arg("stamps") = py::none());
   m.def("decode_layer_grid", &decode_layer_grid);
+  m.def("ring_gemm_exp", &ring_gemm_exp, py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("grid") = 0, py::arg("variant") = 0);
   m.def("oneshot_create", &py_oneshot_create, py::arg("world"), py::arg("rank"), py::arg("cap_elems"));
   m.def("oneshot_open", &py_oneshot_open, py::arg("id"), py::arg("all_handles"), py::arg("world"));
   m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
