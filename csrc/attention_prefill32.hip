@@ -174,24 +174,21 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
 #pragma unroll
           for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const float v = sc[blk][i] * scale_log2;
-              sc[blk][i] = v;
-              tmax = fmaxf(tmax, v);
-            }
+            for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, sc[blk][i]);
         } else {                                  // diagonal tile: causal mask per element
 #pragma unroll
           for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
               const int key = t * KT + 32 * blk + 16 * (i >> 3) + 8 * h + (i & 7);
-              float v = sc[blk][i] * scale_log2;
-              v = key <= my_pos ? v : -INFINITY;
+              const float v = key <= my_pos ? sc[blk][i] : -INFINITY;
               sc[blk][i] = v;
               tmax = fmaxf(tmax, v);
             }
         }
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        // scores stay raw: the scale (> 0) commutes with max and is folded into the FMA that
+        // feeds exp2 below (one VALU op per score instead of a multiply pass plus a subtract)
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
         // deferred rescale (guide T13): the running max moves only when some column's tile max
         // exceeds it by more than 2^RESCALE (then P <= 2^RESCALE, still exact enough in bf16 and
         // in the f32 sums). Wave-uniform branch, so most tiles skip the 64-multiply O rescale.
@@ -213,8 +210,8 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
           rt::u32x4 w;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float p0 = rt::fast_exp2(sc[kc >> 1][8 * (kc & 1) + 2 * j] - msub);
-            const float p1 = rt::fast_exp2(sc[kc >> 1][8 * (kc & 1) + 2 * j + 1] - msub);
+            const float p0 = rt::fast_exp2(__builtin_fmaf(sc[kc >> 1][8 * (kc & 1) + 2 * j], scale_log2, -msub));
+            const float p1 = rt::fast_exp2(__builtin_fmaf(sc[kc >> 1][8 * (kc & 1) + 2 * j + 1], scale_log2, -msub));
             psum += p0 + p1;
             w[j] = rt::pack2(p0, p1);
           }
