@@ -156,13 +156,16 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
         // ---- S^T = K Q^T (two 32-key blocks) ----
         f16v sc[2];
 #pragma unroll
-        for (int blk = 0; blk < 2; ++blk) {
+        for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
           for (int i = 0; i < 16; ++i) sc[blk][i] = 0.f;
-          const int krow = 32 * blk + swap23(c);
+        // the two key blocks' accumulation chains interleaved (independent MFMAs back to back)
 #pragma unroll
-          for (int dk = 0; dk < D / 16; ++dk) {
-            const int ch = 2 * dk + h;
+        for (int dk = 0; dk < D / 16; ++dk) {
+          const int ch = 2 * dk + h;
+#pragma unroll
+          for (int blk = 0; blk < 2; ++blk) {
+            const int krow = 32 * blk + swap23(c);
             const short8 a = *reinterpret_cast<const short8*>(kb + krow * KROW + 16 * (ch ^ (krow & 15)));
             sc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                               __builtin_bit_cast(bf16x8, qf[dk]), sc[blk], 0, 0, 0);
