@@ -122,22 +122,24 @@ RT_DEVICE void issue_w(Stage<PRO, EPI, U>& st, const short8* __restrict__ wt, co
   constexpr size_t kStride = (EPI == EPI_SWIGLU) ? 128 : 64;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int s = s0 + NW * u;
-    if (s < nsteps) {
-      st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + lane);
-      if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + 64 + lane);
-    }
+    // unconditional (steps past the end re-read the last one: an L2 hit) so hipcc counts the
+    // loads and waits vmcnt(next stage) before a stage's MFMAs instead of draining vmcnt(0)
+    const int s = min(s0 + NW * u, nsteps - 1);
+    st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + lane);
+    if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + 64 + lane);
   }
 }
 
 template <int PRO, int EPI, int NW, int U, bool SC1>
 RT_DEVICE void issue_a(Stage<PRO, EPI, U>& st, const XSrc& xr, const XSrc& xr2, bool row_ok, int s0, int nsteps) {
-  const short8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  // unconditional as issue_w: lanes of rows >= M read row 0 (their MFMA rows and row sums are
+  // never stored), steps past the end re-read the last one
+  (void)row_ok;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int s = s0 + NW * u;
-    st.a[u] = (row_ok && s < nsteps) ? ld_x8<SC1>(xr, s * 32) : z;
-    if constexpr (PRO == PRO_NORM_ADD) st.b[u] = (row_ok && s < nsteps) ? ld_x8<SC1>(xr2, s * 32) : z;
+    const int s = min(s0 + NW * u, nsteps - 1);
+    st.a[u] = ld_x8<SC1>(xr, s * 32);
+    if constexpr (PRO == PRO_NORM_ADD) st.b[u] = ld_x8<SC1>(xr2, s * 32);
   }
 }
 
@@ -209,27 +211,24 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
   float ssq = 0.f;
   Stage<PRO, EPI, U> st1;
-  int s = wid;
-  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s, nsteps, lane);
-  issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s, nsteps);
-  for (;;) {
-    const int sn = s + NW * U;
-    if (sn < nsteps) {
-      issue_w<PRO, EPI, NW, U>(st1, wt, wt2, sn, nsteps, lane);
-      issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, sn, nsteps);
-    }
+  // stages of this wave: s = wid + NW*U*j < nsteps. Both halves of a pair sit in ONE basic
+  // block (a break between them lets MachineSink move each stage's loads down next to their
+  // consumer); every issue is unconditional, so the waits are counted, not vmcnt(0).
+  constexpr int SPAN = NW * U;
+  const int nst = wid < nsteps ? (nsteps - wid + SPAN - 1) / SPAN : 0;
+  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane);
+  issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, wid, nsteps);
+  int j = 0;
+  for (; j + 1 < nst; j += 2) {
+    const int s = wid + SPAN * j;
+    issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane);
+    issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
     consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
-    if (sn >= nsteps) break;
-    s = sn;
-    const int sn2 = s + NW * U;
-    if (sn2 < nsteps) {
-      issue_w<PRO, EPI, NW, U>(st0, wt, wt2, sn2, nsteps, lane);
-      issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, sn2, nsteps);
-    }
-    consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
-    if (sn2 >= nsteps) break;
-    s = sn2;
+    issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane);
+    issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
+    consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
   }
+  if (j < nst) consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, wid + SPAN * j, nsteps, xo_r, xo_s);
 
   // C layout: acc[i] = C[m = 4g + i][n = r]
 #pragma unroll
