@@ -77,10 +77,11 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     re = *static_cast<const RopeEpi*>(rope);
     if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
   }
-  // Variant = (waves per workgroup NW, k-steps per stage U). Few column tiles (o/down/qkv
-  // projections: <= ~1.5 workgroups per CU) -> 8 waves so each CU keeps enough weight
-  // bytes in flight; wide GEMMs (gate_up, lm_head) -> 4. RT_SKINNY_CFG=<NW>x<U> (4x4, 8x4,
-  // 8x8, 4x8) pins one for microbenchmarks (tools/microbench.py).
+  // Variant = (waves per workgroup NW, k-steps per stage U). Since the pipeline's waits are
+  // counted (skinny_core.h gemm_tile), 4 waves x 4 steps wins on every decode shape
+  // (profiles/r01_microbench_v3_cfg_sweep.log: qkv 11.9 vs 12.7 us at 8x4, o 7.75 vs 8.3);
+  // before that, the narrow projections needed 8 waves to keep bytes in flight.
+  // RT_SKINNY_CFG=<NW>x<U> (4x4, 8x4, 8x8, 4x8) pins one for microbenchmarks.
   static const int cfg_env = [] {
     const char* e = getenv("RT_SKINNY_CFG");
     if (!e) return 0;
@@ -88,7 +89,7 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     if (sscanf(e, "%dx%d", &nw, &u) != 2) return 0;
     return nw * 100 + u;
   }();
-  const int cfg = cfg_env ? cfg_env : ((N / 16) >= 768 ? 404 : 804);
+  const int cfg = cfg_env ? cfg_env : 404;
   dim3 grid(N / 16);
 #define RT_SG(P, E)                                                                                          \
   do {                                                                                                       \
