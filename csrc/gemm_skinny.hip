@@ -78,10 +78,11 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
   }
   // Variant = (waves per workgroup NW, k-steps per stage U). Since the pipeline's waits are
-  // counted (skinny_core.h gemm_tile), 4 waves x 4 steps wins on every decode shape
-  // (profiles/r01_microbench_v3_cfg_sweep.log: qkv 11.9 vs 12.7 us at 8x4, o 7.75 vs 8.3);
-  // before that, the narrow projections needed 8 waves to keep bytes in flight.
-  // RT_SKINNY_CFG=<NW>x<U> (4x4, 8x4, 8x8, 4x8) pins one for microbenchmarks.
+  // counted (skinny_core.h gemm_tile), 4 waves win on every decode shape: U = 2 for the wide
+  // GEMMs (>= 384 column tiles: qkv 11.5, gate_up 39.0 us), U = 4 for the 256-tile o / down
+  // (8.05 / 20.9 us; U = 2 loses there) — profiles/r01_microbench_v3_cfg_sweep.log, v4.
+  // Before the counted waits the narrow projections needed 8 waves to keep bytes in flight.
+  // RT_SKINNY_CFG=<NW>x<U> (4x2, 8x2, 4x4, 8x4, 8x8, 4x8) pins one for microbenchmarks.
   static const int cfg_env = [] {
     const char* e = getenv("RT_SKINNY_CFG");
     if (!e) return 0;
@@ -89,11 +90,13 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     if (sscanf(e, "%dx%d", &nw, &u) != 2) return 0;
     return nw * 100 + u;
   }();
-  const int cfg = cfg_env ? cfg_env : 404;
+  const int cfg = cfg_env ? cfg_env : ((N / 16) >= 384 ? 402 : 404);
   dim3 grid(N / 16);
 #define RT_SG(P, E)                                                                                          \
   do {                                                                                                       \
     switch (cfg) {                                                                                           \
+      case 402: RT_SGV(P, E, 4, 2); break;                                                                   \
+      case 802: RT_SGV(P, E, 8, 2); break;                                                                   \
       case 408: RT_SGV(P, E, 4, 8); break;                                                                   \
       case 804: RT_SGV(P, E, 8, 4); break;                                                                   \
       case 808: RT_SGV(P, E, 8, 8); break;                                                                   \
