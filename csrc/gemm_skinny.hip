@@ -80,7 +80,8 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   // Variant = (waves per workgroup NW, k-steps per stage U). Since the pipeline's waits are
   // counted (skinny_core.h gemm_tile), 4 waves win on every decode shape: U = 2 for the wide
   // GEMMs (>= 384 column tiles: qkv 11.5, gate_up 39.0 us), U = 4 for the 256-tile o / down
-  // (8.05 / 20.9 us; U = 2 loses there) — profiles/r01_microbench_v3_cfg_sweep.log, v4.
+  // (8.05 / 20.9 us; U = 2 loses there) — profiles/r01_microbench_v3_cfg_sweep.log, v4, v5
+  // (4x1, 2x2, 2x4 lose on every shape).
   // Before the counted waits the narrow projections needed 8 waves to keep bytes in flight.
   // RT_SKINNY_CFG=<NW>x<U> (4x2, 8x2, 4x4, 8x4, 8x8, 4x8) pins one for microbenchmarks.
   static const int cfg_env = [] {
