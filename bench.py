@@ -63,8 +63,24 @@ def parse():
     return p.parse_args()
 
 
+def _self_launch(args) -> int:
+    """``--gpus N`` (N > 1) outside a launcher: start the N ranks as a CHILD torchrun (before this
+    process touches the GPU), forward its output and exit with its code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main() -> int:
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _self_launch(args)
     from theroundtaible_amd.utils.debug import apply_debug_env
     if apply_debug_env():
         print("bench: ROUNDTABLE_DEBUG=1 — kernels serialized, numbers are NOT performance data", file=sys.stderr)
@@ -79,6 +95,9 @@ def main() -> int:
 
     cl = init_cluster(prefer_gpu=args.device != "cpu")
     N = cl.world
+    if N != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but {N} rank(s) joined (WORLD_SIZE); refusing to "
+                         f"report a {N}-GPU run as {args.gpus}")
     device = args.device or cl.device
     kpt = args.knights_per_table
     T = max(1, args.tp)
@@ -184,7 +203,8 @@ def main() -> int:
                    "round_mode": args.round_mode, "prompt_layout": args.layout,
                    "parallelism": (f"knight-placement x{N} (tables striped over GPUs), C1 all-gather" if T == 1 else
                                    f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL")},
-        "detail": {"failed_turns": len(failures), "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
+        "detail": {"world": cl.world, "backend": cl.backend, "c1_ranks": cl.world if cl.distributed else 1,
+                   "failed_turns": len(failures), "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
                    "kv_capacity_tokens": engine.kv_capacity_tokens},

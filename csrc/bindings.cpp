@@ -52,6 +52,8 @@ int oneshot_open(int id, const char* all_handles);
 int oneshot_capacity(int id);
 int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream);
 int oneshot_error(int id);
+int oneshot_clear_error(int id);
+int oneshot_set_poll_limit(int id, long long limit);
 void oneshot_destroy(int id);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
@@ -490,6 +492,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
   m.def("oneshot_capacity", [](int64_t id) { return oneshot_capacity((int)id); });
   m.def("oneshot_error", [](int64_t id) { return oneshot_error((int)id); });
+  m.def("oneshot_clear_error", [](int64_t id) { return oneshot_clear_error((int)id); });
+  m.def("oneshot_set_poll_limit", [](int64_t id, int64_t limit) { return oneshot_set_poll_limit((int)id, limit); });
   m.def("oneshot_destroy", [](int64_t id) { oneshot_destroy((int)id); });
   m.def("decode_advance", &decode_advance);
   m.def("paging_guard", &paging_guard, py::arg("block_tables"), py::arg("ctx_lens"), py::arg("positions"),

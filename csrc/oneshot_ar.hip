@@ -26,7 +26,7 @@
 namespace {
 constexpr int MAXW = 8;    // ranks per all-reduce group (one xGMI hop to every peer)
 constexpr int MAXB = 64;   // workgroups per call (flags per (slot, source rank))
-constexpr long long FLAG_POLL_LIMIT = 1ll << 26;
+constexpr long long FLAG_POLL_LIMIT = 1ll << 26;   // default bound (~seconds); tests lower it per comm
 
 struct Peers {
   uint16_t* data[MAXW];    // rank p's receive buffer: [2 slots][world][cap] bf16
@@ -35,7 +35,7 @@ struct Peers {
 
 __global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ inout, int n, int rank, int world,
                                                          int cap, Peers P, uint32_t* epoch_ctr, uint32_t* done_ctr,
-                                                         int* err) {
+                                                         int* err, long long poll_limit) {
   const uint32_t epoch = __hip_atomic_load(epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int slot = (int)(epoch & 1u);
   const int nb = gridDim.x, blk = blockIdx.x;
@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ 
     long long it = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       __builtin_amdgcn_s_sleep(1);
-      if (++it > FLAG_POLL_LIMIT) {
+      if (++it > poll_limit) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -109,6 +109,7 @@ struct Comm {
   uint32_t* flags = nullptr;              // own flags
   uint32_t* ctr = nullptr;                // [epoch, done] (plain device memory, local only)
   int* err = nullptr;
+  long long poll_limit = FLAG_POLL_LIMIT;
   Peers peers{};
   std::vector<void*> opened;              // IPC mappings to close
 };
@@ -196,7 +197,7 @@ int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream) {
   int nb = n / 2048;                                // ~4 KB of slice per workgroup
   nb = nb < 1 ? 1 : (nb > MAXB ? MAXB : nb);
   hipLaunchKernelGGL(oneshot_ar_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
-                     c->cap, c->peers, c->ctr, c->ctr + 1, c->err);
+                     c->cap, c->peers, c->ctr, c->ctr + 1, c->err, c->poll_limit);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
@@ -207,6 +208,21 @@ int oneshot_error(int id) {
   int e = 0;
   if (hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -2;
   return e;
+}
+
+// Clears the poll-expiry flag after the host has failed the affected turn.
+int oneshot_clear_error(int id) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  return hipMemset(c->err, 0, sizeof(int)) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -2;
+}
+
+// Flag-wait bound in poll iterations (fault-injection tests force an expiry with a tiny bound).
+int oneshot_set_poll_limit(int id, long long limit) {
+  Comm* c = get(id);
+  if (c == nullptr || limit < 1) return -1;
+  c->poll_limit = limit;
+  return 0;
 }
 
 void oneshot_destroy(int id) {

@@ -98,7 +98,7 @@ def _bench(nproc, extra=()):
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
-           "--device", "cpu", "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "8",
+           "--gpus", str(nproc), "--device", "cpu", "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "8",
            "--temperature", "0", *extra]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
@@ -161,3 +161,26 @@ def test_spmd_bench_tp2():
     out = _bench(2, ("--tp", "2", "--knights-per-table", "2", "--knights-per-gpu", "2"))
     assert out["config"]["knights"] == 2 and "tp2" in out["config"]["parallelism"]
     assert out["detail"]["decode_tokens"] == 2 * 8 * 2
+
+
+def test_bench_gpus_flag_self_launches_ranks():
+    """`python bench.py --gpus 4` without a launcher starts 4 ranks itself (child torchrun) and
+    reports them — never a silent 1-GPU run (VERDICT r1 #1)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--device", "cpu", "--model", "tiny-llama",
+           "--steps", "1", "--warmup", "1", "--new-tokens", "4", "--temperature", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 4 and out["config"]["tables"] == 4 and out["detail"]["world"] == 4
+
+
+def test_bench_rejects_world_mismatch():
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "3",
+           "--device", "cpu", "--model", "tiny-llama", "--steps", "1", "--warmup", "0", "--new-tokens", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="1"),
+                       cwd=ROOT)
+    assert r.returncode != 0 and "refusing" in (r.stdout + r.stderr)

@@ -120,8 +120,37 @@ def test_engine_fault_injection_and_health():
     assert r2.error is None and len(r2.ids) == 3
     r3 = e.run_turns([Turn("a", "x", sp)])[0]
     assert r3.error.kind == "device" and not e.healthy
+    # the next call probes the device, drops the (possibly stale) resident KV and serves again
     r4 = e.run_turns([Turn("a", "x", sp)])[0]
-    assert r4.error.kind == "device"
+    assert r4.error is None and e.healthy and len(r4.ids) == 3 and r4.metrics["reused_tokens"] == 0
+
+
+def test_engine_unrecoverable_device_and_flag_faults():
+    """A device the recovery probe cannot clear stays unhealthy; a device-side poll expiry (K9 /
+    persistent-kernel error flag) fails only that turn and drops its KV."""
+    from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+    sp = SamplingParams(temperature=0.0, max_new_tokens=3, ignore_eos=True, stop_on_consensus=False)
+    e = Engine(EngineConfig(model="tiny-llama", device="cpu", dtype="fp32", num_blocks=64,
+                            faults={1: "flag", 3: "device-dead"}))
+    assert e.run_turns([Turn("a", "hello", sp)])[0].error is None
+    r1 = e.run_turns([Turn("a", "hello", sp)])[0]
+    assert r1.error.kind == "device" and "poll expiry" in str(r1.error) and e.healthy
+    assert "a" not in e.kv.seqs                      # its KV was dropped, not trusted
+    assert e.run_turns([Turn("a", "hello", sp)])[0].error is None
+    r3 = e.run_turns([Turn("a", "hello", sp)])[0]
+    assert r3.error.kind == "device" and not e.healthy
+    assert e.run_turns([Turn("a", "hello", sp)])[0].error.kind == "device"
+
+
+def test_engine_reads_device_flags_after_decode(monkeypatch):
+    """The error flags of bounded device waits are read at the end-of-turn sync; a raised flag
+    fails the turn with kind 'device'."""
+    from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+    sp = SamplingParams(temperature=0.0, max_new_tokens=3, ignore_eos=True, stop_on_consensus=False)
+    e = Engine(EngineConfig(model="tiny-llama", device="cpu", dtype="fp32", num_blocks=64))
+    monkeypatch.setattr(e, "device_flag_errors", lambda: ["K9 one-shot all-reduce: a peer's flag never arrived"])
+    r = e.run_turns([Turn("a", "hello", sp)])[0]
+    assert r.error.kind == "device" and "K9" in str(r.error)
 
 
 def test_debug_paging_checks():

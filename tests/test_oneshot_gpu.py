@@ -18,5 +18,9 @@ def test_oneshot_allreduce_ranks_on_one_gpu(world):
     env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == world and all(o["checks"] == 6 + 15 for o in lines)
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"ranks"')]
+    assert len(recs) == 1, r.stdout[-2000:]
+    ranks = recs[0]["ranks"]
+    assert sorted(o["rank"] for o in ranks) == list(range(world))
+    assert all(o["checks"] == 6 + 15 for o in ranks)
+    assert next(o for o in ranks if o["rank"] == 0).get("expiry_flagged") is True

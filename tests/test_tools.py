@@ -8,7 +8,8 @@ from theroundtaible_amd.verify import resolve_verify_commands, validate_command
 
 
 @pytest.mark.parametrize("cmd", ["ls", "ls -la src | grep ts", "grep -rn 'a\\|b' src", "cat x 2>/dev/null",
-                                 "find . -name '*.py' 2>&1 | wc -l", "head -5 README.md | tail -2"])
+                                 "find . -name '*.py' 2>&1 | wc -l", "head -5 README.md | tail -2",
+                                 "grep -rn fprint src", "ls my-execdir-notes"])
 def test_allowed(cmd):
     assert validate_command(cmd) is None
 
@@ -27,6 +28,12 @@ def test_allowed(cmd):
     ("ls\r\nrm x", "forbidden pattern: newline (command separator)"),
     ("ls & rm x", "forbidden pattern: & (background / separator)"),
     ("cat a &", "forbidden pattern: & (background / separator)"),
+    ("find . -execdir rm {} +", "forbidden pattern: -exec*/-ok*"),
+    ("find . -okdir rm {} +", "forbidden pattern: -exec*/-ok*"),
+    ("find . -fprint out.txt", "forbidden pattern: -fprint*/-fls"),
+    ("find . -fprintf out.txt %p", "forbidden pattern: -fprint*/-fls"),
+    ("find . -fprint0 out", "forbidden pattern: -fprint*/-fls"),
+    ("find . -fls out.txt", "forbidden pattern: -fprint*/-fls"),
 ])
 def test_denied(cmd, why):
     assert validate_command(cmd) == why

@@ -28,7 +28,7 @@ import torch
 
 from .. import ops
 from ..consensus import parse_consensus
-from ..errors import AdapterError, EngineTimeout
+from ..errors import AdapterError, DeviceFlagError, EngineTimeout
 from ..models.config import ModelConfig, get_config
 from ..models.gpt2 import build_model
 from ..models.llama import AttnMeta
@@ -124,6 +124,9 @@ class Engine:
         self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}
         self._seg_cache: Dict[Tuple[str, str], List[int]] = {}
         self.healthy = True
+        self.max_recoveries = 3
+        self._recoveries = 0
+        self._dead = False
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0}
         self._calls = 0
         self.faults = dict(ecfg.faults)
@@ -280,7 +283,7 @@ class Engine:
         """Run one turn for each entry (distinct seq_keys), batched; per-turn errors are returned."""
         if not turns:
             return []
-        if not self.healthy:
+        if not self.healthy and not self._recover():
             err = AdapterError("engine", "engine unhealthy after a previous device error", kind="device")
             return [TurnOutput("", [], {}, err) for _ in turns]
         call = self._calls
@@ -294,6 +297,12 @@ class Engine:
             return [TurnOutput("", [], {}, AdapterError("engine", f"out of memory: {e}", kind="oom")) for _ in turns]
         except EngineTimeout as e:
             return [TurnOutput("", [], {}, e) for _ in turns]
+        except DeviceFlagError as e:
+            # a bounded device-side wait expired: this turn's tokens are wrong. Fail the turn,
+            # drop its KV (the knight re-prefills next turn); the engine itself stays usable.
+            for t in turns:
+                self.release(t.seq_key)
+            return [TurnOutput("", [], {}, AdapterError("engine", str(e), kind="device")) for _ in turns]
         except RuntimeError as e:
             msg = str(e)
             if "HIP" in msg or "hip" in msg or "CUDA" in msg or "device" in msg:
@@ -301,6 +310,28 @@ class Engine:
                 return [TurnOutput("", [], {}, AdapterError("engine", f"HIP error: {msg}", kind="device"))
                         for _ in turns]
             raise
+
+    def _recover(self) -> bool:
+        """Try to bring an unhealthy engine back: probe the device with a small
+        kernel; if it answers, drop every resident sequence and captured graph (their state may
+        be stale) and serve again — knights re-prefill from the transcript on their next turn.
+        At most ``max_recoveries`` attempts per engine; a dead device stays unhealthy."""
+        if self._recoveries >= self.max_recoveries or self._dead:
+            return False
+        self._recoveries += 1
+        try:
+            if self.on_gpu:
+                torch.cuda.synchronize(self.device)
+            x = torch.ones(64, 64, device=self.device, dtype=torch.float32)
+            if float((x @ x).sum().item()) != 64.0 ** 3:
+                return False
+        except RuntimeError:
+            return False
+        for key in list(self.kv.seqs):
+            self.kv.free_seq(key)
+        self.graphs.clear()
+        self.healthy = True
+        return True
 
     def _inject(self, call: int) -> None:
         f = self.faults.get(call)
@@ -312,6 +343,11 @@ class Engine:
             raise EngineTimeout("engine", f"injected timeout at call {call}")
         if f == "device":
             raise RuntimeError(f"HIP error: injected device fault at call {call}")
+        if f == "device-dead":      # a fault the recovery probe cannot clear
+            self._dead = True
+            raise RuntimeError(f"HIP error: injected unrecoverable device fault at call {call}")
+        if f == "flag":             # a bounded device-side wait expired (K9 / persistent kernel)
+            raise DeviceFlagError("engine", f"injected poll expiry at call {call}", kind="device")
         raise AdapterError("engine", f"injected failure at call {call}", kind="unknown")
 
     def check_paging(self, block_tables: torch.Tensor, slots: Sequence[int]) -> None:
@@ -343,6 +379,7 @@ class Engine:
         gen, decode_steps = self.decode(seqs, turns, first, deadline=t_start + min(t.timeout_s for t in turns))
         self._sync()
         t2 = time.perf_counter()
+        self.check_device_flags()
         outs = []
         for t, s, g, n, d in zip(turns, seqs, gen, reused, deltas):
             text = self.tokenizer.decode(g)
@@ -360,6 +397,30 @@ class Engine:
     def _sync(self):
         if self.on_gpu:
             torch.cuda.synchronize(self.device)
+
+    def device_flag_errors(self) -> List[str]:
+        """Read (and clear) the poll-expiry flags of the bounded device-side waits: the K9 one-shot
+        all-reduce's peer-flag wait and the persistent decode kernel's phase wait. A set flag means
+        the kernel proceeded on stale data, so the turn's output is wrong."""
+        msgs: List[str] = []
+        if not self.on_gpu:
+            return msgs
+        os_ = self.tp.oneshot
+        if os_ is not None and os_.error() > 0:
+            os_.clear_error()
+            msgs.append("K9 one-shot all-reduce: a peer's flag never arrived (poll expired)")
+        if getattr(self.model, "use_persistent", False):
+            for g in self.graphs.values():
+                if int(g.ws.err.item()):
+                    g.ws.err.zero_()
+                    msgs.append("persistent decode kernel: a phase wait expired")
+        return msgs
+
+    def check_device_flags(self) -> None:
+        msgs = self.device_flag_errors()
+        if self.tp.any_rank(bool(msgs)):     # every rank of a TP knight fails the turn together
+            raise DeviceFlagError("engine", "; ".join(msgs) or "a peer rank's device wait expired",
+                                  kind="device")
 
     # ---- continuous batching (serve.py): admit / step in chunks / retire ----------------------------
     @torch.no_grad()

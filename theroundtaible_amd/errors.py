@@ -86,6 +86,11 @@ class EngineTimeout(AdapterError):
         super().__init__(adapter, message, kind="timeout", **kw)
 
 
+class DeviceFlagError(AdapterError):
+    """A bounded device-side wait expired during a turn (K9 one-shot all-reduce or persistent
+    decode kernel error flag): the kernel proceeded on stale data, so the turn is failed."""
+
+
 _CLASSIFIERS = (
     # (kind, substrings, message template, hint)
     ("not_installed", ("enoent", "not found", "not recognized", "command not found", "no such model"),

@@ -44,6 +44,14 @@ class OneShotAllReduce:
         """1 if a peer's flag never arrived within the poll bound (that call's result is wrong)."""
         return int(self._nat.oneshot_error(self.id))
 
+    def clear_error(self) -> None:
+        self._nat.oneshot_clear_error(self.id)
+
+    def set_poll_limit(self, limit: int) -> None:
+        """Flag-wait bound in poll iterations (default ~2^26; fault-injection tests use a tiny one)."""
+        if self._nat.oneshot_set_poll_limit(self.id, int(limit)) != 0:
+            raise ValueError(f"bad poll limit {limit}")
+
     def close(self) -> None:
         if self.id is not None:
             self._nat.oneshot_destroy(self.id)

@@ -62,6 +62,16 @@ class TPInfo:
                 dist.all_reduce(x, group=self.group)
         return x
 
+    def any_rank(self, flag: bool) -> bool:
+        """True if ``flag`` is set on any rank of the group (host-side agreement, e.g. to fail a
+        turn on every rank of a TP knight when one rank's K9 flag wait expired)."""
+        if self.size == 1:
+            return flag
+        dev = "cpu" if self.backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return bool(int(t.item()))
+
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """Concatenate shards along the last dim (vocab-parallel logits)."""
         if self.size == 1:

@@ -22,6 +22,10 @@ FORBIDDEN_PATTERNS = [
     (re.compile(r"-exec\b"), r"-exec\b"),
     (re.compile(r"-delete\b"), r"-delete\b"),
     (re.compile(r"-ok\b"), r"-ok\b"),
+    # fix over the reference: find's other action / write primaries (-execdir, -okdir run programs;
+    # -fprint, -fprint0, -fprintf, -fls write files)
+    (re.compile(r"(?<![\w-])-(?:exec|ok)\w+"), r"-exec*/-ok*"),
+    (re.compile(r"(?<![\w-])-f(?:print\w*|ls)\b"), r"-fprint*/-fls"),
 ]
 FORBIDDEN_COMMANDS = frozenset({
     "rm", "mv", "cp", "chmod", "chown", "chgrp", "curl", "wget", "eval", "source", "node", "python",

@@ -98,8 +98,25 @@ def main() -> int:
                     dist.all_reduce(x)
                 torch.cuda.synchronize()
                 out[f"rccl_eager_us_n{n}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+    # forced poll expiry (fault injection): rank 0 calls alone with a tiny flag-wait bound, so its
+    # peers' flags never arrive; the error flag must be raised and must clear. The peers wait at
+    # the barrier meanwhile, their IPC buffers still mapped.
+    if rank == 0:
+        ar.set_poll_limit(2000)
+        x = data(rank, 8192, 999, dev)
+        ar(x)
+        torch.cuda.synchronize()
+        assert ar.error() == 1, "poll expiry not flagged"
+        ar.clear_error()
+        assert ar.error() == 0, "error flag did not clear"
+        out["expiry_flagged"] = True
+    dist.barrier()
     ar.close()
-    print(json.dumps(out), flush=True)
+    # one line from rank 0 holding every rank's record: per-rank prints to a shared pipe interleave
+    allout = [None] * world
+    dist.all_gather_object(allout, out)
+    if rank == 0:
+        os.write(1, (json.dumps({"ranks": allout}) + "\n").encode())
     dist.barrier()
     dist.destroy_process_group()
     return 0
