@@ -19,6 +19,16 @@
 // tile's loads in flight while the current tile computes. The 8 waves' softmax states
 // merge through LDS; the splits of one (sequence, kv head) are combined in the same launch
 // by whichever workgroup arrives last (sc1 write-through hand-off, see below).
+//
+// Shared-prefix groups (the knights of one table share the discussion's KV blocks, see
+// engine "shared" prompt layout): n consecutive sequences whose block tables start with the
+// same `shared` blocks form a group. Their n*G query heads fill the MFMA columns together
+// (3 knights x G=4 = 12 <= 16), so every shared K/V byte is read ONCE for the whole group.
+// Work item of workgroup (b, kv head, split y), member index i = b - first:
+//   virtual tiles = shared chunk (i*splits + y) of n*splits over [0, shared)   -> all columns
+//                 + private split y of [shared, ctx_b) of sequence b            -> b's columns
+// Each item leaves one partial (m, l, O) per column: member m collects n*splits partials
+// (slot i*splits + y from every workgroup of the group) and the last arrival combines them.
 #pragma once
 #include "common.h"
 
@@ -72,22 +82,26 @@ struct AttnArgs {
   const uint16_t* v_cache;     // [NB, Hkv, D, 32]
   const int* block_tables;     // [B, max_blocks]
   const int* ctx_lens;         // [B]
-  float* part_o;               // [B, Hq, splits, D]
-  float* part_ml;              // [B, Hq, splits, 4]
+  float* part_o;               // [B, Hq, slot_stride, D]
+  float* part_ml;              // [B, Hq, slot_stride, 4]
   int* counters;               // [B * Hkv], zero between launches
   int Hq, Hkv, max_blocks;
   float scale_log2;
   int num_splits;
+  // shared-prefix groups, nullptr = every sequence on its own: per sequence {first sequence of
+  // its group, group size n, shared full blocks}. n * G <= 16 (host-checked).
+  const int* groups = nullptr;
+  int slot_stride = 0;         // partial slots per (sequence, head) >= n * num_splits; 0 = num_splits
 };
 
-// GM = max query heads per kv head the LDS is sized for (G <= GM). GM = 4 (Llama-3-8B,
-// Mistral-7B) keeps the workgroup at ~26 KB so two fit a CU: 16 waves streaming K/V per CU.
+// GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
+// no groups) keeps the workgroup at ~26 KB so two fit a CU: 16 waves streaming K/V per CU.
 template <int D, int GM = 16>
 struct AttnSmem {
   float s_m[NW][16];
   float s_l[NW][16];
   float s_o[NW][GM][D + 4];
-  int s_last;
+  int s_last;                  // bit m: this workgroup combines member m
 };
 
 RT_DEVICE void store_bf16x4(uint16_t* dst, float a, float b_, float c, float d, bool sc1) {
@@ -101,8 +115,8 @@ RT_DEVICE void store_bf16x4(uint16_t* dst, float a, float b_, float c, float d, 
     *reinterpret_cast<uint2*>(dst) = pk;
 }
 
-// One (sequence, kv head, key split) work item. Returns true when this workgroup wrote the
-// item's final output rows (no split, or the last-arriving split that combined them).
+// One (sequence, kv head, key split) work item. Returns true when this workgroup wrote final
+// output rows (no split, or the last-arriving split that combined them).
 template <int D, bool SC1, int GM = 16>
 RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& S) {
   uint16_t* __restrict__ out = P.out;
@@ -123,19 +137,39 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
 
   const int b = bh / Hkv, hk = bh - (bh / Hkv) * Hkv;
   const int G = Hq / Hkv;
+  int b0 = b, n = 1, sh = 0;
+  if (P.groups != nullptr) {
+    b0 = P.groups[3 * b];
+    n = P.groups[3 * b + 1];
+    sh = P.groups[3 * b + 2];
+    if (n < 1 || n * G > GM || b0 < 0 || b < b0 || b - b0 >= n || sh < 0) {  // malformed: run alone
+      b0 = b;
+      n = 1;
+      sh = 0;
+    }
+  }
+  const int mi = b - b0, ncol = n * G;
+  const int nslots = n * num_splits, slot = mi * num_splits + split;
+  const int stride = P.slot_stride > 0 ? P.slot_stride : num_splits;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
+  const int rseq = r / G, rhead = r - (r / G) * G;  // column r -> (member, head within the kv group)
 
   const int ctx = ctx_lens[b];
   const int ntiles = (ctx + BS - 1) / BS;
-  const int tps = (ntiles + num_splits - 1) / num_splits;
-  const int t_begin = split * tps;
-  const int t_end = min(ntiles, t_begin + tps);
+  // this workgroup's shared chunk (all members' columns) then its private split (own columns)
+  const int sh_per = (sh + nslots - 1) / nslots;
+  const int sh_b = min(sh, slot * sh_per), sh_e = min(sh, sh_b + sh_per);
+  const int npr = max(0, ntiles - sh);
+  const int pr_per = (npr + num_splits - 1) / num_splits;
+  const int pr_b = sh + min(npr, split * pr_per), pr_e = sh + min(npr, split * pr_per + pr_per);
+  const int nsh = sh_e - sh_b, nv = nsh + (pr_e - pr_b);
 
-  // Q^T fragments: column r = query head hk*G + r (zero for r >= G)
+  // Q^T fragments: column r = query head hk*G + rhead of member rseq (zero for r >= ncol)
   short8 qf[D / 32];
   {
-    const uint16_t* qr = q + ((size_t)b * Hq + hk * G + (r < G ? r : 0)) * D + (D / 4) * g;
+    const bool live = r < ncol;
+    const uint16_t* qr = q + ((size_t)(b0 + (live ? rseq : 0)) * Hq + hk * G + (live ? rhead : 0)) * D + (D / 4) * g;
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) {
       short8 v;
@@ -143,7 +177,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
         v = __builtin_bit_cast(short8, rt::sc1_load4(rt::buf_rsrc(q), (int)((qr - q) + 8 * c) * 2));
       else
         v = *reinterpret_cast<const short8*>(qr + 8 * c);
-      if (r >= G) v = short8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (!live) v = short8{0, 0, 0, 0, 0, 0, 0, 0};
       qf[c] = v;
     }
   }
@@ -155,26 +189,31 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   float lsum = 0.f;     // lane-partial running sum of column r
 
   const size_t blk_stride = (size_t)Hkv * BS * D;
+  // virtual tile v -> block-table entry: shared chunk tiles come from the group's first row
+  auto bt_entry = [&](int v) -> int {
+    return v < nsh ? block_tables[(size_t)b0 * max_blocks + sh_b + v]
+                   : block_tables[(size_t)b * max_blocks + pr_b + (v - nsh)];
+  };
   Tile<D> cur, nxt;
-  int t = t_begin + wid;
-  // Block ids of this wave's tiles (t_begin + wid + NW*j) are fetched one per lane up front, in
+  int v = wid;
+  // Block ids of this wave's tiles (v = wid + NW*j) are fetched one per lane up front, in
   // flight with Q, and read out with readlane: no dependent scalar load inside the loop (refilled
   // every 64 tiles, i.e. only past ~164K keys at 10 splits). B=3, ctx 1500: 12.2 -> 11.2 us.
   int blk_lane = 0;
   {
-    const int tt = t + NW * lane;
-    if (tt < t_end) blk_lane = block_tables[(size_t)b * max_blocks + tt];
+    const int tt = v + NW * lane;
+    if (tt < nv) blk_lane = bt_entry(tt);
   }
-  if (t < t_end) {
+  if (v < nv) {
     const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, 0) * blk_stride + (size_t)hk * BS * D;
     load_tile<D, SC1>(cur, k_cache + base, v_cache + base, r, g);
   }
-  for (int j = 1; t < t_end; t += NW, ++j) {
-    const int tn = t + NW;
-    if (tn < t_end) {  // keep the next tile's loads in flight during this tile's math
+  for (int j = 1; v < nv; v += NW, ++j) {
+    const int vn = v + NW;
+    if (vn < nv) {  // keep the next tile's loads in flight during this tile's math
       if ((j & 63) == 0) {
-        const int tt = tn + NW * lane;
-        blk_lane = tt < t_end ? block_tables[(size_t)b * max_blocks + tt] : 0;
+        const int tt = vn + NW * lane;
+        blk_lane = tt < nv ? bt_entry(tt) : 0;
       }
       const size_t base =
           (size_t)__builtin_amdgcn_readlane(blk_lane, j & 63) * blk_stride + (size_t)hk * BS * D;
@@ -190,22 +229,27 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
         s[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, cur.k[h][c]),
                                                        __builtin_bit_cast(bf16x8, qf[c]), s[h], 0, 0, 0);
     }
-    // ---- online softmax down column r: lane holds keys 8g + 4h + i ----
+    // ---- online softmax down column r: lane holds keys 8g + 4h + i. Shared tiles are live
+    // for every member's columns (full blocks); private tiles only for b's own, below ctx. ----
+    const bool shared_t = v < nsh;
+    const int t = shared_t ? sh_b + v : pr_b + (v - nsh);
+    const int klim = shared_t ? (r < ncol ? 0x7fffffff : 0) : (rseq == mi && r < ncol ? ctx : 0);
     const int key0 = t * BS + 8 * g;
     float tmax = -INFINITY;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = s[h][i] * scale_log2;
-        v = key0 + 4 * h + i < ctx ? v : -INFINITY;
-        s[h][i] = v;
-        tmax = fmaxf(tmax, v);
+        float x = s[h][i] * scale_log2;
+        x = key0 + 4 * h + i < klim ? x : -INFINITY;
+        s[h][i] = x;
+        tmax = fmaxf(tmax, x);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(m, tmax);
-    const float alpha = rt::fast_exp2(m - mnew);  // m=-inf first time -> 0
+    const float mref = mnew == -INFINITY ? 0.f : mnew;  // column with no live key yet: alpha = p = 0
+    const float alpha = rt::fast_exp2(m - mref);         // m=-inf first time -> 0
     m = mnew;
     float psum = 0.f;
     rt::u32x4 pw;
@@ -213,7 +257,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float p0 = rt::fast_exp2(s[h][2 * i] - mnew), p1 = rt::fast_exp2(s[h][2 * i + 1] - mnew);
+        const float p0 = rt::fast_exp2(s[h][2 * i] - mref), p1 = rt::fast_exp2(s[h][2 * i + 1] - mref);
         psum += p0 + p1;
         pw[2 * h + i] = rt::pack2(p0, p1);
       }
@@ -238,7 +282,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
 
-  // ---- merge the waves through LDS (only the G live query rows) ----
+  // ---- merge the waves through LDS (only the ncol live query columns) ----
   if (g == 0) {
     s_m[wid][r] = m;
     s_l[wid][r] = lsum;
@@ -247,14 +291,17 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   for (int e = 0; e < D / 16; ++e)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (4 * g + i < G) s_o[wid][4 * g + i][16 * e + r] = oacc[e][i];
+      if (4 * g + i < ncol) s_o[wid][4 * g + i][16 * e + r] = oacc[e][i];
   __syncthreads();
 
-  const size_t bh_q0 = (size_t)b * Hq + hk * G;  // first query head of this workgroup
-  const auto po_rsrc = rt::buf_rsrc(part_o + bh_q0 * num_splits * D);
-  const auto pml_rsrc = rt::buf_rsrc(part_ml + bh_q0 * num_splits * 4);
-  for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
+  // (sequence, head) row of column c relative to the group's first row q0
+  const size_t q0 = (size_t)b0 * Hq + hk * G;
+  auto col_row = [&](int c) -> int { return (c / G) * Hq + (c - (c / G) * G); };
+  const auto po_rsrc = rt::buf_rsrc(part_o + q0 * stride * D);
+  const auto pml_rsrc = rt::buf_rsrc(part_ml + q0 * stride * 4);
+  for (int it = threadIdx.x; it < ncol * (D / 4); it += blockDim.x) {
     const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
+    const int row = col_row(qi);
     float M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][qi]);
@@ -269,56 +316,64 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
         O += f * ow;
       }
     }
-    if (num_splits == 1) {
+    if (nslots == 1) {
       const float inv = L > 0.f ? 1.f / L : 0.f;
-      store_bf16x4(out + (bh_q0 + qi) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
+      store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
     } else {
       // partials leave as 16-B write-through (sc1) stores: the combining workgroup, possibly
       // on another XCD, reads them with sc1 loads and no L2 writeback/invalidate is needed
-      rt::sc1_store4(po_rsrc, ((qi * num_splits + split) * D + d0) * 4, O);
-      if (d0 == 0) rt::sc1_store4(pml_rsrc, (qi * num_splits + split) * 16, float4_{M, L, 0.f, 0.f});
+      rt::sc1_store4(po_rsrc, ((row * stride + slot) * D + d0) * 4, O);
+      if (d0 == 0) rt::sc1_store4(pml_rsrc, (row * stride + slot) * 16, float4_{M, L, 0.f, 0.f});
     }
   }
-  if (num_splits == 1) {
+  if (nslots == 1) {
     __syncthreads();  // LDS is reused by the caller's next item
     return true;
   }
 
   // ---- split-KV combine inside the launch (MI355X_MICROARCH "Valid forms", row 1): every
   // partial is stored sc1 and drained (vmcnt(0)) by each storing wave before the barrier;
-  // ONE lane then bumps the (sequence, kv head) arrival counter; the workgroup whose add
-  // returns num_splits-1 combines, reading every partial with sc1 loads, and re-arms the
-  // counter for the next launch (hipGraph replays need no memset node). A release/acquire
-  // fence pair instead would write back / invalidate caches per workgroup (measured 2x slower).
+  // one lane per member then bumps that member's (sequence, kv head) arrival counter; the
+  // workgroup whose add returns nslots-1 combines the member, reading every partial with sc1
+  // loads, and re-arms the counter for the next launch (hipGraph replays need no memset node).
+  // A release/acquire fence pair instead would write back / invalidate caches per workgroup
+  // (measured 2x slower).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) s_last = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == num_splits - 1;
-    if (s_last) __hip_atomic_store(counters + bh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)threadIdx.x < n) {
+    int* ctr = counters + (size_t)(b0 + threadIdx.x) * Hkv + hk;
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == nslots - 1) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicOr(&s_last, 1 << threadIdx.x);
+    }
   }
   __syncthreads();
-  if (!s_last) return false;
+  const int mask = s_last;
+  if (mask == 0) return false;
 
-  // latency-bound: each output thread issues the (m, l) AND partial-O loads of up to 16 splits
-  // at once (one round trip for <= 16 splits, no LDS weight pass) and merges them online
-  for (int it = threadIdx.x; it < G * (D / 4); it += blockDim.x) {
+  // latency-bound: each output thread issues the (m, l) AND partial-O loads of up to 16 slots
+  // at once (one round trip for <= 16 slots, no LDS weight pass) and merges them online
+  for (int it = threadIdx.x; it < ncol * (D / 4); it += blockDim.x) {
     const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
+    if (!((mask >> (qi / G)) & 1)) continue;
+    const int row = col_row(qi);
     float4_ O = {0.f, 0.f, 0.f, 0.f};
     float Mr = -INFINITY, Lr = 0.f;
-    for (int s0 = 0; s0 < num_splits; s0 += 16) {
-      float4_ v[16], ml[16];
+    for (int s0 = 0; s0 < nslots; s0 += 16) {
+      float4_ vv[16], ml[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const bool ok = s0 + j < num_splits;
-        ml[j] = ok ? rt::sc1_load4(pml_rsrc, (qi * num_splits + s0 + j) * 16) : float4_{-INFINITY, 0.f, 0.f, 0.f};
-        v[j] = ok ? rt::sc1_load4(po_rsrc, ((qi * num_splits + s0 + j) * D + d0) * 4) : float4_{0.f, 0.f, 0.f, 0.f};
+        const bool ok = s0 + j < nslots;
+        ml[j] = ok ? rt::sc1_load4(pml_rsrc, (row * stride + s0 + j) * 16) : float4_{-INFINITY, 0.f, 0.f, 0.f};
+        vv[j] = ok ? rt::sc1_load4(po_rsrc, ((row * stride + s0 + j) * D + d0) * 4) : float4_{0.f, 0.f, 0.f, 0.f};
       }
       float Mc = Mr;
 #pragma unroll
       for (int j = 0; j < 16; ++j)
         if (ml[j][1] > 0.f) Mc = fmaxf(Mc, ml[j][0]);
-      if (Mc == -INFINITY) continue;                 // every split of this chunk was empty
+      if (Mc == -INFINITY) continue;                 // every slot of this chunk was empty
       const float a = Mr == -INFINITY ? 0.f : exp2f(Mr - Mc);
       O *= a;
       Lr *= a;
@@ -326,14 +381,14 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
       for (int j = 0; j < 16; ++j) {
         if (ml[j][1] > 0.f) {
           const float f = exp2f(ml[j][0] - Mc);
-          O += f * v[j];
+          O += f * vv[j];
           Lr += f * ml[j][1];
         }
       }
       Mr = Mc;
     }
     const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
-    store_bf16x4(out + (bh_q0 + qi) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
+    store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
   }
   __syncthreads();
   return true;

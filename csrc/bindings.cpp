@@ -15,7 +15,8 @@ void launch_silu_mul(void* out, const void* x, int rows, int I, hipStream_t stre
 void launch_gelu(void* out, const void* x, int64_t n, hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
-                        int D, int max_blocks, float scale, int num_splits, hipStream_t stream);
+                        int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
+                        hipStream_t stream);
 int prefill_rows_per_tile(int G, int D);
 int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                    const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv, int D,
@@ -146,7 +147,8 @@ void rope_and_cache(torch::Tensor q_out, torch::Tensor qkv, torch::Tensor positi
 
 void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
                             torch::Tensor block_tables, torch::Tensor ctx_lens, double scale, int64_t num_splits,
-                            torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor counters) {
+                            torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor counters,
+                            c10::optional<torch::Tensor> groups, int64_t slot_stride) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
@@ -156,9 +158,18 @@ void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_
   check_type(block_tables, torch::kInt32, "block_tables");
   check_type(ctx_lens, torch::kInt32, "ctx_lens");
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && ctx_lens.numel() >= B, "metadata shape");
+  const int* gp = nullptr;
+  int64_t stride = num_splits;
+  if (groups.has_value() && groups->defined()) {
+    check_type(*groups, torch::kInt32, "groups");
+    TORCH_CHECK(groups->numel() >= 3 * B, "groups must be [B, 3] int32");
+    TORCH_CHECK(slot_stride >= num_splits, "slot_stride must hold n * num_splits partials");
+    gp = groups->data_ptr<int>();
+    stride = slot_stride;
+  }
   check_type(part_o, torch::kFloat32, "partial_o");
   check_type(part_ml, torch::kFloat32, "partial_ml");
-  TORCH_CHECK(num_splits >= 1 && part_o.numel() >= B * Hq * num_splits * D && part_ml.numel() >= B * Hq * num_splits * 4,
+  TORCH_CHECK(num_splits >= 1 && part_o.numel() >= B * Hq * stride * D && part_ml.numel() >= B * Hq * stride * 4,
               "split workspace too small");
   check_type(counters, torch::kInt32, "counters");
   TORCH_CHECK(counters.numel() >= B * k_cache.size(1), "split counters too small");
@@ -166,7 +177,8 @@ void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_
                                      block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), part_o.data_ptr<float>(),
                                      part_ml.data_ptr<float>(), counters.data_ptr<int>(), (int)B, (int)Hq,
                                      (int)k_cache.size(1), (int)D,
-                                     (int)block_tables.size(1), (float)scale, (int)num_splits, cur_stream());
+                                     (int)block_tables.size(1), (float)scale, (int)num_splits, gp, (int)stride,
+                                     cur_stream());
   TORCH_CHECK(rc == 0, "paged_attention_decode: unsupported configuration (rc=", rc, ")");
 }
 
@@ -509,7 +521,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("layer_norm", &layer_norm);
   m.def("fused_add_layer_norm", &fused_add_layer_norm);
   m.def("rope_and_cache", &rope_and_cache);
-  m.def("paged_attention_decode", &paged_attention_decode);
+  m.def("paged_attention_decode", &paged_attention_decode, py::arg("out"), py::arg("q"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("scale"), py::arg("num_splits"),
+        py::arg("part_o"), py::arg("part_ml"), py::arg("counters"), py::arg("groups") = py::none(),
+        py::arg("slot_stride") = 0);
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile, py::arg("G"), py::arg("D") = 128);
   m.def("prefill_attention", &prefill_attention);
   m.def("silu_and_mul", &silu_and_mul);

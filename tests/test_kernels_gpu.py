@@ -108,6 +108,56 @@ def test_paged_decode(hq, hkv, d, splits):
     assert int(ws.counters.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64)])
+@pytest.mark.parametrize("splits", [1, 3, 10])
+@pytest.mark.parametrize("layout", ["table3", "mixed"])
+def test_paged_decode_shared_prefix_groups(hq, hkv, d, splits, layout):
+    """Knights sharing a KV prefix (same leading block ids) decode it once per group: the
+    grouped kernel must equal the fp32 oracle of each sequence alone, for groups of 1..4, a
+    shared prefix longer / shorter than the private tails, and groups wider than 16 columns
+    (cut into sub-groups)."""
+    G = hq // hkv
+    if layout == "table3":      # one table: 3 knights, 1900-token shared prefix + private tails
+        spec = [("A", 1900 // 32, [1900 + 7, 1900 + 300, 1900 + 33])]
+    else:                        # two groups of different size + a lone sequence
+        spec = [("A", 40, [40 * 32 + 1, 40 * 32 + 500]), (None, 0, [700]), ("B", 3, [3 * 32 + 5, 96 + 64, 96 + 1, 96 + 900])]
+    g = torch.Generator().manual_seed(5)
+    lens, group_of, shared = [], [], []
+    for label, sh, ls in spec:
+        for l in ls:
+            lens.append(l)
+            group_of.append(label)
+            shared.append(sh)
+    B = len(lens)
+    nb = sum(sh for _, sh, _ in spec) + sum((l + 31) // 32 for l in lens) + 4
+    kc, vc = make_cache(nb, hkv, d, seed=21)
+    perm = torch.randperm(nb, generator=g).tolist()
+    maxb = max((l + 31) // 32 for l in lens)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    nxt = 0
+    b = 0
+    for label, sh, ls in spec:
+        common = perm[nxt:nxt + sh]
+        nxt += sh
+        for l in ls:
+            own = (l + 31) // 32 - sh
+            bt[b, :sh + own] = torch.tensor(common + perm[nxt:nxt + own], dtype=torch.int32)
+            nxt += own
+            b += 1
+    groups, nmax = ops.decode_groups(group_of, shared, G)
+    assert nmax <= max(1, 16 // G)
+    q = bf(B, hq, d, seed=22)
+    cl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(d)
+    ws = ops.DecodeWorkspace(B, hq, d, splits, DEV, max_group=16 // G)
+    out = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws, groups=groups.to(DEV))
+    exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, cl, scale)
+    close(out, exp.to(DEV), 0.02, 0.02)
+    out2 = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws, groups=groups.to(DEV))
+    assert torch.equal(out, out2)
+    assert int(ws.counters.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("splits", [1, 2, 5])
 def test_paged_decode_long_context(splits):
     """Contexts of 20K / 33K keys: at splits=1 a wave walks > 64 tiles, exercising the per-lane

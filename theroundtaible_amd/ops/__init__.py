@@ -95,13 +95,23 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional
     return ref.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping, n_heads, n_kv_heads, head_dim)
 
 
-class DecodeWorkspace:
-    """Split-KV scratch for paged decode (static: allocated once, reused inside hipGraphs)."""
+MAX_GROUP_COLS = 16      # MFMA columns a shared-prefix group's query heads may fill (n * G)
 
-    def __init__(self, max_batch: int, n_heads: int, head_dim: int, max_splits: int, device):
+
+class DecodeWorkspace:
+    """Split-KV scratch for paged decode (static: allocated once, reused inside hipGraphs).
+
+    ``max_group``: largest shared-prefix group (knights reading the same KV prefix, see
+    :func:`decode_groups`); each (sequence, head) then receives up to ``max_group * max_splits``
+    partials, so the partial buffers are strided by ``slot_stride`` = that product."""
+
+    def __init__(self, max_batch: int, n_heads: int, head_dim: int, max_splits: int, device, max_group: int = 1):
         self.max_splits = max_splits
-        self.partial_o = torch.empty(max_batch * n_heads * max_splits * head_dim, dtype=torch.float32, device=device)
-        self.partial_ml = torch.empty(max_batch * n_heads * max_splits * 4, dtype=torch.float32, device=device)
+        self.max_group = max(1, max_group)
+        self.slot_stride = max_splits * self.max_group
+        self.partial_o = torch.empty(max_batch * n_heads * self.slot_stride * head_dim, dtype=torch.float32,
+                                     device=device)
+        self.partial_ml = torch.empty(max_batch * n_heads * self.slot_stride * 4, dtype=torch.float32, device=device)
         # per-(sequence, kv head) split arrival counters; the kernel re-arms them to 0 itself.
         # Sized by n_heads (>= n_kv_heads) so one workspace serves every GQA ratio.
         self.counters = torch.zeros(max_batch * n_heads, dtype=torch.int32, device=device)
@@ -122,18 +132,53 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: i
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
 
+def decode_groups(group_of: list, shared_blocks: list, G: int) -> Tuple[torch.Tensor, int]:
+    """Per-sequence ``[B, 3]`` int32 ``{first sequence, group size n, shared full blocks}`` for
+    the shared-prefix decode kernel, from a group label per sequence (members must be
+    consecutive; ``None`` = alone) and each group's shared block count. Groups wider than the
+    MFMA columns (n * G > 16) are cut into consecutive sub-groups of the same prefix. Returns
+    the table and the largest n."""
+    B = len(group_of)
+    out = torch.zeros(B, 3, dtype=torch.int32)
+    cap = max(1, MAX_GROUP_COLS // max(1, G))
+    b, nmax = 0, 1
+    while b < B:
+        e = b + 1
+        if group_of[b] is not None:
+            while e < B and group_of[e] == group_of[b] and e - b < cap:
+                e += 1
+        n = e - b
+        sh = int(shared_blocks[b]) if n > 1 else 0
+        if sh <= 0:
+            n, e, sh = 1, b + 1, 0
+        for i in range(b, e):
+            out[i] = torch.tensor([b, n, sh], dtype=torch.int32)
+        nmax = max(nmax, n)
+        b = e
+    return out, nmax
+
+
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, ctx_lens: torch.Tensor, scale: float,
                            num_splits: int = 1, workspace: Optional[DecodeWorkspace] = None,
-                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None, groups: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``groups`` (optional, device ``[B, 3]`` int32 from :func:`decode_groups`): sequences whose
+    block tables share leading blocks decode those keys once for the whole group. The result is
+    identical to decoding every sequence alone (the fp32 oracle ignores ``groups``)."""
     if _use_native(q):
         if out is None:
             out = torch.empty_like(q)
+        G = q.shape[1] // k_cache.shape[1]
         if workspace is None:
-            workspace = DecodeWorkspace(q.shape[0], q.shape[1], q.shape[2], max(1, num_splits), q.device)
+            workspace = DecodeWorkspace(q.shape[0], q.shape[1], q.shape[2], max(1, num_splits), q.device,
+                                        max_group=MAX_GROUP_COLS // G if groups is not None else 1)
+        if groups is not None and (workspace.max_group < MAX_GROUP_COLS // G or workspace.max_splits < num_splits):
+            raise ValueError(f"decode workspace too small for shared-prefix groups (max_group "
+                             f"{workspace.max_group} < {MAX_GROUP_COLS // G})")
         native().paged_attention_decode(out, q, k_cache, v_cache, block_tables, ctx_lens, scale,
                                         int(num_splits), workspace.partial_o, workspace.partial_ml,
-                                        workspace.counters)
+                                        workspace.counters, groups,
+                                        workspace.slot_stride if groups is not None else 0)
         return out
     return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
 
