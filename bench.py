@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--round-mode", default="parallel", choices=["parallel", "sequential"],
                    help="parallel: all knights of a round decode as one batch; sequential: reference "
                         "semantics (speakers in order, each sees the earlier speakers of the round)")
-    p.add_argument("--layout", default="append", choices=["append", "reference"])
+    p.add_argument("--layout", default="append", choices=["append", "shared", "reference"],
+                   help="prompt layout; 'shared' keeps one copy of a table's common transcript KV per GPU")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--kv-fraction", type=float, default=0.85,
                    help="fraction of free HBM for the KV pool (lower it when ranks share a GPU)")

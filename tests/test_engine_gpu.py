@@ -115,3 +115,77 @@ def test_debug_paging_guard_in_decode_graph():
     with pytest.raises(AssertionError, match="position"):
         g.check_guard()
     assert int(g.guard_err.item()) == 0           # cleared after reporting
+
+
+def _shared_turns(transcript, rnd, keyed=True, n_new=16):
+    from theroundtaible_amd.prompt import TurnContext, build_turn_prompt_shared
+    from theroundtaible_amd.types import KnightConfig
+    ks = [KnightConfig(name=n, adapter="local-llm", capabilities=["x"], priority=i) for i, n in
+          enumerate(["Claude", "Gemini", "GPT"])]
+    ctx = TurnContext(topic="Gedeelde KV-blokken voor alle knights van een tafel. " * 40)
+    out = []
+    for k in ks:
+        p = build_turn_prompt_shared(k, ks, ctx, transcript, rnd, shared_key="t@table")
+        if not keyed:
+            p.shared_key = None
+        out.append(Turn(k.name, p, SamplingParams(temperature=0.0, max_new_tokens=n_new, ignore_eos=True,
+                                                  stop_on_consensus=False)))
+    return ks, out
+
+
+@pytest.mark.parametrize("model", ["tiny-llama-128", "llama3-8b-2l"])
+def test_shared_prefix_grouped_decode_matches_private(model):
+    """One decode step over resident KV whose prefix blocks are shared by 3 knights: grouped K3
+    (shared blocks read once for the group) vs every sequence alone — same logits."""
+    from theroundtaible_amd.models.llama import AttnMeta
+    from theroundtaible_amd.prompt import Segment
+    kw = {"model_overrides": {"n_layers": 2}} if model == "llama3-8b-2l" else {}
+    e = eng("llama3-8b" if model == "llama3-8b-2l" else model, num_blocks=2048, **kw)
+    ks, turns = _shared_turns([], 1)
+    outs = e.run_turns(turns)
+    tr = []
+    for k, o in zip(ks, outs):
+        assert o.error is None and o.metrics["shared_tokens"] > 0
+        tr += [Segment(f"\n\n### {k.name} (Ronde 1):\n"), Segment(o.text, o.ids, e.tokenizer.family)]
+    ks, turns = _shared_turns(tr, 2)
+    outs = e.run_turns(turns)
+    assert all(o.error is None for o in outs)
+    seqs = [e.kv.seqs[k.name] for k in ks]
+    sq = e.kv.seqs[e.shared_seq_key("t@table")]
+    from theroundtaible_amd.engine.engine import common_blocks
+    nsh = min(common_blocks(s, sq) for s in seqs)
+    assert nsh >= 4
+    B = len(seqs)
+    dev = e.device
+    bt = torch.zeros(B, max(len(s.blocks) for s in seqs) + 1, dtype=torch.int32)
+    for j, s in enumerate(seqs):
+        e.kv.ensure_capacity(s, s.length + 1)
+        bt[j, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+    pos = [s.length for s in seqs]
+    slots = [s.blocks[p // 32] * 32 + p % 32 for s, p in zip(seqs, pos)]
+    splits = ops.decode_splits(3, e.model.n_kv_heads)
+    G = e.model.n_heads // e.model.n_kv_heads
+    ids = torch.tensor([o.ids[-1] for o in outs], dtype=torch.int64, device=dev)
+    res = []
+    for grouped in (False, True):
+        gt = e.group_table((["t"] * B, [nsh] * B), B).to(dev) if grouped else None
+        ws = ops.DecodeWorkspace(B, e.model.n_heads, e.cfg.head_dim, splits, dev,
+                                 max_group=16 // G if grouped else 1)
+        meta = AttnMeta(kind="decode", slot_mapping=torch.tensor(slots, dtype=torch.int64, device=dev),
+                        block_tables=bt.to(dev), ctx_lens=torch.tensor([p + 1 for p in pos], dtype=torch.int32,
+                                                                      device=dev),
+                        num_splits=splits, workspace=ws, groups=gt)
+        res.append(e.model.forward(ids, torch.tensor(pos, dtype=torch.int64, device=dev), e.kv, meta).float())
+    cos = torch.nn.functional.cosine_similarity(res[0], res[1], dim=-1)
+    assert float(cos.min()) > 0.999, cos
+
+
+def test_shared_layout_graph_equals_eager():
+    """Grouped decode in the captured hipGraph and eagerly: identical greedy tokens."""
+    a = eng(use_graphs=True)
+    b = eng(use_graphs=False)
+    _, ta = _shared_turns([], 1)
+    _, tb = _shared_turns([], 1)
+    oa, ob = a.run_turns(ta), b.run_turns(tb)
+    assert [o.ids for o in oa] == [o.ids for o in ob]
+    assert all(o.metrics["shared_tokens"] > 0 for o in oa)

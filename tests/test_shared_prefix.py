@@ -1,0 +1,71 @@
+"""``shared`` prompt layout: a table's common prefix (header + context + transcript) is
+prefilled once into a shared sequence whose KV blocks every knight references (refcounted),
+and grouped decode reads them once. Same tokens as private per-knight caches, fewer blocks."""
+import torch
+
+from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+from theroundtaible_amd.engine.engine import group_order
+from theroundtaible_amd.prompt import Prompt, Segment, build_turn_prompt_shared, TurnContext
+from theroundtaible_amd.types import KnightConfig
+
+KNIGHTS = [KnightConfig(name=n, adapter=f"local-llm-{n.lower()}", capabilities=["x"], priority=i + 1)
+           for i, n in enumerate(["Claude", "Gemini", "GPT"])]
+
+
+def _engine():
+    return Engine(EngineConfig(model="tiny-llama", device="cpu", dtype="fp32", num_blocks=512, weights="random:3"))
+
+
+def _turns(transcript, rnd, key):
+    ctx = TurnContext(topic="Gedeelde KV voor de ronde tafel " * 8)
+    out = []
+    for k in KNIGHTS:
+        p = build_turn_prompt_shared(k, KNIGHTS, ctx, transcript, rnd, shared_key="t0@table")
+        if key is None:
+            p.shared_key = None
+        out.append(Turn(k.name, p, SamplingParams(temperature=0.0, max_new_tokens=12, ignore_eos=True,
+                                                  stop_on_consensus=False)))
+    return out
+
+
+def test_shared_layout_same_tokens_fewer_blocks():
+    shared, private = _engine(), _engine()
+    tr_s, tr_p = [], []
+    for rnd in (1, 2, 3):
+        a = shared.run_turns(_turns(tr_s, rnd, "t0"))
+        b = private.run_turns(_turns(tr_p, rnd, None))
+        for x, y in zip(a, b):
+            assert x.error is None and y.error is None
+            assert x.ids == y.ids
+        for k, x in zip(KNIGHTS, a):
+            tr_s += [Segment(f"\n\n### {k.name} (Ronde {rnd}):\n"), Segment(x.text, x.ids, shared.tokenizer.family)]
+        for k, y in zip(KNIGHTS, b):
+            tr_p += [Segment(f"\n\n### {k.name} (Ronde {rnd}):\n"), Segment(y.text, y.ids, private.tokenizer.family)]
+        assert a[0].metrics["shared_tokens"] > 0 and b[0].metrics["shared_tokens"] == 0
+    used_s = shared.kv.num_blocks - shared.kv.alloc.num_free
+    used_p = private.kv.num_blocks - private.kv.alloc.num_free
+    assert used_s < 0.6 * used_p, (used_s, used_p)
+    # per round, the shared prefill is the new transcript once plus three short suffixes
+    assert sum(x.metrics["prefill_tokens"] for x in a) < sum(y.metrics["prefill_tokens"] for y in b)
+
+
+def test_attach_keeps_blocks_refcounted():
+    e = _engine()
+    e.run_turns(_turns([], 1, "t0"))
+    sq = e.kv.seqs[e.shared_seq_key("t0@table")]
+    full = sq.length // e.kv.block_size
+    assert full > 0
+    for k in KNIGHTS:
+        s = e.kv.seqs[k.name]
+        assert s.blocks[:full] == sq.blocks[:full]
+    for b in sq.blocks[:full]:
+        assert e.kv.alloc.ref[b] == 1 + len(KNIGHTS)
+    # releasing the knights leaves the shared sequence intact
+    for k in KNIGHTS:
+        e.release(k.name)
+    assert all(e.kv.alloc.ref[b] == 1 for b in sq.blocks[:full])
+
+
+def test_group_order_makes_members_adjacent():
+    assert group_order(["a", None, "b", "a", "b", None]) == [0, 3, 1, 2, 4, 5]
+    assert group_order([None, None]) == [0, 1]

@@ -98,8 +98,8 @@ def validate_config(cfg: Dict[str, Any]) -> None:
         raise ConfigError("rules.timeout_per_turn_seconds must be a positive number.")
     if rules.get("round_mode", "sequential") not in ("sequential", "parallel"):
         raise ConfigError("rules.round_mode must be 'sequential' or 'parallel'.")
-    if rules.get("prompt_layout", "reference") not in ("reference", "append"):
-        raise ConfigError("rules.prompt_layout must be 'reference' or 'append'.")
+    if rules.get("prompt_layout", "reference") not in ("reference", "append", "shared"):
+        raise ConfigError("rules.prompt_layout must be 'reference', 'append' or 'shared'.")
     if not cfg.get("adapter_config") and cfg.get("adapter_config") != {}:
         raise ConfigError("config.json missing 'adapter_config' section.")
     if cfg.get("adapter_config") is None:

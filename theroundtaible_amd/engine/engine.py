@@ -189,6 +189,20 @@ class Engine:
             out = [self.tokenizer.bos_id]
         return out
 
+    def encode_prompt_split(self, prompt: PromptLike) -> Tuple[List[int], int]:
+        """Token ids plus the length of the prompt's shared part (``Prompt.shared_segments``
+        leading segments, chat-template prefix included; 0 without a ``shared_key``)."""
+        ids = self.encode_prompt(prompt)
+        nseg = getattr(prompt, "shared_segments", 0) if getattr(prompt, "shared_key", None) else 0
+        if nseg <= 0:
+            return ids, 0
+        head = Prompt(list(prompt.segments[:nseg]), templated=True)
+        n = len(self.encode_prompt(head)) if head.segments else 0
+        pre = self.tokenizer.chat_prefix
+        if pre and not getattr(prompt, "templated", False):
+            n += len(pre)
+        return ids, min(n, len(ids) - 1)
+
     # ---- prefix reuse ------------------------------------------------------------------------
     def sync_prefix(self, key: str, target: List[int]) -> Tuple[SeqState, int]:
         """Roll the resident sequence back to its LCP with ``target``; return (seq, reused tokens)."""
@@ -200,6 +214,37 @@ class Engine:
             n += 1
         self.kv.truncate(s, n)
         return s, n
+
+    @staticmethod
+    def shared_seq_key(key: str) -> str:
+        return "@shared:" + key
+
+    def sync_shared(self, key: str, shared: List[int]) -> Tuple[SeqState, List[int]]:
+        """Roll the table's shared sequence back to its LCP with ``shared``; return (seq, delta to
+        prefill). The shared sequence is never decoded: it only holds the common KV blocks."""
+        s = self.kv.seq(self.shared_seq_key(key))
+        n, lim, toks = 0, min(len(s.tokens), len(shared)), s.tokens
+        while n < lim and toks[n] == shared[n]:
+            n += 1
+        self.kv.truncate(s, n)
+        return s, shared[n:]
+
+    def attach_shared(self, s: SeqState, shared: SeqState, nblocks: int) -> int:
+        """Make ``s`` start with the first ``nblocks`` FULL blocks of ``shared`` (refcounted, no
+        copy): keep the leading blocks ``s`` already shares with it, drop the rest of ``s`` and
+        reference the shared blocks beyond. Returns the shared token count. Writers copy-on-write
+        a shared tail block, so a referenced block never changes under a reader."""
+        bs = self.kv.block_size
+        nblocks = min(nblocks, shared.length // bs)
+        k = 0
+        while k < min(len(s.blocks), nblocks) and s.blocks[k] == shared.blocks[k]:
+            k += 1
+        self.kv.truncate(s, min(s.length, k * bs))   # keeps <= k blocks, all shared ones
+        for i in range(len(s.blocks), nblocks):
+            self.kv.alloc.incref(shared.blocks[i])
+            s.blocks.append(shared.blocks[i])
+        s.tokens[:] = shared.tokens[:nblocks * bs]     # a referenced shared block is always full
+        return nblocks * bs
 
     def release(self, key: str) -> None:
         self.kv.free_seq(key)
@@ -362,33 +407,89 @@ class Engine:
             raise AssertionError(f"slot mapping outside [0, {lim}): {bad[:4]}")
 
     def _run_turns(self, turns: Sequence[Turn]) -> List[TurnOutput]:
+        # members of one shared-prefix group must be adjacent in the decode batch
+        order = group_order([getattr(t.prompt, "shared_key", None) for t in turns])
+        if order == list(range(len(turns))):
+            return self._run_turns_ordered(turns)
+        outs = self._run_turns_ordered([turns[i] for i in order])
+        res: List[Optional[TurnOutput]] = [None] * len(turns)
+        for j, i in enumerate(order):
+            res[i] = outs[j]
+        return res  # type: ignore[return-value]
+
+    def _sync_groups(self, turns: Sequence[Turn], enc: Sequence[Tuple[List[int], int]]):
+        """Prefill every shared-prefix group's common tokens ONCE into the group's shared
+        sequence and attach its full blocks to each member (``prompt_layout: shared``).
+        Returns (per-turn group key or None, {key: shared seq}, {key: shared prefill tokens})."""
+        keys = [getattr(t.prompt, "shared_key", None) if n > 0 else None for t, (_, n) in zip(turns, enc)]
+        shared: Dict[str, SeqState] = {}
+        pre: Dict[str, int] = {}
+        items = []
+        for key in dict.fromkeys(k for k in keys if k is not None):
+            members = [i for i, k in enumerate(keys) if k == key]
+            common = enc[members[0]][0][:enc[members[0]][1]]
+            for i in members[1:]:
+                common = common[:lcp(common, enc[i][0][:enc[i][1]])]
+            sq, delta = self.sync_shared(key, common)
+            shared[key] = sq
+            pre[key] = len(delta)
+            if delta:
+                items.append((sq, delta))
+        if items:
+            with trace.range("shared prefill"):
+                self.prefill(items)       # KV only; the shared sequence is never sampled
+        bs = self.kv.block_size
+        for t, key in zip(turns, keys):
+            if key is not None:
+                sq = shared[key]
+                self.attach_shared(self.kv.seq(t.seq_key), sq, sq.length // bs)
+        return keys, shared, pre
+
+    def _run_turns_ordered(self, turns: Sequence[Turn]) -> List[TurnOutput]:
         t_start = time.perf_counter()
-        targets = [self.encode_prompt(t.prompt) for t in turns]
+        enc = [self.encode_prompt_split(t.prompt) for t in turns]
+        targets = [ids for ids, _ in enc]
+        self._sync()
+        t0 = time.perf_counter()
+        keys, shared, shared_pre = self._sync_groups(turns, enc)
         seqs, reused = [], []
         for t, ids in zip(turns, targets):
             s, n = self.sync_prefix(t.seq_key, ids)
             seqs.append(s)
             reused.append(n)
         deltas = [ids[n:] for ids, n in zip(targets, reused)]
-        self._sync()
-        t0 = time.perf_counter()
         logits = self.prefill(list(zip(seqs, deltas)))
         first = self._sample_host(logits, seqs, turns)
+        # blocks every member of a group still shares (a member rolled back into the shared
+        # region has copied-on-write its tail): the grouped decode reads those once per group
+        sh_blocks: Dict[str, int] = {}
+        for s, key in zip(seqs, keys):
+            if key is not None:
+                sh_blocks[key] = min(sh_blocks.get(key, 1 << 30), common_blocks(s, shared[key]))
+        groups = ([k if k is not None and sh_blocks[k] > 0 else None for k in keys],
+                  [sh_blocks.get(k, 0) if k is not None else 0 for k in keys])
         self._sync()
         t1 = time.perf_counter()
-        gen, decode_steps = self.decode(seqs, turns, first, deadline=t_start + min(t.timeout_s for t in turns))
+        gen, decode_steps = self.decode(seqs, turns, first, deadline=t_start + min(t.timeout_s for t in turns),
+                                        groups=groups if any(g is not None for g in groups[0]) else None)
         self._sync()
         t2 = time.perf_counter()
         self.check_device_flags()
         outs = []
-        for t, s, g, n, d in zip(turns, seqs, gen, reused, deltas):
+        seen = set()
+        for t, s, g, n, d, key in zip(turns, seqs, gen, reused, deltas, keys):
             text = self.tokenizer.decode(g)
+            spre = 0
+            if key is not None and key not in seen:     # the group's shared prefill, counted once
+                seen.add(key)
+                spre = shared_pre[key]
             outs.append(TurnOutput(text, g, {
-                "prompt_tokens": len(d) + n, "prefill_tokens": len(d), "reused_tokens": n,
+                "prompt_tokens": len(d) + n, "prefill_tokens": len(d) + spre, "reused_tokens": n,
+                "shared_tokens": sh_blocks.get(key, 0) * self.kv.block_size if key is not None else 0,
                 "decode_tokens": len(g), "prefill_ms": (t1 - t0) * 1e3, "decode_ms": (t2 - t1) * 1e3,
                 "decode_tok_s": len(g) / max(t2 - t1, 1e-9), "batch": len(turns),
                 "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3}))
-        self.stats["prefill_tokens"] += sum(len(d) for d in deltas)
+        self.stats["prefill_tokens"] += sum(len(d) for d in deltas) + sum(shared_pre.values())
         self.stats["decode_tokens"] += sum(len(g) for g in gen)
         self.stats["prefill_s"] += t1 - t0
         self.stats["decode_s"] += t2 - t1
@@ -488,7 +589,9 @@ class Engine:
 
     # ---- decode -------------------------------------------------------------------------------------
     def decode(self, seqs: Sequence[SeqState], turns: Sequence[Turn], first: torch.Tensor,
-               deadline: float) -> Tuple[List[List[int]], int]:
+               deadline: float, groups=None) -> Tuple[List[List[int]], int]:
+        """``groups``: optional (per-sequence group key or None, per-sequence shared block count)
+        — consecutive sequences of one key decode their shared KV blocks once (grouped K3)."""
         B = len(seqs)
         max_new = [max(1, t.params.max_new_tokens) for t in turns]
         steps = max(max_new)
@@ -499,7 +602,7 @@ class Engine:
         runner = None
         if self.on_gpu and self.ecfg.use_graphs:
             try:
-                runner = self._graph_for(B, max(s.length for s in seqs) + steps)
+                runner = self._graph_for(B, max(s.length for s in seqs) + steps, grouped=groups is not None)
             except RuntimeError as e:   # e.g. a collective that refuses stream capture: stay eager
                 if self.tp.size == 1:
                     raise
@@ -508,9 +611,9 @@ class Engine:
                 self.ecfg.use_graphs = False
         with trace.range(f"decode B={B} steps={steps}"):
             if runner is not None:
-                toks = runner.run(self, seqs, turns, first, steps, deadline, eos)
+                toks = runner.run(self, seqs, turns, first, steps, deadline, eos, groups)
             else:
-                toks = self._decode_eager(seqs, turns, first, steps, deadline, eos)
+                toks = self._decode_eager(seqs, turns, first, steps, deadline, eos, groups)
         gen: List[List[int]] = []
         for b, (s, t) in enumerate(zip(seqs, turns)):
             g = toks[b][:max_new[b]]
@@ -525,7 +628,18 @@ class Engine:
             self.kv.truncate(s, s.length - 1 if g else s.length)
         return gen, steps
 
-    def _decode_eager(self, seqs, turns, first, steps, deadline, eos) -> List[List[int]]:
+    def group_table(self, groups, B: int) -> Optional[torch.Tensor]:
+        """Host ``[B, 3]`` int32 group table for the grouped decode kernel (rows past the real
+        sequences run alone), or None without groups."""
+        if groups is None:
+            return None
+        labels, shb = list(groups[0]), list(groups[1])
+        labels += [None] * (B - len(labels))
+        shb += [0] * (B - len(shb))
+        t, _ = ops.decode_groups(labels, shb, self.model.n_heads // self.model.n_kv_heads)
+        return t
+
+    def _decode_eager(self, seqs, turns, first, steps, deadline, eos, groups=None) -> List[List[int]]:
         dev = self.device
         B = len(seqs)
         cur = first.clone()
@@ -542,14 +656,18 @@ class Engine:
         bt = bt.to(dev)
         bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
         splits = ops.decode_splits(bucket, self.model.n_kv_heads) if self.on_gpu else 1
-        ws = ops.DecodeWorkspace(B, self.model.n_heads, self.cfg.head_dim, splits, dev) if self.on_gpu else None
+        G = self.model.n_heads // self.model.n_kv_heads
+        ws = ops.DecodeWorkspace(B, self.model.n_heads, self.cfg.head_dim, splits, dev,
+                                 max_group=ops.MAX_GROUP_COLS // G if groups is not None else 1) if self.on_gpu else None
+        gt = self.group_table(groups, B)
+        gt = gt.to(dev) if gt is not None and self.on_gpu else None
         for step in range(1, steps):
             pos = list(lens)
             slots = [s.blocks[p // self.kv.block_size] * self.kv.block_size + p % self.kv.block_size
                      for s, p in zip(seqs, pos)]
             meta = AttnMeta(kind="decode", slot_mapping=torch.tensor(slots, dtype=torch.int64, device=dev),
                             block_tables=bt, ctx_lens=torch.tensor([p + 1 for p in pos], dtype=torch.int32, device=dev),
-                            num_splits=splits, workspace=ws)
+                            num_splits=splits, workspace=ws, groups=gt)
             logits = self.model.forward(cur.to(dev), torch.tensor(pos, dtype=torch.int64, device=dev), self.kv, meta)
             offs = torch.tensor([p + 1 for p in pos], dtype=torch.int64, device=dev)
             cur = ops.sample(logits.contiguous(), temp, top_p, top_k, seeds, offs)
@@ -570,16 +688,40 @@ class Engine:
         for s in seqs:
             self.kv.truncate(s, s.length)
 
-    def _graph_for(self, B: int, max_ctx: int) -> "DecodeGraph":
+    def _graph_for(self, B: int, max_ctx: int, grouped: bool = False) -> "DecodeGraph":
         from .graphs import DecodeGraph
         bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
         splits = ops.decode_splits(bucket, self.model.n_kv_heads)
-        key = (bucket, splits)
+        key = (bucket, splits, grouped)
         g = self.graphs.get(key)
         if g is None:
-            g = DecodeGraph(self, bucket, splits)
+            g = DecodeGraph(self, bucket, splits, grouped=grouped)
             self.graphs[key] = g
         return g
+
+
+def lcp(a: Sequence[int], b: Sequence[int]) -> int:
+    n, lim = 0, min(len(a), len(b))
+    while n < lim and a[n] == b[n]:
+        n += 1
+    return n
+
+
+def common_blocks(s: SeqState, shared: SeqState) -> int:
+    """Leading blocks ``s`` references from ``shared`` (same ids, hence same K/V)."""
+    k, lim = 0, min(len(s.blocks), len(shared.blocks))
+    while k < lim and s.blocks[k] == shared.blocks[k]:
+        k += 1
+    return k
+
+
+def group_order(keys: Sequence[Optional[str]]) -> List[int]:
+    """Stable permutation putting turns with the same shared-prefix key next to each other
+    (first appearance order); key-less turns keep their relative place."""
+    first: Dict[object, int] = {}
+    for i, k in enumerate(keys):
+        first.setdefault(k if k is not None else ("__alone", i), i)
+    return sorted(range(len(keys)), key=lambda i: (first[keys[i] if keys[i] is not None else ("__alone", i)], i))
 
 
 def cut_at_stop(ids: List[int], stops: frozenset) -> List[int]:

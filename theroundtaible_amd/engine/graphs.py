@@ -24,7 +24,7 @@ MAX_STEPS = 8192
 
 
 class DecodeGraph:
-    def __init__(self, engine, bucket: int, splits: int):
+    def __init__(self, engine, bucket: int, splits: int, grouped: bool = False):
         self.engine = engine
         self.B = bucket
         self.splits = splits
@@ -49,7 +49,14 @@ class DecodeGraph:
         self.slots = torch.zeros(B, dtype=torch.int64, device=dev)
         self.offsets = torch.zeros(B, dtype=torch.int64, device=dev)
         self.hidden = torch.zeros(B, engine.model.cfg.hidden, dtype=engine.model.dtype, device=dev)
-        self.ws = ops.DecodeWorkspace(B, engine.model.n_heads, engine.cfg.head_dim, max(1, splits), dev)
+        G = engine.model.n_heads // engine.model.n_kv_heads
+        self.ws = ops.DecodeWorkspace(B, engine.model.n_heads, engine.cfg.head_dim, max(1, splits), dev,
+                                      max_group=ops.MAX_GROUP_COLS // G if grouped else 1)
+        # shared-prefix group table (grouped K3); rows default to "alone"
+        self.groups = None
+        if grouped:
+            self.groups = torch.zeros(B, 3, dtype=torch.int32, device=dev)
+            self._reset_groups()
         self.guard_err = torch.zeros(1, dtype=torch.int32, device=dev)   # debug paging guard (captured)
         self.graph = None
         self._capture()
@@ -71,7 +78,7 @@ class DecodeGraph:
             ops.paging_guard(self.block_tables, self.ctx_lens, self.positions, slots, self.guard_err,
                              e.kv.num_blocks, self.bs)
         meta = AttnMeta(kind="decode", slot_mapping=slots, block_tables=self.block_tables, ctx_lens=self.ctx_lens,
-                        num_splits=self.splits, workspace=self.ws)
+                        num_splits=self.splits, workspace=self.ws, groups=self.groups)
         if hidden is not None:
             logits = e.model.forward(self.input_ids, self.positions, e.kv, meta, hidden=hidden)
         else:
@@ -87,7 +94,12 @@ class DecodeGraph:
             raise AssertionError(f"paging guard tripped in the decode graph (code {code}): "
                                  f"{ops.paging_guard_message(code)}")
 
+    def _reset_groups(self):
+        if self.groups is not None:
+            self.groups.copy_(torch.tensor([[b, 1, 0] for b in range(self.B)], dtype=torch.int32))
+
     def _reset_dummy(self):
+        self._reset_groups()
         self.positions.zero_()
         self.ctx_lens.fill_(1)
         self.step.zero_()
@@ -111,7 +123,7 @@ class DecodeGraph:
         self._reset_dummy()
 
     def run(self, engine, seqs: Sequence, turns: Sequence, first: torch.Tensor, steps: int, deadline: float,
-            eos: int) -> List[List[int]]:
+            eos: int, groups=None) -> List[List[int]]:
         from .engine import _finished
         B = len(seqs)
         dev = engine.device
@@ -123,6 +135,8 @@ class DecodeGraph:
         if engine.debug_checks:
             engine.check_paging(bt, [])
         self.block_tables.copy_(bt.to(dev, non_blocking=True))
+        if self.groups is not None and groups is not None:
+            self.groups.copy_(engine.group_table(groups, self.B).to(dev, non_blocking=True))
         lens = torch.tensor([s.length for s in seqs] + [0] * (self.B - B), dtype=torch.int64)
         self.positions.copy_(lens.to(dev, non_blocking=True))
         self.ctx_lens.copy_((lens + 1).to(torch.int32).to(dev, non_blocking=True))

@@ -62,7 +62,7 @@ class GPT2Model:
                                    self.n_heads, self.n_kv_heads, self.head_dim)
             if meta.kind == "decode":
                 a = ops.paged_attention_decode(q, kv.k_layer(l), kv.v_layer(l), meta.block_tables, meta.ctx_lens,
-                                               self.scale, meta.num_splits, meta.workspace)
+                                               self.scale, meta.num_splits, meta.workspace, groups=meta.groups)
             else:
                 a = ops.prefill_attention(q, kv.k_layer(l), kv.v_layer(l), meta.block_tables, meta.cu_q,
                                           meta.start_pos, self.scale, meta.tile_map)

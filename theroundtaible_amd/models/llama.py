@@ -40,6 +40,7 @@ class AttnMeta:
     start_pos: Optional[torch.Tensor] = None    # prefill: [S] int32
     tile_map: Optional[torch.Tensor] = None     # prefill: [n_tiles, 2] int32
     last_rows: Optional[torch.Tensor] = None    # prefill: rows whose logits are needed
+    groups: Optional[torch.Tensor] = None       # decode: [B, 3] shared-prefix groups (ops.decode_groups)
 
 
 class LlamaModel:
@@ -65,7 +66,7 @@ class LlamaModel:
     def attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         if meta.kind == "decode":
             return ops.paged_attention_decode(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale,
-                                              meta.num_splits, meta.workspace)
+                                              meta.num_splits, meta.workspace, groups=meta.groups)
         return ops.prefill_attention(q, kc, vc, meta.block_tables, meta.cu_q, meta.start_pos, self.scale,
                                      meta.tile_map)
 

@@ -37,7 +37,7 @@ from .context import build_context
 from .errors import AdapterError, classify_error
 from .knights.base import KnightBackend, TurnRequest, TurnResult
 from .prompt import (Prompt, Segment, TurnContext, build_turn_prompt_append, build_turn_prompt_reference,
-                     transcript_entry_segments, KING_DEMAND)
+                     build_turn_prompt_shared, transcript_entry_segments, KING_DEMAND)
 from .tools import resolve_file_requests
 from .types import (UNDEFINED, ConsensusBlock, ContinueOptions, KnightConfig, RoundEntry,
                     RoundtableConfig, SessionResult)
@@ -150,11 +150,14 @@ class Orchestrator:
                 king_demand: bool, resolved_files: str, resolved_commands: str) -> Prompt:
         if self.layout == "append":
             return build_turn_prompt_append(knight, self.config.knights, ctx, self.transcript, rnd)
+        if self.layout == "shared":
+            return build_turn_prompt_shared(knight, self.config.knights, ctx, self.transcript, rnd,
+                                            shared_key=self.table_id + "@table")
         return build_turn_prompt_reference(knight, self.config.knights, ctx, visible, king_demand=king_demand,
                                            resolved_files=resolved_files, resolved_commands=resolved_commands)
 
     def _append_transcript(self, entry: RoundEntry, res: Optional[TurnResult]) -> None:
-        if self.layout != "append":
+        if self.layout not in ("append", "shared"):
             return
         ids = res.ids if res is not None else None
         tok = res.tokenizer if res is not None else None
@@ -195,7 +198,7 @@ class Orchestrator:
                 new = resolve_file_requests(consensus.file_requests, self.root, self.config.rules.ignore)
                 if new:
                     tool_state["files"] += ("\n\n" if tool_state["files"] else "") + new
-                    if self.layout == "append":
+                    if self.layout in ("append", "shared"):
                         self.transcript.append(Segment(
                             f"\n\nOPGEVRAAGDE BESTANDEN (via file_requests van {knight.name}):\n{new}"))
             if consensus.verify_commands:
@@ -203,7 +206,7 @@ class Orchestrator:
                 new = resolve_verify_commands(consensus.verify_commands, self.root, log=ui.dim)
                 if new:
                     tool_state["commands"] += ("\n\n" if tool_state["commands"] else "") + new
-                    if self.layout == "append":
+                    if self.layout in ("append", "shared"):
                         self.transcript.append(Segment(
                             f"\n\nVERIFICATIE RESULTATEN (via verify_commands van {knight.name}):\n{new}"))
         else:
@@ -266,10 +269,10 @@ class Orchestrator:
             for e in continue_from.all_rounds:
                 if e.consensus:
                     self.latest[e.knight] = e.consensus
-            if self.layout == "append" and not self.transcript:
+            if self.layout in ("append", "shared") and not self.transcript:
                 for e in continue_from.all_rounds:
                     self.transcript.extend(transcript_entry_segments(e))
-            if self.layout == "append":
+            if self.layout in ("append", "shared"):
                 self.transcript.append(Segment("\n" + KING_DEMAND))
         self.start = continue_from.start_round if continue_from else 1
         self.end = self.start + rules.max_rounds - 1
