@@ -4,12 +4,15 @@
 Workload (one "step" = one complete discussion round):
   * knights are Llama-3-8B (bf16, random-init weights: there are no checkpoints), 3 per
     table, a table = one 3-knight ``discuss`` (BASELINE config 2 / metric "3-knight discuss");
-  * N GPUs host N tables (3N knights). Knight j of table t lives on rank (3t + j) mod N,
-    so every GPU hosts exactly 3 knights (batched in one decode hipGraph) and every table
-    spans min(3, N) GPUs — each round's responses cross xGMI in the RCCL all-gather (C1).
+  * N GPUs host N tables (3N knights), 3 knights per GPU batched in one decode hipGraph.
+    ``--placement packed`` (default): table t lives on GPU t, so its knights share one copy
+    of the discussion's KV (``shared`` layout); every rank still runs every table's
+    orchestrator (SPMD) and each round's responses are all-gathered over RCCL (C1).
+    ``striped``: knight j of table t on rank (3t + j) mod N, every response crossing xGMI.
     Per-GPU work is fixed as N grows: ``scaling: weak``;
-  * ``parallel`` round mode, ``append`` prompt layout, the real orchestrator
-    (prompt assembly, consensus parse, discussion.md/metrics writes) inside the timed region;
+  * ``parallel`` round mode, ``shared`` prompt layout (``--layout append`` is the
+    round-1 layout), the real orchestrator (prompt assembly, consensus parse,
+    discussion.md/metrics writes) inside the timed region;
   * fixed ``--new-tokens`` per turn with EOS ignored (random weights never emit a
     consensus block; BASELINE.md measurement protocol).
 
@@ -53,8 +56,13 @@ def parse():
     p.add_argument("--round-mode", default="parallel", choices=["parallel", "sequential"],
                    help="parallel: all knights of a round decode as one batch; sequential: reference "
                         "semantics (speakers in order, each sees the earlier speakers of the round)")
-    p.add_argument("--layout", default="append", choices=["append", "shared", "reference"],
-                   help="prompt layout; 'shared' keeps one copy of a table's common transcript KV per GPU")
+    p.add_argument("--layout", default="shared", choices=["shared", "append", "reference"],
+                   help="prompt layout; 'shared' (default) keeps ONE copy of a table's common prefix KV per GPU, "
+                        "read once per decode step for all of the table's knights there (grouped K3)")
+    p.add_argument("--placement", default="packed", choices=["packed", "striped"],
+                   help="packed (default): a table's knights share one GPU group (batched decode + shared prefix "
+                        "KV); striped: knight j of table t on group (kpt*t + j) mod groups (every response "
+                        "crosses xGMI, no KV sharing)")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--kv-fraction", type=float, default=0.85,
                    help="fraction of free HBM for the KV pool (lower it when ranks share a GPU)")
@@ -115,7 +123,8 @@ def main() -> int:
         knights = []
         for j in range(kpt):
             name = f"{base_names[j % len(base_names)]}-{t}"
-            placement[name] = group_ranks[(kpt * t + j) % n_groups]
+            slot = (t * kpt + j) // max(1, args.knights_per_gpu) if args.placement == "packed" else kpt * t + j
+            placement[name] = group_ranks[slot % n_groups]
             knights.append({"name": name, "adapter": f"local-llm-{name.lower()}", "capabilities": ["architecture"],
                             "priority": j + 1})
         tables.append(knights)
@@ -202,12 +211,14 @@ def main() -> int:
                    "knights_per_gpu": args.knights_per_gpu, "new_tokens_per_turn": args.new_tokens,
                    "global_batch": kpt * n_tables, "seq_len": args.new_tokens,
                    "round_mode": args.round_mode, "prompt_layout": args.layout,
-                   "parallelism": (f"knight-placement x{N} (tables striped over GPUs), C1 all-gather" if T == 1 else
-                                   f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL")},
+                   "placement": args.placement,
+                   "parallelism": (f"knight-placement x{N} (tables {args.placement} over GPUs), C1 all-gather"
+                                   if T == 1 else f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL")},
         "detail": {"world": cl.world, "backend": cl.backend, "c1_ranks": cl.world if cl.distributed else 1,
                    "failed_turns": len(failures), "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
+                   "kv_blocks_used_rank0": engine.kv.num_blocks - engine.kv.alloc.num_free,
                    "kv_capacity_tokens": engine.kv_capacity_tokens},
     }
     if cl.rank == 0:

@@ -353,21 +353,37 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   const int mask = s_last;
   if (mask == 0) return false;
 
-  // latency-bound: each output thread issues the (m, l) AND partial-O loads of up to 16 slots
-  // at once (one round trip for <= 16 slots, no LDS weight pass) and merges them online
-  for (int it = threadIdx.x; it < ncol * (D / 4); it += blockDim.x) {
-    const int qi = it / (D / 4), d0 = 4 * (it - qi * (D / 4));
-    if (!((mask >> (qi / G)) & 1)) continue;
-    const int row = col_row(qi);
+  // latency-bound: tpi threads per output element (member head, 4 dims) split its slots
+  // (s = sub, sub+tpi, ...), each issuing the (m, l) AND partial-O loads of up to 16 slots at
+  // once, merge them online, then merge the tpi states with xor-shuffles: one round trip per
+  // 16*tpi slots, no LDS weight pass
+  const int per_m = G * (D / 4);
+  const int nm = __popc(mask);
+  // threads per element: 4 when the elements leave room (a lone sequence: 128 elements), else
+  // 1 (a group's last arrival usually combines every member: 3 x 128 elements on 512 threads)
+  const int lg = nm * per_m * 4 <= (int)blockDim.x ? 2 : (nm * per_m * 2 <= (int)blockDim.x ? 1 : 0);
+  const int tpi = 1 << lg;
+  const int sub = threadIdx.x & (tpi - 1);
+  for (int it = threadIdx.x >> lg; it < nm * per_m; it += blockDim.x >> lg) {
+    const int k = it / per_m;
+    int mm = 0;
+    for (int bits = mask, c = 0;; bits &= bits - 1) {   // k-th member set in the mask
+      mm = __ffs(bits) - 1;
+      if (c++ == k) break;
+    }
+    const int w = it - k * per_m;
+    const int hj = w / (D / 4), d0 = 4 * (w - hj * (D / 4));
+    const int row = mm * Hq + hj;
     float4_ O = {0.f, 0.f, 0.f, 0.f};
     float Mr = -INFINITY, Lr = 0.f;
-    for (int s0 = 0; s0 < nslots; s0 += 16) {
+    for (int s0 = 0; s0 < nslots; s0 += 16 * tpi) {
       float4_ vv[16], ml[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const bool ok = s0 + j < nslots;
-        ml[j] = ok ? rt::sc1_load4(pml_rsrc, (row * stride + s0 + j) * 16) : float4_{-INFINITY, 0.f, 0.f, 0.f};
-        vv[j] = ok ? rt::sc1_load4(po_rsrc, ((row * stride + s0 + j) * D + d0) * 4) : float4_{0.f, 0.f, 0.f, 0.f};
+        const int sl = s0 + tpi * j + sub;
+        const bool ok = sl < nslots;
+        ml[j] = ok ? rt::sc1_load4(pml_rsrc, (row * stride + sl) * 16) : float4_{-INFINITY, 0.f, 0.f, 0.f};
+        vv[j] = ok ? rt::sc1_load4(po_rsrc, ((row * stride + sl) * D + d0) * 4) : float4_{0.f, 0.f, 0.f, 0.f};
       }
       float Mc = Mr;
 #pragma unroll
@@ -387,8 +403,21 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
       }
       Mr = Mc;
     }
-    const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
-    store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
+    for (int x = 1; x < tpi; x <<= 1) {               // merge the sub-states (same wave, uniform tpi)
+      const float Mo = __shfl_xor(Mr, x, 64), Lo = __shfl_xor(Lr, x, 64);
+      float4_ Oo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Oo[i] = __shfl_xor(O[i], x, 64);
+      const float Mn = fmaxf(Mr, Mo);
+      const float fa = Mr == -INFINITY ? 0.f : exp2f(Mr - Mn), fb = Mo == -INFINITY ? 0.f : exp2f(Mo - Mn);
+      O = O * fa + Oo * fb;
+      Lr = Lr * fa + Lo * fb;
+      Mr = Mn;
+    }
+    if (sub == 0) {
+      const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
+      store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
+    }
   }
   __syncthreads();
   return true;

@@ -116,11 +116,20 @@ def test_spmd_bench_two_ranks():
 
 @pytest.mark.parametrize("nproc", [4, 8])
 def test_spmd_bench_scaling_world_sizes(nproc):
-    """The driver's scaling run (N = 4, 8 ranks) on the gloo/CPU path: 3 knights per rank,
-    tables striped over ranks, every response crossing ranks in the C1 exchange."""
+    """The driver's scaling run (N = 4, 8 ranks) on the gloo/CPU path: 3 knights per rank, one
+    table per rank sharing its prefix KV (default packed placement), every table's responses
+    all-gathered to every rank in the C1 exchange."""
     out = _bench(nproc)
     assert out["n_gpus"] == nproc and out["config"]["tables"] == nproc and out["config"]["knights"] == 3 * nproc
     assert out["detail"]["decode_tokens"] == 3 * nproc * 8 * 2 and out["detail"]["failed_turns"] == 0
+    assert out["config"]["placement"] == "packed" and out["config"]["prompt_layout"] == "shared"
+
+
+def test_spmd_bench_striped_append_layout():
+    """Round-1 placement and layout: knights of a table on different ranks, private KV."""
+    out = _bench(4, ("--placement", "striped", "--layout", "append"))
+    assert out["config"]["tables"] == 4 and out["detail"]["failed_turns"] == 0
+    assert out["detail"]["decode_tokens"] == 3 * 4 * 8 * 2
 
 
 def test_cli_discuss_under_torchrun_with_tp_knight(tmp_path):

@@ -655,7 +655,7 @@ class Engine:
             bt[j, :len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
         bt = bt.to(dev)
         bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
-        splits = ops.decode_splits(bucket, self.model.n_kv_heads) if self.on_gpu else 1
+        splits = ops.decode_splits(bucket, self.model.n_kv_heads, grouped=groups is not None) if self.on_gpu else 1
         G = self.model.n_heads // self.model.n_kv_heads
         ws = ops.DecodeWorkspace(B, self.model.n_heads, self.cfg.head_dim, splits, dev,
                                  max_group=ops.MAX_GROUP_COLS // G if groups is not None else 1) if self.on_gpu else None
@@ -691,7 +691,7 @@ class Engine:
     def _graph_for(self, B: int, max_ctx: int, grouped: bool = False) -> "DecodeGraph":
         from .graphs import DecodeGraph
         bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
-        splits = ops.decode_splits(bucket, self.model.n_kv_heads)
+        splits = ops.decode_splits(bucket, self.model.n_kv_heads, grouped=grouped)
         key = (bucket, splits, grouped)
         g = self.graphs.get(key)
         if g is None:

@@ -120,7 +120,8 @@ class DecodeWorkspace:
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 64) -> int:
+def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 64,
+                  grouped: bool = False) -> int:
     """Split-KV count fixed per (batch bucket, kv heads): at most one 8-wave workgroup per CU
     (measured on MI355X, profiles/r01_microbench_v1.log: B=3, ctx 6000 -> 8 splits 22 µs,
     11 splits 27 µs, 16 splits 28 µs; extra workgroups only add hand-off round trips).
@@ -128,7 +129,11 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: i
     The kernel derives each split's key range from the *runtime* context length, so one
     captured hipGraph serves every length (splits past the end are empty and skipped by the
     combine) — no re-capture as a knight's discussion grows."""
-    want = num_cus // max(1, batch * n_kv_heads)   # never more workgroups than CUs: a second
+    # grouped (shared-prefix) decode: a workgroup streams 1/n of the group's shared keys, so the
+    # launch is shorter and its fixed latency chain weighs more — 3/4 of the CUs measured best
+    # (B=3, shared 22K/40K: 8 splits 30.8/42.7 us vs 10 splits 31.7/43.8, r2_gattn_v1.log)
+    cus = num_cus * 3 // 4 if grouped else num_cus
+    want = cus // max(1, batch * n_kv_heads)        # never more workgroups than CUs: a second
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
 

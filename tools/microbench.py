@@ -121,6 +121,35 @@ def bench_attn(B, ctx, splits_list):
         row(f"decode attn B={B} ctx={ctx} splits={splits}", timed(fn), nbytes)
 
 
+def bench_attn_grouped(B, shared, private, splits_list):
+    """Shared-prefix groups: B knights read one `shared`-token prefix + `private` own tokens."""
+    hq, hkv, d = 32, 8, 128
+    G = hq // hkv
+    nsh, npr = shared // 32, (private + 31) // 32
+    nblk = nsh + B * npr
+    copies = 6
+    caches = [(bf(nblk, hkv, 32, d), bf(nblk, hkv, d, 32)) for _ in range(copies)]
+    bt = torch.zeros(B, nsh + npr, dtype=torch.int32)
+    for b in range(B):
+        bt[b, :nsh] = torch.arange(nsh)
+        bt[b, nsh:] = nsh + b * npr + torch.arange(npr)
+    bt = bt.to(DEV)
+    cl = torch.full((B,), nsh * 32 + private, device=DEV, dtype=torch.int32)
+    q = bf(B, hq, d)
+    groups, _ = ops.decode_groups(["g"] * B, [nsh] * B, G)
+    groups = groups.to(DEV)
+    nbytes = (nsh * 32 + B * private) * hkv * d * 2 * 2
+    for splits in splits_list:
+        for grouped in (True, False):
+            ws = ops.DecodeWorkspace(B, hq, d, splits, DEV, max_group=16 // G if grouped else 1)
+            out = torch.empty_like(q)
+            gt = groups if grouped else None
+            fn = lambda i, ws=ws, splits=splits, out=out, gt=gt: ops.paged_attention_decode(
+                q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out, groups=gt)
+            row(f"decode attn {'grouped' if grouped else 'private'} B={B} shared={shared} own={private} splits={splits}",
+                timed(fn), nbytes if grouped else nbytes + (B - 1) * nsh * 32 * hkv * d * 4)
+
+
 def bench_sample(B):
     V = 128256
     lg = bf(B, V)
@@ -155,6 +184,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=6000)
     ap.add_argument("--only", default="gemm,attn,sample,prefill")
     ap.add_argument("--splits", default="4,8,11,16,32")
+    ap.add_argument("--shared", default="22000:1500", help="grouped attention: shared:private tokens list, comma-sep")
     a = ap.parse_args()
     only = set(a.only.split(","))
     torch.manual_seed(0)
@@ -163,6 +193,10 @@ def main():
     if "attn" in only:
         bench_attn(a.batch, a.ctx, [int(s) for s in a.splits.split(",")])
         bench_attn(a.batch, 1500, [4, 8, 11, 16])
+    if "gattn" in only:
+        for sp in a.shared.split(","):
+            sh, pr = (int(x) for x in sp.split(":"))
+            bench_attn_grouped(a.batch, sh, pr, [int(s) for s in a.splits.split(",")])
     if "sample" in only:
         bench_sample(a.batch)
     if "prefill" in only:
