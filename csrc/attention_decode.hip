@@ -3,13 +3,15 @@
 // file holds the grid launch: blockIdx = (sequence x kv head, key split).
 #include "attn_core.h"
 
+#include <cstdlib>
+
 namespace {
 using namespace attn;
 
-template <int D, int GM>
-__global__ void __launch_bounds__(NW * 64) paged_decode_kernel(AttnArgs p) {
-  __shared__ AttnSmem<D, GM> sm;
-  attn_item<D, false, GM>(p, blockIdx.x, blockIdx.y, sm);
+template <int D, int GM, int W = NW>
+__global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
+  __shared__ AttnSmem<D, GM, W> sm;
+  attn_item<D, false, GM, W>(p, blockIdx.x, blockIdx.y, sm);
 }
 }  // namespace
 
@@ -29,9 +31,11 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   dim3 grid(B * Hkv, num_splits), block(NW * 64);
   const float sl2 = scale * LOG2E;
   if (groups != nullptr && slot_stride < num_splits) return -4;
-  const AttnArgs args{(uint16_t*)out, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+  AttnArgs args{(uint16_t*)out, (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
                       block_tables, ctx_lens, part_o, part_ml, counters, Hq, Hkv, max_blocks, sl2, num_splits,
                       groups, groups != nullptr ? slot_stride : 0};
+  static const int probe = getenv("RT_ATTN_PROBE") ? atoi(getenv("RT_ATTN_PROBE")) : 0;
+  args.probe = probe;
   const int G = Hq / Hkv;
   // a group's n*G columns need the 16-column LDS merge buffers
 #define RT_PD(DV)                                                                                  \

@@ -92,15 +92,16 @@ struct AttnArgs {
   // its group, group size n, shared full blocks}. n * G <= 16 (host-checked).
   const int* groups = nullptr;
   int slot_stride = 0;         // partial slots per (sequence, head) >= n * num_splits; 0 = num_splits
+  int probe = 0;               // latency probe (microbench only, RT_ATTN_PROBE): stop after phase k
 };
 
 // GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
 // no groups) keeps the workgroup at ~26 KB so two fit a CU: 16 waves streaming K/V per CU.
-template <int D, int GM = 16>
+template <int D, int GM = 16, int W = NW>
 struct AttnSmem {
-  float s_m[NW][16];
-  float s_l[NW][16];
-  float s_o[NW][GM][D + 4];
+  float s_m[W][16];
+  float s_l[W][16];
+  float s_o[W][GM][D + 4];
   int s_last;                  // bit m: this workgroup combines member m
 };
 
@@ -117,8 +118,10 @@ RT_DEVICE void store_bf16x4(uint16_t* dst, float a, float b_, float c, float d, 
 
 // One (sequence, kv head, key split) work item. Returns true when this workgroup wrote final
 // output rows (no split, or the last-arriving split that combined them).
-template <int D, bool SC1, int GM = 16>
-RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& S) {
+// W = waves per workgroup (8; 16 for grouped launches: twice the K/V in flight per CU and
+// enough threads to combine a whole group's slots in one round trip).
+template <int D, bool SC1, int GM = 16, int W = NW>
+RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W>& S) {
   uint16_t* __restrict__ out = P.out;
   const uint16_t* __restrict__ q = P.q;
   const uint16_t* __restrict__ k_cache = P.k_cache;
@@ -156,6 +159,10 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   const int rseq = r / G, rhead = r - (r / G) * G;  // column r -> (member, head within the kv group)
 
   const int ctx = ctx_lens[b];
+  if (P.probe == 1) {          // launch + metadata round trip only
+    if (ctx == -12345) out[0] = 0;
+    return false;
+  }
   const int ntiles = (ctx + BS - 1) / BS;
   // this workgroup's shared chunk (all members' columns) then its private split (own columns)
   const int sh_per = (sh + nslots - 1) / nslots;
@@ -196,23 +203,23 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   };
   Tile<D> cur, nxt;
   int v = wid;
-  // Block ids of this wave's tiles (v = wid + NW*j) are fetched one per lane up front, in
+  // Block ids of this wave's tiles (v = wid + W*j) are fetched one per lane up front, in
   // flight with Q, and read out with readlane: no dependent scalar load inside the loop (refilled
   // every 64 tiles, i.e. only past ~164K keys at 10 splits). B=3, ctx 1500: 12.2 -> 11.2 us.
   int blk_lane = 0;
   {
-    const int tt = v + NW * lane;
+    const int tt = v + W * lane;
     if (tt < nv) blk_lane = bt_entry(tt);
   }
   if (v < nv) {
     const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, 0) * blk_stride + (size_t)hk * BS * D;
     load_tile<D, SC1>(cur, k_cache + base, v_cache + base, r, g);
   }
-  for (int j = 1; v < nv; v += NW, ++j) {
-    const int vn = v + NW;
+  for (int j = 1; v < nv; v += W, ++j) {
+    const int vn = v + W;
     if (vn < nv) {  // keep the next tile's loads in flight during this tile's math
       if ((j & 63) == 0) {
-        const int tt = vn + NW * lane;
+        const int tt = vn + W * lane;
         blk_lane = tt < nv ? bt_entry(tt) : 0;
       }
       const size_t base =
@@ -278,6 +285,10 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
     }
     cur = nxt;
   }
+  if (P.probe == 2) {          // + block ids, Q, every K/V tile and the math
+    if (m == 12345.f && lsum == 1.f) out[0] = (uint16_t)oacc[0][0];
+    return false;
+  }
   // column-complete partial sum for q = r
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
@@ -304,12 +315,12 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
     const int row = col_row(qi);
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][qi]);
+    for (int w = 0; w < W; ++w) M = fmaxf(M, s_m[w][qi]);
     float L = 0.f;
     float4_ O = {0.f, 0.f, 0.f, 0.f};
     if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
+      for (int w = 0; w < W; ++w) {
         const float f = exp2f(s_m[w][qi] - M);
         L += f * s_l[w][qi];
         const float4_ ow = *reinterpret_cast<const float4_*>(&s_o[w][qi][d0]);
@@ -351,20 +362,20 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
   }
   __syncthreads();
   const int mask = s_last;
+  if (P.probe == 3) return false;   // + wave merge, partial stores, drain, arrival atomics
   if (mask == 0) return false;
 
-  // latency-bound: tpi threads per output element (member head, 4 dims) split its slots
-  // (s = sub, sub+tpi, ...), each issuing the (m, l) AND partial-O loads of up to 16 slots at
-  // once, merge them online, then merge the tpi states with xor-shuffles: one round trip per
-  // 16*tpi slots, no LDS weight pass
-  const int per_m = G * (D / 4);
+  // One thread per output element (member head row, 4 dims); the RL = D/4 threads of a row are
+  // consecutive lanes. Per chunk of RL slots each lane loads ONE slot's (m, l) (shared with the
+  // row's other lanes by shuffles, not re-loaded by each) and its 4 dims of all RL partial O's:
+  // one round trip for up to RL slots (a group of 3 at 8 splits has 24), and the single
+  // combining CU moves half the bytes of a per-element (m, l) load.
+  constexpr int RL = D / 4;
+  const int per_m = G * RL;
   const int nm = __popc(mask);
-  // threads per element: 4 when the elements leave room (a lone sequence: 128 elements), else
-  // 1 (a group's last arrival usually combines every member: 3 x 128 elements on 512 threads)
-  const int lg = nm * per_m * 4 <= (int)blockDim.x ? 2 : (nm * per_m * 2 <= (int)blockDim.x ? 1 : 0);
-  const int tpi = 1 << lg;
-  const int sub = threadIdx.x & (tpi - 1);
-  for (int it = threadIdx.x >> lg; it < nm * per_m; it += blockDim.x >> lg) {
+  const int lr = threadIdx.x & (RL - 1);
+  const int lane0 = (threadIdx.x & 63) & ~(RL - 1);
+  for (int it = threadIdx.x; it < nm * per_m; it += blockDim.x) {   // rows are all-or-nothing
     const int k = it / per_m;
     int mm = 0;
     for (int bits = mask, c = 0;; bits &= bits - 1) {   // k-th member set in the mask
@@ -372,52 +383,40 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM>& 
       if (c++ == k) break;
     }
     const int w = it - k * per_m;
-    const int hj = w / (D / 4), d0 = 4 * (w - hj * (D / 4));
+    const int hj = w / RL, d0 = 4 * (w - hj * RL);
     const int row = mm * Hq + hj;
     float4_ O = {0.f, 0.f, 0.f, 0.f};
     float Mr = -INFINITY, Lr = 0.f;
-    for (int s0 = 0; s0 < nslots; s0 += 16 * tpi) {
-      float4_ vv[16], ml[16];
+    for (int s0 = 0; s0 < nslots; s0 += RL) {
+      const bool mine = s0 + lr < nslots;
+      const float4_ mlq = mine ? rt::sc1_load4(pml_rsrc, (row * stride + s0 + lr) * 16)
+                               : float4_{-INFINITY, 0.f, 0.f, 0.f};
+      float4_ vv[RL];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int sl = s0 + tpi * j + sub;
-        const bool ok = sl < nslots;
-        ml[j] = ok ? rt::sc1_load4(pml_rsrc, (row * stride + sl) * 16) : float4_{-INFINITY, 0.f, 0.f, 0.f};
-        vv[j] = ok ? rt::sc1_load4(po_rsrc, ((row * stride + sl) * D + d0) * 4) : float4_{0.f, 0.f, 0.f, 0.f};
-      }
-      float Mc = Mr;
+      for (int j = 0; j < RL; ++j)
+        vv[j] = s0 + j < nslots ? rt::sc1_load4(po_rsrc, ((row * stride + s0 + j) * D + d0) * 4)
+                                : float4_{0.f, 0.f, 0.f, 0.f};
+      float mc = mlq[1] > 0.f ? mlq[0] : -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (ml[j][1] > 0.f) Mc = fmaxf(Mc, ml[j][0]);
+      for (int x = 1; x < RL; x <<= 1) mc = fmaxf(mc, __shfl_xor(mc, x, 64));
+      const float Mc = fmaxf(Mr, mc);
       if (Mc == -INFINITY) continue;                 // every slot of this chunk was empty
       const float a = Mr == -INFINITY ? 0.f : exp2f(Mr - Mc);
       O *= a;
       Lr *= a;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (ml[j][1] > 0.f) {
-          const float f = exp2f(ml[j][0] - Mc);
+      for (int j = 0; j < RL; ++j) {
+        const float mj = __shfl(mlq[0], lane0 + j, 64), lj = __shfl(mlq[1], lane0 + j, 64);
+        if (lj > 0.f) {
+          const float f = exp2f(mj - Mc);
           O += f * vv[j];
-          Lr += f * ml[j][1];
+          Lr += f * lj;
         }
       }
       Mr = Mc;
     }
-    for (int x = 1; x < tpi; x <<= 1) {               // merge the sub-states (same wave, uniform tpi)
-      const float Mo = __shfl_xor(Mr, x, 64), Lo = __shfl_xor(Lr, x, 64);
-      float4_ Oo;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Oo[i] = __shfl_xor(O[i], x, 64);
-      const float Mn = fmaxf(Mr, Mo);
-      const float fa = Mr == -INFINITY ? 0.f : exp2f(Mr - Mn), fb = Mo == -INFINITY ? 0.f : exp2f(Mo - Mn);
-      O = O * fa + Oo * fb;
-      Lr = Lr * fa + Lo * fb;
-      Mr = Mn;
-    }
-    if (sub == 0) {
-      const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
-      store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
-    }
+    const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
+    store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
   }
   __syncthreads();
   return true;
