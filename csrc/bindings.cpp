@@ -59,6 +59,8 @@ void oneshot_destroy(int id);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
+int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows, int D, int swiglu,
+                            hipStream_t stream);
 
 
 namespace {
@@ -483,6 +485,14 @@ void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tens
                                        (int)(rope_heads * head_dim), (int)head_dim, swiglu ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "shuffle_weight: unsupported configuration (rc=", rc, ")");
 }
+void unshuffle_weight(torch::Tensor W, torch::Tensor Ws, int64_t rope_heads, int64_t head_dim, bool swiglu) {
+  check_bf16(W, "W");
+  check_bf16(Ws, "Ws");
+  TORCH_CHECK(W.dim() == 2 && Ws.numel() == W.numel(), "unshuffle_weight shapes");
+  const int rc = launch_unshuffle_weight(W.data_ptr(), Ws.data_ptr(), (int)W.size(0), (int)W.size(1),
+                                         (int)(rope_heads * head_dim), (int)head_dim, swiglu ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "unshuffle_weight: unsupported configuration (rc=", rc, ")");
+}
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -491,6 +501,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none());
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
         py::arg("rope_heads") = 0, py::arg("head_dim") = 0, py::arg("swiglu") = false);
+  m.def("unshuffle_weight", &unshuffle_weight, py::arg("W"), py::arg("Ws"), py::arg("rope_heads") = 0,
+        py::arg("head_dim") = 0, py::arg("swiglu") = false);
   m.def("decode_prep", &decode_prep);
   m.def("decode_layer", &decode_layer, py::arg("res"), py::arg("q"), py::arg("a"), py::arg("g"), py::arg("wqkv"),
         py::arg("wo"), py::arg("wgu"), py::arg("wd"), py::arg("positions"), py::arg("cos_sin"), py::arg("k_cache"),

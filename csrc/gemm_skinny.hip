@@ -65,7 +65,45 @@ __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restri
     Ws[i] = v;
   }
 }
+
+// Exact inverse of shuffle_kernel's permutation (gamma, if any, stays folded): the row-major
+// weight for the prefill GEMMs when only the shuffled copy is kept resident (70B on one GPU).
+__global__ void unshuffle_kernel(uint16_t* __restrict__ W, const short8* __restrict__ Ws, int N, int K, int rope_rows,
+                                 int D, int swiglu) {
+  const int nsteps = K / 32;
+  const int64_t total = (int64_t)(N / 16) * nsteps * 64;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(i & 63);
+    int64_t ts = i >> 6;
+    int h = 0;
+    if (swiglu) {
+      h = (int)(ts & 1);
+      ts >>= 1;
+    }
+    const int s = (int)(ts % nsteps);
+    const int64_t t = ts / nsteps;
+    int row = (int)(16 * t + (l & 15)) + h * (N / 2);
+    if (row < rope_rows) {
+      const int hh = row / D, p = row - hh * D;
+      row = hh * D + (p >> 1) + (p & 1) * (D >> 1);
+    }
+    const int k0 = 32 * s + 8 * (l >> 4);
+    *reinterpret_cast<short8*>(W + (size_t)row * K + k0) = Ws[i];
+  }
+}
 }  // namespace
+
+int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows, int D, int swiglu,
+                            hipStream_t stream) {
+  if (N % 16 || K % 32 || N <= 0 || K <= 0 || rope_rows > N || (rope_rows && (D <= 0 || D % 2)) ||
+      (swiglu && (N / 2) % 16))
+    return -1;
+  const int64_t total = (int64_t)(N / 16) * (K / 32) * 64;
+  const int64_t grid = (total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536;
+  hipLaunchKernelGGL(unshuffle_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (uint16_t*)W, (const short8*)Ws,
+                     N, K, rope_rows, D, swiglu);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
                        int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream) {

@@ -162,3 +162,23 @@ def test_debug_paging_checks():
         e.check_paging(torch.tensor([[16]], dtype=torch.int32), [])
     with _pt.raises(AssertionError):
         e.check_paging(torch.tensor([[0]], dtype=torch.int32), [16 * 32])
+
+
+def test_shuffled_only_residency_matches_dual():
+    """Dropping the row-major linears after shuffling (one weight copy resident) leaves the
+    unfused/prefill path numerically equal: it rebuilds each gamma-folded operand by the exact
+    inverse permutation (ops.unshuffle_weight) and normalizes with unit weights."""
+    from theroundtaible_amd.engine import Engine, EngineConfig
+    from theroundtaible_amd import ops
+    a = Engine(EngineConfig(model="tiny-llama-128", device="cpu", dtype="fp32", num_blocks=64, weights="random-full:5"))
+    b = Engine(EngineConfig(model="tiny-llama-128", device="cpu", dtype="fp32", num_blocks=64, weights="random-full:5"))
+    b.model.decode_weights(drop_originals=True)
+    assert b.model.shuffled_only and b.model.layers[0]["wqkv"] is None and b.model.w["lm_head"] is None
+    ids = a.encode_prompt("Een gedeelde sleutel voor de ronde tafel, graag. " * 4)
+    la = a.prefill([(a.kv.seq("k"), ids)])
+    lb = b.prefill([(b.kv.seq("k"), ids)])
+    assert torch.allclose(la, lb, atol=1e-4, rtol=1e-4)
+    # the inverse permutation is exact, rope-permuted qkv rows included
+    W = torch.randn(3 * 2 * 128, 64)
+    Ws = ops.shuffle_weight(W, None, rope_heads=4, head_dim=128)
+    assert torch.equal(ops.unshuffle_weight(Ws, rope_heads=4, head_dim=128), W)

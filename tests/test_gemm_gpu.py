@@ -173,3 +173,29 @@ def test_ring_gemm_experiment_matches(variant):
         ops.native().ring_gemm_exp(out, x, ops.shuffle_weight(W), grid, variant)
         want = x.float() @ W.float().t()
         assert torch.allclose(out.float(), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,K,rope,swiglu", [(6 * 128, 256, 4, False), (512, 4096, 0, True), (4096, 14336, 0, False)])
+def test_unshuffle_is_exact_inverse(N, K, rope, swiglu):
+    W = bf(N, K, seed=3)
+    Ws = ops.shuffle_weight(W, None, rope_heads=rope, head_dim=128 if rope else 0, swiglu=swiglu)
+    assert torch.equal(ops.unshuffle_weight(Ws, rope_heads=rope, head_dim=128 if rope else 0, swiglu=swiglu), W)
+
+
+def test_shuffled_only_residency_engine():
+    """One resident weight copy (shuffled; prefill unshuffles per GEMM) vs both copies: same
+    prefill logits (up to the folded-gamma rounding) and the same fused decode."""
+    from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
+    kw = dict(model="llama3-8b", weights="random-full:5", device=DEV, num_blocks=256,
+              model_overrides={"n_layers": 2})
+    a = Engine(EngineConfig(weight_residency="dual", **kw))
+    b = Engine(EngineConfig(weight_residency="shuffled", **kw))
+    assert b.model.shuffled_only and not a.model.shuffled_only
+    ids = a.encode_prompt("een enkele kopie van de gewichten in HBM " * 20)
+    la = a.prefill([(a.kv.seq("k"), ids)]).float()
+    lb = b.prefill([(b.kv.seq("k"), ids)]).float()
+    assert float(torch.nn.functional.cosine_similarity(la, lb, dim=-1).min()) > 0.999
+    sp = SamplingParams(temperature=0.0, max_new_tokens=6, ignore_eos=True, stop_on_consensus=False)
+    oa = a.run_turns([Turn("x", "hallo tafel " * 30, sp)])[0]
+    ob = b.run_turns([Turn("x", "hallo tafel " * 30, sp)])[0]
+    assert oa.error is None and ob.error is None and len(ob.ids) == 6

@@ -67,6 +67,9 @@ class EngineConfig:
     debug_checks: bool = False
     # wrap each turn as one user message with the checkpoint's chat template (checkpoint tokenizers only)
     chat_template: bool = True
+    # GPU weight copies: "dual" (row-major for prefill + shuffled for decode), "shuffled" (shuffled
+    # only; prefill unshuffles per GEMM into scratch), "auto" = dual when 2x weights <= 35% of HBM
+    weight_residency: str = "auto"
 
 
 @dataclass
@@ -109,16 +112,22 @@ class Engine:
             weights = materialize(self.cfg, ecfg.weights, self.device, self.dtype, self.tp)
             self.model = build_model(self.cfg, weights, self.device, self.dtype, self.tp)
             if self.on_gpu and hasattr(self.model, "decode_weights"):
-                # shuffled decode copies (+1x weight memory) before sizing the KV pool — only when they
-                # leave room for KV: a 70B knight on one GPU keeps the unfused (hipBLASLt) decode path
+                # shuffled decode copies before sizing the KV pool. Both layouts (+1x weight memory)
+                # when that leaves most of HBM to KV; otherwise shuffle in place and keep ONLY the
+                # shuffled weights (prefill unshuffles per GEMM): a 70B knight on one GPU keeps the
+                # fused decode path and ~140 GB of KV
                 wbytes = sum(t.numel() * t.element_size() for t in weights.values())
                 total = torch.cuda.get_device_properties(self.device).total_memory
-                if 2 * wbytes <= 0.7 * total:
-                    self.model.decode_weights()
-                else:
-                    self.model.use_fused = False
+                mode = ecfg.weight_residency
+                if mode == "auto":
+                    mode = "dual" if 2 * wbytes <= 0.35 * total else "shuffled"
+                del weights
+                self.model.decode_weights(drop_originals=(mode == "shuffled"))
+                self.weight_residency = mode
         if self.on_gpu and self.tp.size > 1:
             self.tp.setup_oneshot()      # K9: collective over the TP group; RCCL stays the fallback
+        if not hasattr(self, "weight_residency"):
+            self.weight_residency = "dual"
         self.load_s = time.perf_counter() - t0
         self.kv = self._alloc_kv()
         self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}

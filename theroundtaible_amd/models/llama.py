@@ -82,23 +82,69 @@ class LlamaModel:
     force_tp_path = False   # tests: run the tensor-parallel fused path at tp=1 (all-reduces are no-ops)
     _dec = None
 
-    def decode_weights(self):
-        """Fragment-shuffled, norm-folded copies of every linear for the fused decode path
-        (built lazily once; +1x weight memory, affordable on 288 GB HBM)."""
+    # shuffled-only residency: the row-major linears were dropped after shuffling (a knight whose
+    # weights do not fit twice, e.g. Llama-3-70B on one GPU); prefill GEMMs rebuild each row-major
+    # (gamma-folded) operand in a per-shape scratch buffer with ops.unshuffle_weight
+    shuffled_only = False
+    _scratch: Optional[Dict[tuple, torch.Tensor]] = None
+
+    # (name, folded norm, shuffle kwargs) of the linears the fused decode path streams
+    def _lin_specs(self):
+        return (("wqkv", "attn_norm", {"rope_heads": self.n_heads + self.n_kv_heads, "head_dim": self.head_dim}),
+                ("wo", None, {}), ("w_gate_up", "ffn_norm", {"swiglu": True}), ("w_down", None, {}))
+
+    def decode_weights(self, drop_originals: bool = False):
+        """Fragment-shuffled, norm-folded copies of every linear for the fused decode path (built
+        lazily once). Default: +1x weight memory, affordable on 288 GB HBM for 7-8B knights.
+        ``drop_originals``: shuffle one linear at a time and free its row-major tensor (peak +1
+        tensor), so only ONE copy of the weights stays resident (see :attr:`shuffled_only`)."""
         if self._dec is None:
             with torch.no_grad():
                 layers = []
                 for lw in self.layers:
-                    layers.append({
-                        "wqkv": ops.shuffle_weight(lw["wqkv"], lw["attn_norm"],
-                                                   rope_heads=self.n_heads + self.n_kv_heads,
-                                                   head_dim=self.head_dim),
-                        "wo": ops.shuffle_weight(lw["wo"]),
-                        "w_gate_up": ops.shuffle_weight(lw["w_gate_up"], lw["ffn_norm"], swiglu=True),
-                        "w_down": ops.shuffle_weight(lw["w_down"]),
-                    })
-                self._dec = {"layers": layers, "lm_head": ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])}
+                    d = {}
+                    for name, norm, kw in self._lin_specs():
+                        d[name] = ops.shuffle_weight(lw[name], lw[norm] if norm else None, **kw)
+                        if drop_originals:
+                            lw[name] = None
+                    layers.append(d)
+                lm = ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])
+                if drop_originals:
+                    for k in [k for k in self.w if k.startswith("layers.") and k.split(".", 2)[2] in
+                              ("wqkv", "wo", "w_gate_up", "w_down")] + ["lm_head"]:
+                        self.w[k] = None
+                    self.shuffled_only = True
+                    self._scratch = {}
+                    if self.device.type == "cuda":
+                        torch.cuda.empty_cache()
+                self._dec = {"layers": layers, "lm_head": lm}
         return self._dec
+
+    def _row_major(self, l: Optional[int], name: str) -> torch.Tensor:
+        """The row-major operand of a prefill / unfused GEMM: the resident tensor, or (shuffled-only
+        residency) the gamma-folded weight unshuffled into a scratch buffer reused per shape."""
+        if not self.shuffled_only:
+            return self.layers[l][name] if l is not None else self.w[name]
+        if l is None:
+            Ws, kw = self._dec["lm_head"], {}
+        else:
+            Ws = self._dec["layers"][l][name]
+            kw = next(k for n, _, k in self._lin_specs() if n == name)
+        key = tuple(Ws.shape)
+        buf = self._scratch.get(key)
+        if buf is None:
+            buf = self._scratch[key] = torch.empty_like(Ws)
+        return ops.unshuffle_weight(Ws, out=buf, **kw)
+
+    def _norm_w(self, l: Optional[int], name: str) -> torch.Tensor:
+        """Norm weight of the unfused path: ones when gamma is folded into the next linear."""
+        w = self.layers[l][name] if l is not None else self.w[name]
+        if self.shuffled_only:
+            ones = self._scratch.get(("ones", w.numel()))
+            if ones is None:
+                ones = self._scratch[("ones", w.numel())] = torch.ones_like(w)
+            return ones
+        return w
 
     accepts_hidden = True  # forward(..., hidden=) takes pre-gathered embedding rows (decode_prep)
 
@@ -184,21 +230,22 @@ class LlamaModel:
         for l, lw in enumerate(self.layers):
             if res is None:
                 res = h
-                x = ops.rms_norm(h, lw["attn_norm"], cfg.norm_eps)
+                x = ops.rms_norm(h, self._norm_w(l, "attn_norm"), cfg.norm_eps)
             else:
-                x, res = ops.fused_add_rms_norm(h, res, lw["attn_norm"], cfg.norm_eps)
-            qkv = F.linear(x, lw["wqkv"])
+                x, res = ops.fused_add_rms_norm(h, res, self._norm_w(l, "attn_norm"), cfg.norm_eps)
+            qkv = F.linear(x, self._row_major(l, "wqkv"))
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, kv.k_layer(l), kv.v_layer(l), meta.slot_mapping,
                                    self.n_heads, self.n_kv_heads, self.head_dim)
             a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)
-            h = tp.all_reduce(F.linear(a.reshape(T, -1), lw["wo"]))
-            x, res = ops.fused_add_rms_norm(h, res, lw["ffn_norm"], cfg.norm_eps)
-            g = ops.silu_and_mul(F.linear(x, lw["w_gate_up"]))
-            h = tp.all_reduce(F.linear(g, lw["w_down"]))
+            h = tp.all_reduce(F.linear(a.reshape(T, -1), self._row_major(l, "wo")))
+            x, res = ops.fused_add_rms_norm(h, res, self._norm_w(l, "ffn_norm"), cfg.norm_eps)
+            g = ops.silu_and_mul(F.linear(x, self._row_major(l, "w_gate_up")))
+            h = tp.all_reduce(F.linear(g, self._row_major(l, "w_down")))
         if meta.kind == "prefill" and meta.last_rows is not None:
             h = h.index_select(0, meta.last_rows)
             res = res.index_select(0, meta.last_rows)
-        x, _ = ops.fused_add_rms_norm(h, res.clone() if not res.is_cuda else res, self.w["final_norm"], cfg.norm_eps)
-        logits = F.linear(x, self.w["lm_head"])
+        x, _ = ops.fused_add_rms_norm(h, res.clone() if not res.is_cuda else res, self._norm_w(None, "final_norm"),
+                                      cfg.norm_eps)
+        logits = F.linear(x, self._row_major(None, "lm_head"))
         logits = tp.all_gather_last(logits)
         return logits[:, :cfg.vocab]

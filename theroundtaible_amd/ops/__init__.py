@@ -236,6 +236,25 @@ def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None, rope_h
     return ref.fold_gamma(W, gamma, rope_heads, head_dim)
 
 
+def unshuffle_weight(Ws: torch.Tensor, rope_heads: int = 0, head_dim: int = 0, swiglu: bool = False,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row-major weight back from a :func:`shuffle_weight` copy: the exact inverse permutation
+    (a folded RMSNorm gamma stays folded). Lets a knight keep ONLY the shuffled weights resident
+    and rebuild each prefill GEMM's row-major operand in a reused scratch buffer."""
+    if out is None:
+        out = torch.empty_like(Ws)
+    if _use_native(Ws):
+        native().unshuffle_weight(out, Ws, int(rope_heads), int(head_dim), bool(swiglu))
+        return out
+    if rope_heads:
+        inv = torch.empty(Ws.shape[0], dtype=torch.long)
+        inv[ref.rope_row_perm(Ws.shape[0], rope_heads, head_dim)] = torch.arange(Ws.shape[0])
+        out.copy_(Ws[inv])
+    else:
+        out.copy_(Ws)
+    return out
+
+
 def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: int = EPI_STORE,
                 res: Optional[torch.Tensor] = None, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
                 xout: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
