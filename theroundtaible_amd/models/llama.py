@@ -58,6 +58,7 @@ class LlamaModel:
         self.cos_sin = rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device)
         self.layers = [{k.split(".", 2)[2]: v for k, v in weights.items() if k.startswith(f"layers.{i}.")}
                        for i in range(cfg.n_layers)]
+        self.lm_rows = weights["lm_head"].shape[0]   # (vocab shard) rows of the lm_head
 
     @property
     def kv_heads_local(self) -> int:
@@ -74,7 +75,7 @@ class LlamaModel:
         cfg = self.cfg
         return (ids.is_cuda and 1 <= ids.shape[0] <= 16 and self.use_fused
                 and cfg.hidden % 32 == 0 and cfg.ffn % 32 == 0 and (cfg.n_heads * cfg.head_dim) % 32 == 0
-                and self.w["lm_head"].shape[0] % 16 == 0)
+                and self.lm_rows % 16 == 0)
 
     use_fused = True
     # one persistent launch per layer instead of five (csrc/decode_layer.hip)
