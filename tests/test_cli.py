@@ -96,3 +96,51 @@ def test_manifest_commands(project):
     assert main(["--quiet", "manifest", "deprecate", "feat-1", "--replaced-by", "feat-2"]) == 0
     m = json.load(open(project / ".roundtable" / "manifest.json"))
     assert m["features"][0]["status"] == "deprecated" and m["features"][0]["lead_knight"] == "manual"
+
+
+def _scripted(project, **script):
+    cfg = _init(project, model="tiny-llama", knights=3, max_new=64)
+    cfg["rules"]["max_rounds"] = 4
+    cfg["rules"]["round_mode"] = "parallel"
+    cfg["rules"]["prompt_layout"] = "shared"
+    cfg["engine"]["scripted_consensus"] = {"free_tokens": 6, "files": ["NEW:docs/besluit.md"], **script}
+    json.dump(cfg, open(project / ".roundtable" / "config.json", "w"), indent=2)
+    return cfg
+
+
+def _session(project):
+    sess = os.listdir(project / ".roundtable" / "sessions")
+    assert len(sess) == 1
+    return project / ".roundtable" / "sessions" / sess[0]
+
+
+def test_scripted_consensus_discuss_then_apply_dry_run(project):
+    """Engine knights with the forced consensus tail (knights/script.py): round 1 scores 6, round 2
+    scores 9 -> consensus after round 2 (early exit, scope, lead knight, chronicle); then
+    `apply --dry-run` parses the lead's forced RTDIFF/1 block and plans one in-scope NEW file."""
+    _scripted(project, scores=[6, 9])
+    assert run(["discuss", "Gedeelde KV per tafel", "--no-read-codebase", "--seed", "1"]) == 0
+    sp = _session(project)
+    st = json.load(open(sp / "status.json"))
+    assert st["consensus_reached"] is True and st["phase"] == "consensus_reached" and st["round"] == 2
+    assert st["allowed_files"] == ["NEW:docs/besluit.md"] and st["lead_knight"] in ("Claude", "Gemini", "GPT")
+    rounds = [json.loads(l) for l in open(sp / "rounds.jsonl")]
+    assert len(rounds) == 6 and all(r["consensus"] is not None for r in rounds)      # stopped after round 2
+    assert "Consensus in 2 round(s)" in open(project / ".roundtable" / "chronicle.md").read()
+    assert run(["apply", "--dry-run", "--yes"]) == 0
+    plan = json.load(open(sp / "apply-plan.json"))
+    assert [p["path"] for p in plan["planned"]] == ["docs/besluit.md"] and plan["planned"][0]["new_file"]
+    assert "+# Besluit van de ronde tafel" in plan["planned"][0]["diff"] and plan["skipped"] == []
+    assert not (project / "docs" / "besluit.md").exists()                            # dry run never writes
+    assert run(["apply", "--noparley", "--yes"]) == 0
+    assert (project / "docs" / "besluit.md").read_text().startswith("# Besluit van de ronde tafel")
+    man = json.load(open(project / ".roundtable" / "manifest.json"))
+    assert man["features"][-1]["status"] == "implemented" and man["features"][-1]["files"] == ["docs/besluit.md"]
+
+
+def test_scripted_unanimous_rejection(project):
+    _scripted(project, reject=True, reject_round=1)
+    assert run(["discuss", "Alles in een kernel", "--no-read-codebase", "--seed", "1"]) == 0
+    st = json.load(open(_session(project) / "status.json"))
+    assert st["consensus_reached"] is True and st["round"] == 1
+    assert "Unanimous rejection in 1 round(s)" in open(project / ".roundtable" / "chronicle.md").read()

@@ -61,3 +61,28 @@ def test_summon_and_apply_dry_run_on_gpu(gproject):
     rc = main(["--quiet", "apply", "--dry-run", "--yes"])
     assert rc in (0, 6)             # random weights: usually no parseable edit blocks (ValidationError = 6)
     assert (gproject / "mod.py").read_text() == before   # dry run never writes
+
+
+def test_scripted_consensus_summon_apply_dry_run_on_gpu(gproject):
+    """Config 4's path with a deterministic ending: summon (sequential, shared layout) on the GPU
+    engine, the knights' forced consensus tail agrees in round 1, and `apply --dry-run` plans the
+    lead knight's forced RTDIFF/1 edit: rc 0 and a non-empty planned diff."""
+    cfg = _init(gproject, "sequential")
+    cfg["rules"]["prompt_layout"] = "shared"
+    cfg["engine"]["scripted_consensus"] = {"free_tokens": 12, "scores": [9], "files": ["NEW:docs/besluit.md"]}
+    json.dump(cfg, open(gproject / ".roundtable" / "config.json", "w"), indent=2)
+    (gproject / "mod.py").write_text("def f():\n    return 1\n")
+    git = ["git", "-c", "user.email=t@example.invalid", "-c", "user.name=t"]
+    subprocess.run(git + ["init", "-q"], cwd=gproject, check=True)
+    subprocess.run(git + ["add", "-A"], cwd=gproject, check=True)
+    subprocess.run(git + ["commit", "-qm", "base"], cwd=gproject, check=True)
+    (gproject / "mod.py").write_text("def f():\n    return 2\n")
+    assert main(["--quiet", "summon", "--read-codebase"]) == 0
+    sess = os.listdir(gproject / ".roundtable" / "sessions")
+    sp = gproject / ".roundtable" / "sessions" / sess[0]
+    st = json.load(open(sp / "status.json"))
+    assert st["consensus_reached"] is True and st["round"] == 1 and st["allowed_files"] == ["NEW:docs/besluit.md"]
+    assert main(["--quiet", "apply", "--dry-run", "--yes"]) == 0
+    plan = json.load(open(sp / "apply-plan.json"))
+    assert plan["planned"] and plan["planned"][0]["path"] == "docs/besluit.md" and plan["planned"][0]["diff"]
+    assert not (gproject / "docs").exists()

@@ -253,6 +253,12 @@ def apply_command(args, ui: UI) -> int:
         written.append(rel)
 
     if dry:
+        # the plan is kept with the session (never in the project tree): review it, then apply for real
+        import json as _json
+        atomic_write_text(os.path.join(path, "apply-plan.json"), _json.dumps({
+            "lead_knight": lead, "created_at": iso_now(),
+            "planned": [{"path": rel, "new_file": old is None, "diff": _diff(rel, old, new)} for rel, old, new in plan],
+            "skipped": skipped}, indent=2, ensure_ascii=False) + "\n")
         ui.ok(f"\n  Dry run complete: {len(plan)} file(s) would be written, {len(skipped)} skipped. Nothing was written.")
         return 0
     if not plan and not written:

@@ -481,6 +481,7 @@ class Engine:
         t1 = time.perf_counter()
         gen, decode_steps = self.decode(seqs, turns, first, deadline=t_start + min(t.timeout_s for t in turns),
                                         groups=groups if any(g is not None for g in groups[0]) else None)
+        self._force_tails(seqs, turns, gen)
         self._sync()
         t2 = time.perf_counter()
         self.check_device_flags()
@@ -503,6 +504,23 @@ class Engine:
         self.stats["prefill_s"] += t1 - t0
         self.stats["decode_s"] += t2 - t1
         return outs
+
+    def _force_tails(self, seqs: Sequence[SeqState], turns: Sequence[Turn], gen: List[List[int]]) -> None:
+        """Teacher-force ``params.forced_tail`` after each turn's sampled tokens (scripted
+        consensus): prefill it like generated text, so the resident KV covers the whole reply
+        except its last token, as after a normal decode."""
+        items = []
+        for s, t, g in zip(seqs, turns, gen):
+            if not t.params.forced_tail:
+                continue
+            tail = self.tokenizer.encode(t.params.forced_tail)
+            feed = ([g[-1]] if g else []) + tail[:-1]
+            g.extend(tail)
+            if feed:
+                items.append((s, feed))
+        if items:
+            with trace.range("forced tail"):
+                self.prefill(items)
 
     def _sync(self):
         if self.on_gpu:

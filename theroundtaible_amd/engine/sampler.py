@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import hashlib
+from typing import Optional
 from dataclasses import dataclass
 
 
@@ -14,6 +15,8 @@ class SamplingParams:
     max_new_tokens: int = 512
     ignore_eos: bool = False
     stop_on_consensus: bool = True
+    # teacher-forced text appended after the sampled tokens (knights/script.py scripted consensus)
+    forced_tail: Optional[str] = None
 
     def seq_seed(self, seq_key: str) -> int:
         """Deterministic per (engine seed, knight): sample i of a knight depends only on (seed, knight, position)."""

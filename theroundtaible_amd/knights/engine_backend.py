@@ -14,6 +14,7 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union
 from ..engine.engine import Engine, EngineConfig, Turn
 from ..engine.sampler import SamplingParams
 from .base import KnightBackend, TurnRequest, TurnResult
+from .script import ConsensusScript
 
 ADAPTER_DISPLAY_NAMES = {
     "claude-cli": "Claude", "claude-api": "Claude", "gemini-cli": "Gemini", "gemini-api": "Gemini",
@@ -23,12 +24,13 @@ ADAPTER_DISPLAY_NAMES = {
 
 class EngineBackend(KnightBackend):
     def __init__(self, name: str, adapter_id: str, engine: Engine, params: SamplingParams,
-                 lock: Optional[threading.Lock] = None):
+                 lock: Optional[threading.Lock] = None, script: Optional[ConsensusScript] = None):
         self.name = name
         self.adapter_id = adapter_id
         self.engine = engine
         self.params = params
         self.lock = lock or threading.Lock()
+        self.script = script
 
     def group_key(self):
         return id(self.engine)
@@ -43,6 +45,11 @@ class EngineBackend(KnightBackend):
         p = self.params
         if req.max_new_tokens:
             p = SamplingParams(**{**p.__dict__, "max_new_tokens": int(req.max_new_tokens)})
+        if self.script is not None:   # scripted consensus: free tokens, then the forced tail
+            knight = req.seq_key.rsplit("/", 1)[-1].split(":", 1)[-1]
+            p = SamplingParams(**{**p.__dict__, "max_new_tokens": min(p.max_new_tokens, self.script.free_tokens),
+                                  "stop_on_consensus": False,
+                                  "forced_tail": self.script.tail(knight, req.round, req.seq_key)})
         return Turn(req.seq_key, req.prompt, p, timeout_s)
 
     def execute_group(self, pairs: Sequence[Tuple["EngineBackend", TurnRequest]],

@@ -19,6 +19,7 @@ from ..utils.ui import NULL_UI, UI
 from .base import KnightBackend
 from .engine_backend import ADAPTER_DISPLAY_NAMES, EngineBackend, EnginePool
 from .external import create_external, wants_external
+from .script import ConsensusScript
 from .fake import FakeBackend
 
 KNOWN_PREFIXES = ("claude-", "gemini-", "openai-", "local-llm", "engine", "fake")
@@ -93,7 +94,8 @@ class BackendFactory:
                                 max_new_tokens=int(st.get("max_new_tokens", 512)),
                                 ignore_eos=bool(st.get("ignore_eos", False)),
                                 stop_on_consensus=bool(st.get("stop_on_consensus", True)))
-        return EngineBackend(name, adapter_id, engine, params, lock)
+        return EngineBackend(name, adapter_id, engine, params, lock,
+                             script=ConsensusScript.from_config(st.get("scripted_consensus")))
 
     __call__ = create
 
