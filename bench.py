@@ -68,6 +68,10 @@ def parse():
                    help="fraction of free HBM for the KV pool (lower it when ranks share a GPU)")
     p.add_argument("--max-kv-tokens", type=int, default=None, help="cap the KV pool (tokens per engine)")
     p.add_argument("--device", default=None, help="override device (cpu for a plumbing run)")
+    p.add_argument("--consensus-round", type=int, default=0,
+                   help="scripted consensus (knights/script.py): after the free --new-tokens every knight's reply "
+                        "ends in a forced consensus JSON scoring 6, then 9 in this round, so the tables reach "
+                        "consensus and stop there (0 = off; use warmup + steps to end inside the timed region)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
 
@@ -146,7 +150,12 @@ def main() -> int:
                             ignore_eos=True, stop_on_consensus=False, seed=7)
     import threading
     lock = threading.Lock()
-    local = {n: EngineBackend(n, f"local-llm-{n.lower()}", engine, params, lock) for n in local_names}
+    script = None
+    if args.consensus_round:
+        from theroundtaible_amd.knights.script import ConsensusScript
+        script = ConsensusScript(free_tokens=args.new_tokens, scores=[6] * (args.consensus_round - 1) + [9],
+                                 files=["NEW:docs/besluit.md"])
+    local = {n: EngineBackend(n, f"local-llm-{n.lower()}", engine, params, lock, script=script) for n in local_names}
     pool = DistributedPool(cl, placement, local, engine.tokenizer)
     load_s = time.perf_counter() - t_load
 
@@ -173,7 +182,7 @@ def main() -> int:
                 torch.cuda.synchronize()
             cl.barrier()
             timing["t0"] = time.perf_counter()
-        if rnd == rounds:
+        if rnd == rounds or (args.consensus_round and rnd == args.consensus_round):
             if device.startswith("cuda"):
                 torch.cuda.synchronize()
             cl.barrier()
@@ -185,19 +194,22 @@ def main() -> int:
     runner = run_tables_parallel if args.round_mode == "parallel" else run_tables_sequential
     runner(orchs, [f"{TOPIC} (tafel {t})" for t in range(n_tables)], on_round=on_round)
     elapsed = cl.max_scalar(timing["t1"] - timing["t0"])
-    timed = range(args.warmup + 1, rounds + 1)
-    dec = pre = reused = 0
+    last = min(rounds, args.consensus_round) if args.consensus_round else rounds
+    timed = range(args.warmup + 1, last + 1)
+    dec = pre = reused = forced = 0
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
                 dec += int(e.metrics.get("decode_tokens", 0))
                 pre += int(e.metrics.get("prefill_tokens", 0))
                 reused += int(e.metrics.get("reused_tokens", 0))
+                forced += int(e.metrics.get("forced_tokens", 0))
     failures = [f for o in orchs for f in o.failures]
     if failures:
         print(f"[rank {cl.rank}] {len(failures)} failed knight turns; first: {failures[0]}", file=sys.stderr, flush=True)
-    exch = sum(pool.exchange_ms[-args.steps:]) / max(1, args.steps) if pool.exchange_ms else 0.0
-    ms_round = elapsed / max(1, args.steps) * 1e3
+    n_timed = max(1, len(timed))
+    exch = sum(pool.exchange_ms[-n_timed:]) / n_timed if pool.exchange_ms else 0.0
+    ms_round = elapsed / n_timed * 1e3
     value = dec / elapsed if elapsed > 0 else 0.0
     ref_bound_ms = kpt * 120_000.0
     out = {
@@ -219,7 +231,10 @@ def main() -> int:
                    "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
                    "kv_blocks_used_rank0": engine.kv.num_blocks - engine.kv.alloc.num_free,
-                   "kv_capacity_tokens": engine.kv_capacity_tokens},
+                   "kv_capacity_tokens": engine.kv_capacity_tokens,
+                   "consensus_round": args.consensus_round or None,
+                   "consensus_reached": sum(1 for o in orchs if o.result is not None and o.result.consensus),
+                   "forced_tokens": forced},
     }
     if cl.rank == 0:
         line = json.dumps(out)

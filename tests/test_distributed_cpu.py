@@ -193,3 +193,17 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="1"),
                        cwd=ROOT)
     assert r.returncode != 0 and "refusing" in (r.stdout + r.stderr)
+
+
+def test_bench_consensus_round_variant():
+    """bench.py --consensus-round K: scripted consensus ends the table in round K (inside the
+    timed region); forced tail tokens are reported apart from decoded ones."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--model", "tiny-llama", "--steps", "2",
+           "--warmup", "1", "--new-tokens", "8", "--consensus-round", "3"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"),
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    d = out["detail"]
+    assert d["consensus_reached"] == 1 and d["consensus_round"] == 3
+    assert d["decode_tokens"] == 3 * 8 * 2 and d["forced_tokens"] > 0

@@ -481,13 +481,13 @@ class Engine:
         t1 = time.perf_counter()
         gen, decode_steps = self.decode(seqs, turns, first, deadline=t_start + min(t.timeout_s for t in turns),
                                         groups=groups if any(g is not None for g in groups[0]) else None)
-        self._force_tails(seqs, turns, gen)
+        forced = self._force_tails(seqs, turns, gen)
         self._sync()
         t2 = time.perf_counter()
         self.check_device_flags()
         outs = []
         seen = set()
-        for t, s, g, n, d, key in zip(turns, seqs, gen, reused, deltas, keys):
+        for t, s, g, n, d, key, nf in zip(turns, seqs, gen, reused, deltas, keys, forced):
             text = self.tokenizer.decode(g)
             spre = 0
             if key is not None and key not in seen:     # the group's shared prefill, counted once
@@ -496,31 +496,34 @@ class Engine:
             outs.append(TurnOutput(text, g, {
                 "prompt_tokens": len(d) + n, "prefill_tokens": len(d) + spre, "reused_tokens": n,
                 "shared_tokens": sh_blocks.get(key, 0) * self.kv.block_size if key is not None else 0,
-                "decode_tokens": len(g), "prefill_ms": (t1 - t0) * 1e3, "decode_ms": (t2 - t1) * 1e3,
-                "decode_tok_s": len(g) / max(t2 - t1, 1e-9), "batch": len(turns),
+                "decode_tokens": len(g) - nf, "forced_tokens": nf, "prefill_ms": (t1 - t0) * 1e3,
+                "decode_ms": (t2 - t1) * 1e3, "decode_tok_s": (len(g) - nf) / max(t2 - t1, 1e-9), "batch": len(turns),
                 "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3}))
         self.stats["prefill_tokens"] += sum(len(d) for d in deltas) + sum(shared_pre.values())
-        self.stats["decode_tokens"] += sum(len(g) for g in gen)
+        self.stats["decode_tokens"] += sum(len(g) for g in gen) - sum(forced)
         self.stats["prefill_s"] += t1 - t0
         self.stats["decode_s"] += t2 - t1
         return outs
 
-    def _force_tails(self, seqs: Sequence[SeqState], turns: Sequence[Turn], gen: List[List[int]]) -> None:
+    def _force_tails(self, seqs: Sequence[SeqState], turns: Sequence[Turn], gen: List[List[int]]) -> List[int]:
         """Teacher-force ``params.forced_tail`` after each turn's sampled tokens (scripted
         consensus): prefill it like generated text, so the resident KV covers the whole reply
         except its last token, as after a normal decode."""
-        items = []
+        items, counts = [], []
         for s, t, g in zip(seqs, turns, gen):
             if not t.params.forced_tail:
+                counts.append(0)
                 continue
             tail = self.tokenizer.encode(t.params.forced_tail)
             feed = ([g[-1]] if g else []) + tail[:-1]
             g.extend(tail)
+            counts.append(len(tail))
             if feed:
                 items.append((s, feed))
         if items:
             with trace.range("forced tail"):
                 self.prefill(items)
+        return counts
 
     def _sync(self):
         if self.on_gpu:
