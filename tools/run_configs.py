@@ -128,8 +128,13 @@ class Shard{i}:
 '''
 
 
-def config4(files: int, new_tokens: int, model: str = "llama3-8b"):
-    """3-knight summon over a synthetic git diff with the codebase read (long context), then apply --dry-run."""
+def config4(files: int, new_tokens: int, model: str = "llama3-8b", scripted: bool = True):
+    """3-knight summon over a synthetic git diff with the codebase read (long context), then apply --dry-run.
+
+    ``scripted`` (default): the knights' replies end in the forced consensus tail (knights/script.py),
+    so the table agrees in round 1 and ``apply --dry-run`` plans the lead knight's RTDIFF/1 edit
+    (random weights alone never write a parseable block); the ``shared`` layout keeps one copy of
+    the ~11K-token summon context's KV for the three knights."""
     from theroundtaible_amd.cli import main
     root = tempfile.mkdtemp(prefix="rt-cfg4-")
     src = os.path.join(root, "src")
@@ -150,8 +155,10 @@ def config4(files: int, new_tokens: int, model: str = "llama3-8b"):
                               "min(self.items.values(), key=lambda e: (e.ttl, e.key))"))
     knights = [{"name": n, "adapter": a, "capabilities": ["x"], "priority": i + 1}
                for i, (n, a) in enumerate([("Claude", "claude-cli"), ("Gemini", "gemini-cli"), ("GPT", "openai-cli")])]
-    _write_project(root, _config(knights, {"default_model": model, "weights": "random:3",
-                                           "max_new_tokens": new_tokens, "ignore_eos": True}))
+    engine = {"default_model": model, "weights": "random:3", "max_new_tokens": new_tokens, "ignore_eos": True}
+    if scripted:
+        engine["scripted_consensus"] = {"free_tokens": new_tokens, "scores": [9], "files": ["NEW:docs/besluit.md"]}
+    _write_project(root, _config(knights, engine, {"prompt_layout": "shared"}))
     cwd = os.getcwd()
     os.chdir(root)
     try:
@@ -164,7 +171,13 @@ def config4(files: int, new_tokens: int, model: str = "llama3-8b"):
         os.chdir(cwd)
     path, rows = _session_metrics(root)
     prompt_tokens = sum(int(r.get("prefill_tokens", 0)) + int(r.get("reused_tokens", 0)) for r in rows)
+    plan = None
+    if path and os.path.exists(os.path.join(path, "apply-plan.json")):
+        with open(os.path.join(path, "apply-plan.json")) as f:
+            p = json.load(f)
+        plan = {"planned": [x["path"] for x in p["planned"]], "skipped": p["skipped"]}
     return {"config": 4, "desc": f"3-knight summon (synthetic diff, --read-codebase) + apply --dry-run, {model}",
+            "scripted_consensus": scripted, "apply_plan": plan,
             "rc_summon": rc1, "rc_apply": rc2, "summon_s": round(t1 - t0, 3), "apply_dry_run_s": round(t2 - t1, 3),
             "source_files": files, "turn_metrics": rows[-3:] if rows else [], "prompt_tokens_total": prompt_tokens}
 
@@ -176,10 +189,11 @@ def main_():
     ap.add_argument("--files", type=int, default=120, help="config 4: synthetic source files read into context")
     ap.add_argument("--new-tokens", type=int, default=256)
     ap.add_argument("--model", default="llama3-8b", help="config 4 model (tiny-llama for a CPU smoke run)")
+    ap.add_argument("--no-script", action="store_true", help="config 4: free replies only (no forced consensus)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     res = {1: config1, 2: lambda: config2(a.steps), 3: lambda: config3(a.steps),
-           4: lambda: config4(a.files, a.new_tokens, a.model)}[a.config]()
+           4: lambda: config4(a.files, a.new_tokens, a.model, not a.no_script)}[a.config]()
     line = json.dumps(res)
     print(line, flush=True)
     if a.out:
