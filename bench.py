@@ -156,7 +156,7 @@ def main() -> int:
         script = ConsensusScript(free_tokens=args.new_tokens, scores=[6] * (args.consensus_round - 1) + [9],
                                  files=["NEW:docs/besluit.md"])
     local = {n: EngineBackend(n, f"local-llm-{n.lower()}", engine, params, lock, script=script) for n in local_names}
-    pool = DistributedPool(cl, placement, local, engine.tokenizer)
+    pool = DistributedPool(cl, placement, local, engine.tokenizer, max_reply_tokens=args.new_tokens + 512)
     load_s = time.perf_counter() - t_load
 
     rounds = args.warmup + args.steps

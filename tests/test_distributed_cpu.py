@@ -79,6 +79,54 @@ def _exchange_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _static_exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from theroundtaible_amd.knights.base import TurnRequest, TurnResult
+        from theroundtaible_amd.knights.distributed import DistributedPool, RemoteKnight
+        from theroundtaible_amd.parallel.cluster import Cluster
+        c = Cluster(rank=rank, world=world, backend="gloo", cpu_group=dist.group.WORLD)
+
+        class Echo:   # local backend: replies with rank-dependent ids (rank 2's overflow the static width)
+            def __init__(self, n):
+                self.n = n
+
+            def group_key(self):
+                return self.n
+
+            def max_source_chars(self):
+                return None
+
+            def execute_group(self, pairs, timeout_s):
+                return [TurnResult("", list(range(12 if rank == 2 else 3 + rank)), "bpe", {}) for _ in pairs]
+
+        placement = {f"K{r}": [r] for r in range(world)}
+        pool = DistributedPool(c, placement, {f"K{rank}": Echo(rank)}, tokenizer=None, max_reply_tokens=8)
+        ks = [RemoteKnight(pool, f"K{r}", f"K{r}", "x") for r in range(world)]
+        res = pool.execute_round([(k, TurnRequest(k.name, "p")) for k in ks], 10.0)
+        q.put((rank, [r.ids for r in res]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_static_c1_exchange_with_overflow_fallback():
+    """Static-shape async C1 all-gather; a rank whose reply exceeds the static width makes every
+    rank join the shape-agreeing fallback, and all ranks still see every reply."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_static_exchange_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+    expect = [list(range(3)), list(range(4)), list(range(12))]
+    for r in range(3):
+        assert res[r] == expect
+
+
 def test_token_exchange_ragged():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -16,24 +16,29 @@ speaker's group computes while the others wait in the collective.
 from __future__ import annotations
 
 import time
-from typing import Dict, List, Optional, Sequence, Tuple, Union
+from typing import Dict, List, Optional, Sequence, Tuple, Union  # noqa: F401
 
 from ..errors import AdapterError
 from ..parallel.cluster import Cluster
-from ..parallel.exchange import exchange_token_ids
+from ..parallel.exchange import TokenExchange, exchange_token_ids
 from ..utils import trace
 from .base import KnightBackend, TurnRequest, TurnResult
 
 
 class DistributedPool:
     def __init__(self, cluster: Cluster, placement: Dict[str, List[int]], local: Dict[str, KnightBackend],
-                 tokenizer=None):
-        """``placement``: knight name -> ranks hosting it (first = leader). ``local``: name -> backend here."""
+                 tokenizer=None, max_reply_tokens: int = 4096):
+        """``placement``: knight name -> ranks hosting it (first = leader). ``local``: name -> backend here.
+        ``max_reply_tokens``: width of the static C1 buffers (longer replies take the shape-agreeing path)."""
         self.cluster = cluster
         self.placement = placement
         self.local = local
         self.tokenizer = tokenizer
         self.exchange_ms: List[float] = []
+        self.exchange: Optional[TokenExchange] = None
+        if cluster.distributed:
+            led = [sum(1 for r in placement.values() if r[0] == k) for k in range(cluster.world)]
+            self.exchange = TokenExchange(cluster, max(led), max_reply_tokens, cluster.device)
         budgets = [b.max_source_chars() for b in local.values()]
         mine = min([b for b in budgets if b is not None], default=200_000)
         self._src_budget = int(-cluster.max_scalar(-float(mine))) if cluster.distributed else mine
@@ -71,12 +76,25 @@ class DistributedPool:
                 if has_ids:
                     ids_contrib.append((i, list(o.ids)))
         with trace.range("C1 exchange"):
-            all_meta = self.cluster.all_gather_object(meta)
-            all_ids = exchange_token_ids(self.cluster, ids_contrib, self.cluster.device)
+            ex = self.exchange
+            if ex is None:
+                all_meta = self.cluster.all_gather_object(meta)
+                all_ids = exchange_token_ids(self.cluster, ids_contrib, self.cluster.device)
+            else:
+                # the static-shape token all-gather (RCCL) is in flight while the gloo metadata
+                # round runs; a rank whose replies overflow the static buffers says so in its
+                # metadata and every rank then joins the shape-agreeing fallback (collective)
+                fits = ex.fits(ids_contrib)
+                ex.start(ids_contrib if fits else [])
+                meta[-1] = not fits
+                all_meta = self.cluster.all_gather_object(meta)
+                all_ids = ex.wait()
+                if any(m.get(-1) for m in all_meta):
+                    all_ids.update(exchange_token_ids(self.cluster, [] if fits else ids_contrib, self.cluster.device))
         self.exchange_ms.append((time.perf_counter() - t0) * 1e3)
         merged: Dict[int, tuple] = {}
         for m in all_meta:
-            merged.update(m)
+            merged.update({k: v for k, v in m.items() if k != -1})
         results: List[Union[TurnResult, BaseException]] = []
         for i, (k, _) in enumerate(pairs):
             m = merged.get(i)

@@ -20,6 +20,44 @@ from .cluster import Cluster
 Contribution = List[Tuple[int, List[int]]]
 
 
+class TokenExchange:
+    """C1 with static shapes: every rank contributes a ``[rows, width]`` int32 buffer (rows = the
+    most knights any rank leads, from the placement; width = the reply-length cap + 2), so no
+    shape agreement round is needed. The all-gather is issued asynchronously (RCCL on GPUs, on
+    its own stream) and the caller overlaps it with the gloo metadata exchange and host work;
+    :meth:`wait` returns ``{slot: ids}``. Replies longer than the cap take :func:`exchange_token_ids`."""
+
+    def __init__(self, cluster: Cluster, rows: int, width: int, device: str):
+        self.cluster, self.rows, self.width = cluster, max(1, rows), width + 2
+        self.dev = device if cluster.backend == "nccl" else "cpu"
+        self._src = torch.full((self.rows, self.width), -1, dtype=torch.int32, device=self.dev)
+        self._out = torch.empty((cluster.world * self.rows, self.width), dtype=torch.int32, device=self.dev)
+        self._work = None
+
+    def fits(self, mine: Contribution) -> bool:
+        return len(mine) <= self.rows and all(len(ids) + 2 <= self.width for _, ids in mine)
+
+    def start(self, mine: Contribution) -> None:
+        buf = torch.full((self.rows, self.width), -1, dtype=torch.int32)
+        for r, (slot, ids) in enumerate(mine):
+            buf[r, 0] = slot
+            buf[r, 1] = len(ids)
+            if ids:
+                buf[r, 2:2 + len(ids)] = torch.tensor(ids, dtype=torch.int32)
+        self._src.copy_(buf, non_blocking=True)
+        self._work = dist.all_gather_into_tensor(self._out, self._src, async_op=True)
+
+    def wait(self) -> Dict[int, List[int]]:
+        self._work.wait()
+        self._work = None
+        res: Dict[int, List[int]] = {}
+        for row in self._out.cpu().tolist():
+            slot, n = row[0], row[1]
+            if slot >= 0:
+                res[slot] = row[2:2 + n]
+        return res
+
+
 def exchange_token_ids(cluster: Cluster, mine: Contribution, device: str) -> Dict[int, List[int]]:
     """All-gather ragged token-id lists keyed by request slot. Returns {slot: ids} for all ranks."""
     if not cluster.distributed:
