@@ -38,4 +38,6 @@ def project(tmp_path, monkeypatch):
     subprocess.run(["git", "init", "-q"], cwd=tmp_path, check=True)
     subprocess.run(["git", "config", "user.email", "t@t"], cwd=tmp_path, check=True)
     subprocess.run(["git", "config", "user.name", "t"], cwd=tmp_path, check=True)
+    if not _gpu_available():   # `init` scouts GPUs in a child process; CPU tests skip the probe
+        monkeypatch.setenv("ROUNDTABLE_FAKE_GPUS", '{"gpus": [], "links": {}}')
     return tmp_path

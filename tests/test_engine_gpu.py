@@ -189,3 +189,26 @@ def test_shared_layout_graph_equals_eager():
     oa, ob = a.run_turns(ta), b.run_turns(tb)
     assert [o.ids for o in oa] == [o.ids for o in ob]
     assert all(o.metrics["shared_tokens"] > 0 for o in oa)
+
+
+def test_heterogeneous_engines_share_gpu_concurrently():
+    """Two different models on one GPU: the pool splits the free HBM between their KV pools
+    after both loaded, and each engine runs on its own HIP stream from its own host thread —
+    same greedy tokens as running them one after the other."""
+    from concurrent.futures import ThreadPoolExecutor
+    from theroundtaible_amd.knights.engine_backend import EnginePool
+    pool = EnginePool()
+    cfgs = [EngineConfig(model=m, weights="random-full:3", device="cuda:0", max_kv_tokens=1 << 20)
+            for m in ("tiny-llama-128", "tiny-llama")]
+    engines = [pool.get(c, defer_kv=True)[0] for c in cfgs]
+    assert not any(e.kv_allocated for e in engines)
+    caps = pool.finalize()["cuda:0"]
+    assert len(caps) == 2 and all(c > 0 for c in caps)
+    assert engines[0].stream is not None and engines[0].stream != engines[1].stream
+    p = "Twee modellen, een GPU, twee streams. " * 6
+    solo = [e.run_turns([Turn("k", p, GREEDY)])[0].ids for e in engines]
+    for e in engines:
+        e.release("k")
+    with ThreadPoolExecutor(2) as ex:
+        both = list(ex.map(lambda e: e.run_turns([Turn("k", p, GREEDY)])[0].ids, engines))
+    assert both == solo

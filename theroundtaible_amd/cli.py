@@ -60,14 +60,16 @@ def confirm(ui: UI, question: str, default_yes: bool = True) -> bool:
 
 
 # ---- init ---------------------------------------------------------------------------------------
-def gpu_inventory() -> List[dict]:
-    """GPUs without initializing HIP in this process (device_count only; rocm-smi for HBM)."""
-    try:
-        import torch
-        n = torch.cuda.device_count()
-    except Exception:  # noqa: BLE001
-        n = 0
-    return [{"index": i} for i in range(n)]
+def gpu_inventory():
+    """GPU inventory (name, HBM, CUs, xGMI links) scouted in a child process, so this process
+    never initializes HIP (parallel/placement.py). ``ROUNDTABLE_FAKE_GPUS`` (a JSON inventory)
+    replaces the probe in tests."""
+    from .parallel.placement import Inventory, scout_gpus
+    fake = os.environ.get("ROUNDTABLE_FAKE_GPUS")
+    if fake:
+        import json as _json
+        return Inventory.from_json(_json.loads(fake))
+    return scout_gpus()
 
 
 CLI_TOOLS = {"claude-cli": "claude", "gemini-cli": "gemini", "openai-cli": "codex"}
@@ -135,8 +137,16 @@ def cmd_init(args, ui: UI) -> int:
     ui.dim(f"  Version: v{__version__}")
     project = args.project or (os.path.basename(root) if args.yes else ask(ui, f"  Project name? ({os.path.basename(root)})", os.path.basename(root)))
     language = args.language or ("nl" if args.yes else ask(ui, "  Discussion language? (nl)", "nl"))
-    gpus = gpu_inventory()
-    ui.ok(f"  Scouting complete: {len(gpus)} GPU(s) visible" + ("" if gpus else " — knights will run on CPU"))
+    inv = gpu_inventory()
+    gpus = inv.gpus
+    if gpus:
+        g = gpus[0]
+        xgmi = sum(1 for v in inv.links.values() if v == "XGMI")
+        ui.ok(f"  Scouting complete: {len(gpus)} x {g.name or 'GPU'} ({g.arch}), "
+              f"{g.hbm_bytes / (1 << 30):.0f} GiB HBM each, {g.cus} CUs"
+              + (f", {xgmi} xGMI link(s)" if inv.links else ""))
+    else:
+        ui.ok("  Scouting complete: 0 GPU(s) visible — knights will run on CPU")
     seats = [("Claude", "claude-cli"), ("Gemini", "gemini-cli"), ("GPT", "openai-cli")][:max(1, min(3, args.knights))]
     extra = max(0, args.knights - 3)
     knights = []
@@ -184,18 +194,36 @@ def cmd_init(args, ui: UI) -> int:
     if not knights:
         ui.error("\n  A roundtable with no knights is just a table.")
         return 0
-    for i, k in enumerate(knights):
-        eng = dict(local_engine.get(k["adapter"], {"model": args.model}), tp=args.tp)
-        if gpus:
-            g0 = (i * args.tp) % len(gpus)
-            eng["gpus"] = [(g0 + t) % len(gpus) for t in range(args.tp)]
-        else:
-            eng["device"] = "cpu"
-        adapter_engine[k["adapter"]] = eng
-    cfg = generate_config(project, language, knights,
-                          engine={"default_model": args.model, "weights": args.weights, "dtype": "bf16",
-                                  "max_new_tokens": args.max_new_tokens},
-                          adapter_engine=adapter_engine)
+    placement = None
+    if args.tp is not None or not gpus:
+        tp = args.tp or 1      # manual: knights dealt round-robin, tp consecutive GPUs each
+        for i, k in enumerate(knights):
+            eng = dict(local_engine.get(k["adapter"], {"model": args.model}), tp=tp)
+            if gpus:
+                g0 = (i * tp) % len(gpus)
+                eng["gpus"] = [(g0 + t) % len(gpus) for t in range(tp)]
+            else:
+                eng["device"] = "cpu"
+            adapter_engine[k["adapter"]] = eng
+    else:
+        # automatic placement: tp by memory fit + decode-step target, same-model knights together
+        from .parallel.placement import plan_placement
+        seats = [{"name": k["adapter"], **local_engine.get(k["adapter"], {"model": args.model})} for k in knights]
+        plans = plan_placement([{"name": s_["name"], "model": s_["model"], "overrides": s_.get("model_overrides")}
+                                for s_ in seats], inv)
+        for pl in plans:
+            for aid in pl.knights:
+                adapter_engine[aid] = dict(local_engine.get(aid, {"model": args.model}), tp=pl.tp, gpus=pl.gpus)
+            ui.ok(f"  Placement: {pl.model} x{len(pl.knights)} -> GPU {','.join(map(str, pl.gpus))} "
+                  f"(tp={pl.tp}, {pl.weight_gib_per_gpu} GiB weights/GPU, ~{pl.step_ms} ms/step: {pl.reason})")
+        placement = {"inventory": inv.to_json(),
+                     "groups": [{"model": pl.model, "tp": pl.tp, "gpus": pl.gpus, "adapters": pl.knights,
+                                 "reason": pl.reason} for pl in plans]}
+    eng_top = {"default_model": args.model, "weights": args.weights, "dtype": "bf16",
+               "max_new_tokens": args.max_new_tokens}
+    if placement is not None:
+        eng_top["placement"] = placement
+    cfg = generate_config(project, language, knights, engine=eng_top, adapter_engine=adapter_engine)
     for aid, ac in external.items():
         cfg["adapter_config"].setdefault(aid, {}).update(ac)
         if aid in adapter_engine and "endpoint" in ac:
@@ -217,7 +245,7 @@ def cmd_init(args, ui: UI) -> int:
     ui.ok("\n  TheRoundtAIble is ready.\n")
     ui.print(f"    Project:   {project}")
     ui.print(f"    Language:  {language}")
-    ui.print(f"    Knights:   {', '.join(k['name'] for k in knights)} ({args.model}, tp={args.tp})")
+    ui.print(f"    Knights:   {', '.join(k['name'] for k in knights)} ({args.model})")
     ui.dim('\n  The table is set. Run `roundtable discuss "your question"` to begin.\n')
     return 0
 
@@ -608,7 +636,8 @@ def build_parser() -> argparse.ArgumentParser:
     i.add_argument("--model", default="llama3-8b")
     i.add_argument("--weights", default="random:0")
     i.add_argument("--knights", type=int, default=3)
-    i.add_argument("--tp", type=int, default=1)
+    i.add_argument("--tp", type=int, default=None,
+                   help="tensor-parallel degree for every knight (default: automatic placement from the GPU scout)")
     i.add_argument("--max-new-tokens", type=int, default=512)
     i.add_argument("--local-models", action="store_true",
                    help="seat every detected local checkpoint (ROUNDTABLE_MODELS_DIR, ./models, HF cache)")

@@ -67,6 +67,10 @@ class EngineConfig:
     debug_checks: bool = False
     # wrap each turn as one user message with the checkpoint's chat template (checkpoint tokenizers only)
     chat_template: bool = True
+    # KV pool size in bytes (None: kv_cache_fraction of the free HBM at load); defer_kv: allocate on
+    # allocate_kv() / first turn (EnginePool.finalize splits a GPU between its engines)
+    kv_budget_bytes: Optional[int] = None
+    defer_kv: bool = False
     # GPU weight copies: "dual" (row-major for prefill + shuffled for decode), "shuffled" (shuffled
     # only; prefill unshuffles per GEMM into scratch), "auto" = dual when 2x weights <= 35% of HBM
     weight_residency: str = "auto"
@@ -129,7 +133,10 @@ class Engine:
         if not hasattr(self, "weight_residency"):
             self.weight_residency = "dual"
         self.load_s = time.perf_counter() - t0
-        self.kv = self._alloc_kv()
+        # every engine issues its work on its OWN HIP stream: engines of different models sharing a
+        # GPU run their batches concurrently (one host thread each, orchestrator.execute_plan)
+        self.stream = torch.cuda.Stream(self.device) if self.on_gpu else None
+        self._kv: Optional[PagedKVCache] = None if ecfg.defer_kv else self._alloc_kv()
         self.graphs: Dict[Tuple[int, int], "DecodeGraph"] = {}
         self._seg_cache: Dict[Tuple[str, str], List[int]] = {}
         self.healthy = True
@@ -151,6 +158,8 @@ class Engine:
         per_block = PagedKVCache.bytes_per_block(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, bs,
                                                  torch.finfo(self.dtype).bits // 8)
         nb = self.ecfg.num_blocks
+        if nb is None and self.ecfg.kv_budget_bytes is not None:
+            nb = max(64, int(self.ecfg.kv_budget_bytes) // per_block)
         if nb is None:
             if self.on_gpu:
                 free, _total = torch.cuda.mem_get_info(self.device)
@@ -162,6 +171,29 @@ class Engine:
             nb = min(nb, (self.ecfg.max_kv_tokens + bs - 1) // bs + self.ecfg.max_batch)
         return PagedKVCache(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, int(nb), bs,
                             self.device, self.dtype)
+
+    def allocate_kv(self, budget_bytes: Optional[int] = None) -> None:
+        """Deferred KV pool (``defer_kv``): sized by ``budget_bytes`` — EnginePool.finalize splits a
+        GPU's free HBM between the engines placed on it once all their weights are resident."""
+        if self._kv is None:
+            if budget_bytes is not None:
+                self.ecfg.kv_budget_bytes = int(budget_bytes)
+            self._kv = self._alloc_kv()
+
+    @property
+    def kv(self) -> PagedKVCache:
+        """The paged KV pool (allocated on first use when deferred)."""
+        if self._kv is None:
+            self.allocate_kv()
+        return self._kv
+
+    @property
+    def kv_allocated(self) -> bool:
+        return self._kv is not None
+
+    def kv_bytes_per_token(self) -> int:
+        return PagedKVCache.bytes_per_block(self.cfg.n_layers, self.model.kv_heads_local, self.cfg.head_dim, 1,
+                                            torch.finfo(self.dtype).bits // 8)
 
     @property
     def kv_capacity_tokens(self) -> int:
@@ -344,6 +376,9 @@ class Engine:
         self._calls += 1
         try:
             self._inject(call)
+            if self.stream is not None:
+                with torch.cuda.stream(self.stream):
+                    return self._run_turns(turns)
             return self._run_turns(turns)
         except KVCacheOOM as e:
             for t in turns:  # drop partial state; the knight re-prefills next time
@@ -527,7 +562,8 @@ class Engine:
 
     def _sync(self):
         if self.on_gpu:
-            torch.cuda.synchronize(self.device)
+            # this engine's stream only: another engine on the same GPU keeps running
+            (self.stream or torch.cuda.current_stream(self.device)).synchronize()
 
     def device_flag_errors(self) -> List[str]:
         """Read (and clear) the poll-expiry flags of the bounded device-side waits: the K9 one-shot

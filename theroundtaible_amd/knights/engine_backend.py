@@ -81,12 +81,38 @@ class EnginePool:
         self.engines: Dict[tuple, Engine] = {}
         self.locks: Dict[tuple, threading.Lock] = {}
 
-    def get(self, ecfg: EngineConfig) -> Tuple[Engine, threading.Lock]:
+    def get(self, ecfg: EngineConfig, defer_kv: bool = False) -> Tuple[Engine, threading.Lock]:
+        """``defer_kv``: load weights only; :meth:`finalize` sizes the KV pools afterwards."""
         key = (ecfg.model, ecfg.weights, ecfg.dtype, ecfg.device, ecfg.block_size)
         if key not in self.engines:
+            if defer_kv and ecfg.num_blocks is None and ecfg.kv_budget_bytes is None:
+                ecfg.defer_kv = True
             self.engines[key] = Engine(ecfg)
             self.locks[key] = threading.Lock()
         return self.engines[key], self.locks[key]
+
+    def finalize(self) -> Dict[str, List[int]]:
+        """Split each GPU's free HBM between the engines placed on it (once every engine's weights
+        are resident), instead of the first engine taking ``kv_cache_fraction`` of everything:
+        equal bytes per engine. Returns {device: [kv tokens per engine]}."""
+        import torch
+        by_dev: Dict[str, List[Engine]] = {}
+        for e in self.engines.values():
+            if not e.kv_allocated:
+                by_dev.setdefault(str(e.device), []).append(e)
+        out: Dict[str, List[int]] = {}
+        for dev, engines in by_dev.items():
+            if engines[0].on_gpu:
+                free, _ = torch.cuda.mem_get_info(engines[0].device)
+                frac = engines[0].ecfg.kv_cache_fraction
+                share = max(0, int(free * frac) - (2 << 30) * len(engines)) // len(engines)
+                for e in engines:
+                    e.allocate_kv(share)
+            else:
+                for e in engines:
+                    e.allocate_kv()
+            out[dev] = [e.kv_capacity_tokens for e in engines]
+        return out
 
     def close(self) -> None:
         self.engines.clear()

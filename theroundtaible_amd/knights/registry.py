@@ -48,6 +48,7 @@ class BackendFactory:
         self.device_override = device_override
         self._auto_next = 0
         self._auto: Dict[str, str] = {}
+        self.defer_kv = False    # initialize_backends: KV pools sized after every engine's weights load
 
     def _device_for(self, adapter_id: str, st: dict) -> str:
         if self.device_override:
@@ -88,7 +89,7 @@ class BackendFactory:
         if ecfg.device == "cpu":
             ecfg.dtype = "fp32" if st.get("dtype") in (None, "bf16") and st.get("cpu_fp32", True) else ecfg.dtype
             ecfg.use_graphs = False
-        engine, lock = self.pool.get(ecfg)
+        engine, lock = self.pool.get(ecfg, defer_kv=self.defer_kv)
         params = SamplingParams(temperature=float(st.get("temperature", 0.7)), top_p=float(st.get("top_p", 0.95)),
                                 top_k=int(st.get("top_k", 0)), seed=int(st.get("seed", 0)),
                                 max_new_tokens=int(st.get("max_new_tokens", 512)),
@@ -103,6 +104,7 @@ class BackendFactory:
 def initialize_backends(config: RoundtableConfig, ui: UI = NULL_UI,
                         factory: Optional[BackendFactory] = None) -> Dict[str, KnightBackend]:
     factory = factory or BackendFactory(config)
+    factory.defer_kv = True
     out: Dict[str, KnightBackend] = {}
     for knight in config.knights:
         if knight.adapter in out:
@@ -132,4 +134,7 @@ def initialize_backends(config: RoundtableConfig, ui: UI = NULL_UI,
                 ui.ok(f"  ✓ {knight.name} ready (fallback: {knight.fallback})")
                 continue
         ui.warn(f"  ✗ {knight.name} not available")
+    # every engine's weights are resident: split each GPU's free HBM between its engines' KV pools
+    factory.pool.finalize()
+    factory.defer_kv = False     # engines created later (runtime fallbacks) size their pool at once
     return out

@@ -32,6 +32,7 @@ from ..utils.ui import NULL_UI, UI
 from .distributed import DistributedPool, RemoteKnight
 from .engine_backend import EngineBackend
 from .registry import display_name
+from .script import ConsensusScript
 
 
 def plan_placement(config: RoundtableConfig, world: int) -> Dict[str, List[int]]:
@@ -98,7 +99,8 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
                                 max_new_tokens=int(max_new_tokens or st.get("max_new_tokens", 512)),
                                 ignore_eos=bool(st.get("ignore_eos", False)),
                                 stop_on_consensus=bool(st.get("stop_on_consensus", True)))
-        local[aid] = EngineBackend(display_name(aid, config), aid, engine, params, lock)
+        local[aid] = EngineBackend(display_name(aid, config), aid, engine, params, lock,
+                                   script=ConsensusScript.from_config(st.get("scripted_consensus")))
         ui.ok(f"  ✓ {k.name}: {st['model']} on rank(s) {ranks}" + (f" (tp={len(ranks)})" if len(ranks) > 1 else ""))
     if tokenizer is None:   # a rank hosting no knight still decodes exchanged ids
         from ..engine.tokenizer import get_tokenizer
