@@ -63,6 +63,9 @@ def parse():
                    help="packed (default): a table's knights share one GPU group (batched decode + shared prefix "
                         "KV); striped: knight j of table t on group (kpt*t + j) mod groups (every response "
                         "crosses xGMI, no KV sharing)")
+    p.add_argument("--layers", type=int, default=None,
+                   help="rehearsal only: override the model's layer count (reported in config.model)")
+    p.add_argument("--weight-residency", default="auto", choices=["auto", "dual", "shuffled"])
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--kv-fraction", type=float, default=0.85,
                    help="fraction of free HBM for the KV pool (lower it when ranks share a GPU)")
@@ -145,7 +148,9 @@ def main() -> int:
     engine = Engine(EngineConfig(model=args.model, weights=f"random:{1234}", device=device,
                                  use_graphs=not args.no_graphs and device != "cpu",
                                  dtype="bf16" if device != "cpu" else "fp32",
-                                 kv_cache_fraction=args.kv_fraction, max_kv_tokens=args.max_kv_tokens), tp)
+                                 kv_cache_fraction=args.kv_fraction, max_kv_tokens=args.max_kv_tokens,
+                                 weight_residency=args.weight_residency,
+                                 model_overrides={"n_layers": args.layers} if args.layers else {}), tp)
     params = SamplingParams(temperature=args.temperature, top_p=args.top_p, max_new_tokens=args.new_tokens,
                             ignore_eos=True, stop_on_consensus=False, seed=7)
     import threading
@@ -219,7 +224,8 @@ def main() -> int:
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "reference_bound_ms_per_round": ref_bound_ms, "speedup_vs_reference_bound": round(ref_bound_ms / ms_round, 1),
         "dtype": "bf16" if device != "cpu" else "fp32", "data": "synthetic prompts, random-init weights",
-        "config": {"model": args.model, "knights_per_table": kpt, "tables": n_tables, "knights": kpt * n_tables,
+        "config": {"model": args.model + (f" ({args.layers} layers, rehearsal)" if args.layers else ""),
+                   "knights_per_table": kpt, "tables": n_tables, "knights": kpt * n_tables,
                    "knights_per_gpu": args.knights_per_gpu, "new_tokens_per_turn": args.new_tokens,
                    "global_batch": kpt * n_tables, "seq_len": args.new_tokens,
                    "round_mode": args.round_mode, "prompt_layout": args.layout,

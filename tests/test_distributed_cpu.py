@@ -34,6 +34,8 @@ def _tp_worker(rank, world, port, model, q, overrides=None):
         logits = e.prefill([(e.kv.seq("k"), ids)])
         out = e.run_turns([Turn("k2", "tensor parallel", SamplingParams(temperature=0, max_new_tokens=6,
                                                                         ignore_eos=True, stop_on_consensus=False))])[0]
+        # greedy decode took the C3 (value, id) all-gather, not the full-logit gather
+        assert getattr(tp, "c3_greedy_calls", 0) >= 5, "distributed greedy argmax not used"
         if rank == 0:
             q.put((logits.tolist(), out.ids))
     finally:
@@ -43,7 +45,9 @@ def _tp_worker(rank, world, port, model, q, overrides=None):
 @pytest.mark.parametrize("model,tp,overrides", [("tiny-llama", 2, None), ("tiny-gpt2", 2, None),
                                                  ("tiny-llama", 4, {"n_kv_heads": 4})])
 def test_tp_matches_tp1(model, tp, overrides):
-    """TP=2/4 forward + greedy decode equal TP=1."""
+    """TP=2/4 forward + greedy decode equal TP=1; the TP decode samples
+    greedily with the per-rank argmax + (value, id) all-gather (C3), so identical tokens show the
+    distributed argmax matches the full-vocab one."""
     from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
     e = Engine(EngineConfig(model=model, device="cpu", dtype="fp32", num_blocks=64, weights="random-full:9",
                             model_overrides=dict(overrides or {})))

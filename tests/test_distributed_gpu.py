@@ -20,14 +20,14 @@ from test_distributed_cpu import ROOT, free_port
 pytestmark = pytest.mark.gpu
 
 
-def _bench(extra=()):
+def _bench(extra=(), nproc=2):
     # the ranks size their KV pools from free HBM: return what earlier in-process GPU tests cached
     gc.collect()
     torch.cuda.empty_cache()
     port = free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "16",
+           "--gpus", str(nproc), "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "16",
            "--temperature", "0", "--kv-fraction", "0.1", "--max-kv-tokens", "65536", *extra]
     env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
@@ -50,3 +50,15 @@ def test_two_rank_tp2_bench_on_shared_gpu():
     out = _bench(("--tp", "2", "--knights-per-table", "2", "--knights-per-gpu", "2"))
     assert "tp2" in out["config"]["parallelism"]
     assert out["detail"]["decode_tokens"] == 2 * 16 * 2, out["_log"]
+
+
+def test_four_rank_tp4_llama70b_shapes_on_shared_gpu():
+    """Config 5 rehearsal on one MI355X: 4 gloo ranks form one TP=4 group hosting 2 knights of a
+    Llama-3-70B-shaped model (hidden 8192, 64/8 heads -> 16/2 per rank, FFN 28672, 4 layers).
+    Exercises the column/row-parallel shards, K9 one-shot all-reduces between the ranks' IPC
+    buffers, C3's distributed greedy argmax and the C1 exchange."""
+    out = _bench(("--tp", "4", "--model", "llama3-70b", "--layers", "4", "--knights-per-table", "2",
+                  "--knights-per-gpu", "2", "--new-tokens", "8", "--kv-fraction", "0.05", "--max-kv-tokens", "32768",
+                  "--layout", "shared"), nproc=4)
+    assert "tp4" in out["config"]["parallelism"] and out["config"]["model"].startswith("llama3-70b")
+    assert out["detail"]["decode_tokens"] == 2 * 8 * 2 and out["detail"]["failed_turns"] == 0, out["_log"]

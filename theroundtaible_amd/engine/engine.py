@@ -668,7 +668,8 @@ class Engine:
         runner = None
         if self.on_gpu and self.ecfg.use_graphs:
             try:
-                runner = self._graph_for(B, max(s.length for s in seqs) + steps, grouped=groups is not None)
+                runner = self._graph_for(B, max(s.length for s in seqs) + steps, grouped=groups is not None,
+                                         dist_greedy=self.dist_greedy(turns))
             except RuntimeError as e:   # e.g. a collective that refuses stream capture: stay eager
                 if self.tp.size == 1:
                     raise
@@ -727,16 +728,20 @@ class Engine:
                                  max_group=ops.MAX_GROUP_COLS // G if groups is not None else 1) if self.on_gpu else None
         gt = self.group_table(groups, B)
         gt = gt.to(dev) if gt is not None and self.on_gpu else None
+        dist_greedy = self.dist_greedy(turns)
         for step in range(1, steps):
             pos = list(lens)
             slots = [s.blocks[p // self.kv.block_size] * self.kv.block_size + p % self.kv.block_size
                      for s, p in zip(seqs, pos)]
             meta = AttnMeta(kind="decode", slot_mapping=torch.tensor(slots, dtype=torch.int64, device=dev),
                             block_tables=bt, ctx_lens=torch.tensor([p + 1 for p in pos], dtype=torch.int32, device=dev),
-                            num_splits=splits, workspace=ws, groups=gt)
+                            num_splits=splits, workspace=ws, groups=gt, local_logits=dist_greedy)
             logits = self.model.forward(cur.to(dev), torch.tensor(pos, dtype=torch.int64, device=dev), self.kv, meta)
             offs = torch.tensor([p + 1 for p in pos], dtype=torch.int64, device=dev)
-            cur = ops.sample(logits.contiguous(), temp, top_p, top_k, seeds, offs)
+            if dist_greedy:
+                cur = self.tp.greedy_gather(logits, self.cfg.vocab)
+            else:
+                cur = ops.sample(logits.contiguous(), temp, top_p, top_k, seeds, offs)
             for b, x in enumerate(cur.tolist()):
                 out[b].append(int(x))
             lens = [l + 1 for l in lens]
@@ -754,14 +759,18 @@ class Engine:
         for s in seqs:
             self.kv.truncate(s, s.length)
 
-    def _graph_for(self, B: int, max_ctx: int, grouped: bool = False) -> "DecodeGraph":
+    def dist_greedy(self, turns: Sequence[Turn]) -> bool:
+        """TP knight decoding greedily: C3 moves (value, id) per rank instead of the logits."""
+        return self.tp.size > 1 and all(t.params.temperature <= 0 for t in turns)
+
+    def _graph_for(self, B: int, max_ctx: int, grouped: bool = False, dist_greedy: bool = False) -> "DecodeGraph":
         from .graphs import DecodeGraph
         bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
         splits = ops.decode_splits(bucket, self.model.n_kv_heads, grouped=grouped)
-        key = (bucket, splits, grouped)
+        key = (bucket, splits, grouped, dist_greedy)
         g = self.graphs.get(key)
         if g is None:
-            g = DecodeGraph(self, bucket, splits, grouped=grouped)
+            g = DecodeGraph(self, bucket, splits, grouped=grouped, dist_greedy=dist_greedy)
             self.graphs[key] = g
         return g
 

@@ -24,10 +24,11 @@ MAX_STEPS = 8192
 
 
 class DecodeGraph:
-    def __init__(self, engine, bucket: int, splits: int, grouped: bool = False):
+    def __init__(self, engine, bucket: int, splits: int, grouped: bool = False, dist_greedy: bool = False):
         self.engine = engine
         self.B = bucket
         self.splits = splits
+        self.dist_greedy = dist_greedy   # TP greedy: C3 all-gathers (value, id) per rank, not logits
         dev = engine.device
         kv = engine.kv
         self.bs = kv.block_size
@@ -78,12 +79,15 @@ class DecodeGraph:
             ops.paging_guard(self.block_tables, self.ctx_lens, self.positions, slots, self.guard_err,
                              e.kv.num_blocks, self.bs)
         meta = AttnMeta(kind="decode", slot_mapping=slots, block_tables=self.block_tables, ctx_lens=self.ctx_lens,
-                        num_splits=self.splits, workspace=self.ws, groups=self.groups)
+                        num_splits=self.splits, workspace=self.ws, groups=self.groups, local_logits=self.dist_greedy)
         if hidden is not None:
             logits = e.model.forward(self.input_ids, self.positions, e.kv, meta, hidden=hidden)
         else:
             logits = e.model.forward(self.input_ids, self.positions, e.kv, meta)
-        nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets)
+        if self.dist_greedy:
+            nxt = e.tp.greedy_gather(logits, e.cfg.vocab)
+        else:
+            nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets)
         # one epilogue launch: record ids, advance positions / lengths / step
         ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt)
 

@@ -74,7 +74,10 @@ class GPT2Model:
             h = h.index_select(0, meta.last_rows)
             res = res.index_select(0, meta.last_rows)
         x, _ = ops.fused_add_layer_norm(h, res, self.w["ln_f.w"], self.w["ln_f.b"], cfg.norm_eps)
-        logits = tp.all_gather_last(F.linear(x, self.lm_head))
+        logits = F.linear(x, self.lm_head)
+        if meta.kind == "decode" and meta.local_logits:
+            return logits
+        logits = tp.all_gather_last(logits)
         return logits[:, :cfg.vocab]
 
 

@@ -41,6 +41,7 @@ class AttnMeta:
     tile_map: Optional[torch.Tensor] = None     # prefill: [n_tiles, 2] int32
     last_rows: Optional[torch.Tensor] = None    # prefill: rows whose logits are needed
     groups: Optional[torch.Tensor] = None       # decode: [B, 3] shared-prefix groups (ops.decode_groups)
+    local_logits: bool = False                  # TP decode: return this rank's vocab shard (C3 greedy argmax)
 
 
 class LlamaModel:
@@ -213,6 +214,8 @@ class LlamaModel:
             cur = 1 - cur
             h = tp.all_reduce(ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_STORE))
         logits = ops.skinny_gemm(bufs[cur], dec["lm_head"], ops.PRO_NORM_ADD, ops.EPI_STORE, eps=eps, x2=h)
+        if meta.local_logits:
+            return logits
         logits = tp.all_gather_last(logits)
         return logits[:, :cfg.vocab]
 
@@ -248,5 +251,7 @@ class LlamaModel:
         x, _ = ops.fused_add_rms_norm(h, res.clone() if not res.is_cuda else res, self._norm_w(None, "final_norm"),
                                       cfg.norm_eps)
         logits = F.linear(x, self._row_major(None, "lm_head"))
+        if meta.kind == "decode" and meta.local_logits:
+            return logits
         logits = tp.all_gather_last(logits)
         return logits[:, :cfg.vocab]

@@ -72,6 +72,26 @@ class TPInfo:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return bool(int(t.item()))
 
+    def greedy_gather(self, local: torch.Tensor, vocab: int) -> torch.Tensor:
+        """C3 for greedy decoding without moving the logits: every rank takes the argmax of its
+        vocab shard, the group all-gathers ``[B, 2]`` (value, global id) and picks the best —
+        ``B * 8`` bytes per rank instead of ``B * V/tp * 4``. Ties resolve to the lowest id,
+        like an argmax over the gathered row. Returns ``[B]`` int64 ids on ``local``'s device."""
+        B, vs = local.shape
+        off = self.rank * vs
+        lim = max(0, min(vs, vocab - off))        # zero-padded vocab rows never win
+        val, idx = local[:, :lim].float().max(dim=1)
+        pair = torch.stack([val, (idx + off).float()], dim=1)
+        self.c3_greedy_calls = getattr(self, "c3_greedy_calls", 0) + 1
+        if self.size == 1:
+            return pair[:, 1].long()
+        src = pair.cpu() if self._host_staged(local) else pair
+        parts = [torch.empty_like(src) for _ in range(self.size)]
+        dist.all_gather(parts, src, group=self.group)
+        g = torch.stack(parts).to(local.device)            # [tp, B, 2]
+        best = g[..., 0].argmax(dim=0)                     # first max = lowest rank = lowest id
+        return g[best, torch.arange(B, device=local.device), 1].long()
+
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """Concatenate shards along the last dim (vocab-parallel logits)."""
         if self.size == 1:
