@@ -202,6 +202,13 @@ def main() -> int:
     last = min(rounds, args.consensus_round) if args.consensus_round else rounds
     timed = range(args.warmup + 1, last + 1)
     dec = pre = reused = forced = 0
+    # engine time per timed round (the slowest turn of the round: turns of one engine batch run
+    # together) vs the round's wall clock: the rest is host work (prompts, parse, files, C1)
+    eng_ms = {}
+    for o in orchs:
+        for e in o.all_rounds:
+            if e.round in timed:
+                eng_ms[e.round] = max(eng_ms.get(e.round, 0.0), float(e.metrics.get("turn_ms", 0.0)))
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
@@ -240,7 +247,9 @@ def main() -> int:
                    "kv_capacity_tokens": engine.kv_capacity_tokens,
                    "consensus_round": args.consensus_round or None,
                    "consensus_reached": sum(1 for o in orchs if o.result is not None and o.result.consensus),
-                   "forced_tokens": forced},
+                   "forced_tokens": forced,
+                   "engine_ms_per_round": round(sum(eng_ms.values()) / n_timed, 2),
+                   "host_ms_per_round": round(ms_round - sum(eng_ms.values()) / n_timed, 2)},
     }
     if cl.rank == 0:
         line = json.dumps(out)
