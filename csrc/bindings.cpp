@@ -6,6 +6,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 void launch_norm(void* out, const void* x, void* res, const void* w, const void* b, int rows, int H, float eps,
                  bool add, bool ln, hipStream_t stream);
 void launch_rope_cache(void* q_out, const void* qkv, const int64_t* positions, const float* cos_sin, void* k_cache,
@@ -59,6 +61,8 @@ void oneshot_destroy(int id);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
+int launch_kv_block_copy(void* k, void* v, const int* src, const int* dst, int n, int L, int num_blocks,
+                         int64_t block_elems, hipStream_t stream);
 int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows, int D, int swiglu,
                             hipStream_t stream);
 
@@ -493,6 +497,28 @@ void unshuffle_weight(torch::Tensor W, torch::Tensor Ws, int64_t rope_heads, int
                                          (int)(rope_heads * head_dim), (int)head_dim, swiglu ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "unshuffle_weight: unsupported configuration (rc=", rc, ")");
 }
+void kv_block_copy(torch::Tensor k, torch::Tensor v, torch::Tensor src, torch::Tensor dst) {
+  check_bf16(k, "k_cache");
+  check_bf16(v, "v_cache");
+  TORCH_CHECK(k.dim() == 3 && k.sizes() == v.sizes(), "caches must be [L, NB, block_elems]");
+  check_type(src, torch::kInt32, "src");
+  check_type(dst, torch::kInt32, "dst");
+  TORCH_CHECK(src.numel() == dst.numel(), "src/dst length");
+  const int64_t nb = k.size(1);
+  if (src.numel() == 0) return;
+  // host-side validation before the launch: every id in range, no duplicate destination
+  auto s = src.cpu(), d = dst.cpu();
+  std::vector<char> seen(nb, 0);
+  for (int64_t i = 0; i < s.numel(); ++i) {
+    const int a = s.data_ptr<int>()[i], b = d.data_ptr<int>()[i];
+    TORCH_CHECK(a >= 0 && a < nb && b >= 0 && b < nb, "kv_block_copy: block id out of range");
+    TORCH_CHECK(!seen[b], "kv_block_copy: duplicate destination block");
+    seen[b] = 1;
+  }
+  const int rc = launch_kv_block_copy(k.data_ptr(), v.data_ptr(), src.data_ptr<int>(), dst.data_ptr<int>(),
+                                      (int)src.numel(), (int)k.size(0), (int)nb, k.size(2), cur_stream());
+  TORCH_CHECK(rc == 0, "kv_block_copy: unsupported configuration (rc=", rc, ")");
+}
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -501,6 +527,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none());
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
         py::arg("rope_heads") = 0, py::arg("head_dim") = 0, py::arg("swiglu") = false);
+  m.def("kv_block_copy", &kv_block_copy, py::arg("k"), py::arg("v"), py::arg("src"), py::arg("dst"));
   m.def("unshuffle_weight", &unshuffle_weight, py::arg("W"), py::arg("Ws"), py::arg("rope_heads") = 0,
         py::arg("head_dim") = 0, py::arg("swiglu") = false);
   m.def("decode_prep", &decode_prep);

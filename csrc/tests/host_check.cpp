@@ -20,6 +20,10 @@ int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int6
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
                           const int64_t* next, int B, int max_steps, hipStream_t stream);
 int prefill32_rows(int G);
+int launch_kv_block_copy(void* k, void* v, const int* src, const int* dst, int n, int L, int num_blocks,
+                         int64_t block_elems, hipStream_t stream);
+int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows, int D, int swiglu,
+                            hipStream_t stream);
 
 static int failures = 0;
 #define EXPECT(cond)                                                   \
@@ -59,6 +63,14 @@ int main() {
   static const int grp[3] = {0, 1, 0};
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 32, 8,
                              128, 4, 0.1f, 4, grp, 2, nullptr) == -4);   // group slots < splits
+  // K8 block copy: empty list launches nothing; unaligned block size / empty layer set refused
+  EXPECT(launch_kv_block_copy(nullptr, nullptr, nullptr, nullptr, 0, 32, 16, 8192, nullptr) == 0);
+  EXPECT(launch_kv_block_copy(nullptr, nullptr, nullptr, nullptr, 2, 32, 16, 8190, nullptr) == -1);
+  EXPECT(launch_kv_block_copy(nullptr, nullptr, nullptr, nullptr, 2, 0, 16, 8192, nullptr) == -1);
+  // weight unshuffle: N%16, K%32, rope rows beyond N
+  EXPECT(launch_unshuffle_weight(nullptr, nullptr, 24, 64, 0, 0, 0, nullptr) == -1);
+  EXPECT(launch_unshuffle_weight(nullptr, nullptr, 32, 48, 0, 0, 0, nullptr) == -1);
+  EXPECT(launch_unshuffle_weight(nullptr, nullptr, 32, 64, 64, 128, 0, nullptr) == -1);
   EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 2, 0, 16, 32, nullptr) == -1);
   EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 0, 4, 16, 32, nullptr) == 0);
   EXPECT(launch_decode_advance(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 8, nullptr) == 0);

@@ -22,7 +22,7 @@ def test_launcher_validation_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "host_check")
     srcs = [os.path.join(CSRC, "tests", "host_check.cpp")] + [
         os.path.join(CSRC, f) for f in ("gemm_skinny.hip", "attention_decode.hip", "attention_prefill32.hip",
-                                         "decode_step.hip")]
+                                         "decode_step.hip", "kv_copy.hip")]
     cmd = [HIPCC, "--offload-arch=gfx950", "-O1", "-g", "-std=c++17",
            "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
            "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined",

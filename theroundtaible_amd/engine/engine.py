@@ -290,8 +290,8 @@ class Engine:
     def release(self, key: str) -> None:
         self.kv.free_seq(key)
 
-    def fork(self, src: str, dst: str) -> None:
-        self.kv.fork(src, dst)
+    def fork(self, src: str, dst: str, copy: bool = False) -> None:
+        self.kv.fork(src, dst, copy=copy)
 
     # ---- forward helpers -----------------------------------------------------------------------
     def _max_blocks(self) -> int:

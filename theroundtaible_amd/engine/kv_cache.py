@@ -110,10 +110,15 @@ class PagedKVCache:
     def _cow_tail(self, s: SeqState) -> None:
         old = s.blocks[-1]
         new = self.alloc.alloc()
-        self.k[:, new].copy_(self.k[:, old])
-        self.v[:, new].copy_(self.v[:, old])
+        self.copy_blocks([old], [new])
         self.alloc.release(old)
         s.blocks[-1] = new
+
+    def copy_blocks(self, src: List[int], dst: List[int]) -> None:
+        """K8 (csrc/kv_copy.hip): whole-block copies across every layer of K and V, one launch."""
+        from .. import ops
+        ops.kv_block_copy(self.k.view(self.n_layers, self.num_blocks, -1),
+                          self.v.view(self.n_layers, self.num_blocks, -1), src, dst)
 
     def truncate(self, s: SeqState, n_tokens: int) -> None:
         n_tokens = max(0, min(n_tokens, s.length))
@@ -129,10 +134,17 @@ class PagedKVCache:
             for b in s.blocks:
                 self.alloc.release(b)
 
-    def fork(self, src: str, dst: str) -> SeqState:
-        """Share ``src``'s blocks with a new sequence ``dst`` (prefix sharing; K8 analogue)."""
+    def fork(self, src: str, dst: str, copy: bool = False) -> SeqState:
+        """``dst`` starts as ``src``. Default: share the blocks (refcounted prefix sharing; a writer
+        copies-on-write its tail). ``copy=True``: a deep snapshot in fresh blocks (K8 batch copy),
+        e.g. a continuation branch that must survive the live sequence being rolled back."""
         self.free_seq(dst)
         a = self.seqs[src]
+        if copy:
+            new = [self.alloc.alloc() for _ in a.blocks]
+            self.copy_blocks(list(a.blocks), new)
+            b = self.seqs[dst] = SeqState(dst, list(a.tokens), new)
+            return b
         b = self.seqs[dst] = SeqState(dst, list(a.tokens), list(a.blocks))
         for blk in b.blocks:
             self.alloc.incref(blk)

@@ -236,6 +236,21 @@ def shuffle_weight(W: torch.Tensor, gamma: Optional[torch.Tensor] = None, rope_h
     return ref.fold_gamma(W, gamma, rope_heads, head_dim)
 
 
+def kv_block_copy(k: torch.Tensor, v: torch.Tensor, src, dst) -> None:
+    """K8: copy whole KV blocks ``src[i] -> dst[i]`` in every layer of both caches (``[L, NB, E]``)
+    in one launch (csrc/kv_copy.hip); CPU: indexed copies."""
+    if not src:
+        return
+    if _use_native(k):
+        s_t = torch.tensor(list(src), dtype=torch.int32, device=k.device)
+        d_t = torch.tensor(list(dst), dtype=torch.int32, device=k.device)
+        native().kv_block_copy(k, v, s_t, d_t)
+        return
+    si, di = torch.tensor(list(src)), torch.tensor(list(dst))
+    k[:, di] = k[:, si]
+    v[:, di] = v[:, si]
+
+
 def unshuffle_weight(Ws: torch.Tensor, rope_heads: int = 0, head_dim: int = 0, swiglu: bool = False,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Row-major weight back from a :func:`shuffle_weight` copy: the exact inverse permutation
