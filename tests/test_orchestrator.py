@@ -200,3 +200,44 @@ def test_sequential_visibility_within_round(tmp_path):
     o = Orchestrator(config(n=2, max_rounds=1, mode="sequential"), bk, str(tmp_path))
     run_tables_sequential([o], ["T"])
     assert "EERSTE-ANTWOORD-XYZ" in seen["Gemini"] and "EERSTE-ANTWOORD-XYZ" not in seen["Claude"]
+
+
+@pytest.mark.parametrize("mode", ["parallel", "sequential"])
+def test_shared_layout_prompts_share_a_growing_prefix(tmp_path, mode):
+    """`shared` layout: every knight's prompt of a round starts with the same shared segments
+    (header + context + transcript), each ends in a one-line suffix naming the speaker, and the
+    shared prefix only grows across rounds (pure append for the engine's shared sequence)."""
+    sc = {k: [consensus_reply(5, f"{k} ronde {r}") for r in (1, 2, 3)] for k in ("Claude", "Gemini", "GPT")}
+    b = backends(sc)
+    Orchestrator(config(n=3, max_rounds=3, layout="shared", mode=mode), b, str(tmp_path),
+                 options=RunOptions(shuffle_seed=0)).run("T")
+    shared = []
+    for k in ("Claude", "Gemini", "GPT"):
+        for req_prompt in [p for _, p in b[f"fake-{k.lower()}"].prompt_objs]:
+            assert req_prompt.shared_key and req_prompt.shared_segments > 0
+            head = "".join(s.text for s in req_prompt.segments[:req_prompt.shared_segments])
+            tail = "".join(s.text for s in req_prompt.segments[req_prompt.shared_segments:])
+            assert f"jij bent {k}" in tail and len(tail) < 200
+            shared.append(head)
+    by_len = sorted(set(shared), key=len)
+    for a, c in zip(by_len, by_len[1:]):
+        assert c.startswith(a)                     # one growing prefix for the whole table
+    if mode == "parallel":                         # a round's three prompts share the same prefix
+        assert len(set(shared)) == 3
+
+
+def test_shared_layout_continuation_keeps_prefix(tmp_path):
+    """King's send-back with the shared layout: the continuation's prompts extend the first
+    session's shared prefix (transcript + KING demand), so the engine re-prefills only the delta."""
+    sc = {k: [consensus_reply(4)] * 4 for k in ("Claude", "Gemini")}
+    b = backends(sc)
+    o = Orchestrator(config(n=2, max_rounds=1, layout="shared", mode="parallel"), b, str(tmp_path),
+                     options=RunOptions(shuffle_seed=0))
+    res = o.run("T")
+    first = [p for _, p in b["fake-claude"].prompt_objs][-1]
+    cont = ContinueOptions(res.session_path, res.all_rounds, res.rounds + 1)
+    o.run("T", continue_from=cont)
+    nxt = [p for _, p in b["fake-claude"].prompt_objs][-1]
+    h1 = "".join(s.text for s in first.segments[:first.shared_segments])
+    h2 = "".join(s.text for s in nxt.segments[:nxt.shared_segments])
+    assert h2.startswith(h1) and "THE KING HAS SENT YOU BACK" in h2[len(h1):]

@@ -39,6 +39,7 @@ class FakeBackend(KnightBackend):
         self.max_chars = max_chars
         self.calls: Dict[str, int] = defaultdict(int)
         self.prompts: List[Tuple[str, str]] = []
+        self.prompt_objs: List[Tuple[str, object]] = []   # the Prompt objects (segments, shared split)
 
     def is_available(self) -> bool:
         return self.available
@@ -52,6 +53,7 @@ class FakeBackend(KnightBackend):
         self.calls[seq_key] += 1
         text = prompt_text(prompt)
         self.prompts.append((seq_key, text))
+        self.prompt_objs.append((seq_key, prompt))
         fault = self.faults.get((seq_key, idx))
         if fault == "hang":
             time.sleep(min(timeout_s, 0.05))
