@@ -79,6 +79,7 @@ def bench_gemm(M):
         ("gate_up (norm+swiglu)", 2 * ffn, hid),
         ("down (+resid)", hid, ffn),
         ("lm_head (norm)", vocab, hid),
+        ("gate_up-plain (norm, unpaired)", 2 * ffn, hid),
     ]
     for name, N, K in shapes:
         nbytes = N * K * 2
