@@ -40,3 +40,19 @@ def test_code_red_command_with_fake_doctors(project):
         fake.FakeBackend.__init__ = orig
     log = open(project / ".roundtable" / "error-log.md").read()
     assert "## CR-001 [OPEN] — login crasht" in log and "**Root cause:** race-in-cache" in log
+
+
+def test_code_red_on_engine_doctors_with_scripted_verdicts(project):
+    """code-red with engine-hosted doctors: the scripted tail gives every doctor the same
+    root_cause_key at confidence 6 in triage and 9 from round 2 -> convergence after the
+    blind round, logged OPEN as CR-001 in error-log.md."""
+    import json
+    from theroundtaible_amd.cli import main
+    assert main(["--quiet", "init", "--yes", "--model", "tiny-llama", "--knights", "3", "--max-new-tokens", "16"]) == 0
+    p = project / ".roundtable" / "config.json"
+    cfg = json.load(open(p))
+    cfg["engine"]["scripted_consensus"] = {"free_tokens": 4}
+    json.dump(cfg, open(p, "w"), indent=2)
+    assert main(["--quiet", "code-red", "decode hangt na 40K tokens", "--no-read-codebase"]) == 0
+    log = (project / ".roundtable" / "error-log.md").read_text()
+    assert "CR-001" in log and "OPEN" in log and "kv-cache-exhausted" in log
