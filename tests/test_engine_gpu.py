@@ -99,6 +99,39 @@ def test_serve_on_gpu_batches_requests():
         srv.close()
 
 
+def test_serve_on_gpu_shared_system_prompt_grouped_decode():
+    """Concurrent clients with one system prompt: its KV is resident once, and their batched
+    decode runs the grouped (shared-prefix) hipGraph."""
+    import json
+    import threading
+    import urllib.request
+    from theroundtaible_amd.serve import build_server
+    srv = build_server("tiny-llama-128", weights="random:2", device="cuda:0", port=0, max_batch=4, max_tokens=8,
+                       num_blocks=512).start()
+    sys_prompt = "Een lange gedeelde systeemprompt voor alle clients. " * 30
+    try:
+        codes = []
+
+        def go(i):
+            req = urllib.request.Request(srv.url + "/v1/chat/completions", method="POST",
+                                         headers={"Content-Type": "application/json"},
+                                         data=json.dumps({"messages": [{"role": "system", "content": sys_prompt},
+                                                                       {"role": "user", "content": f"q{i}"}],
+                                                          "max_tokens": 8, "user": f"u{i}"}).encode())
+            with urllib.request.urlopen(req, timeout=120) as r:
+                codes.append(r.status)
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert codes == [200] * 4
+        assert any(k.startswith("@shared:sys:") for k in srv.engine.kv.seqs)
+        assert any(key[2] for key in srv.engine.graphs)          # a grouped decode graph was used
+    finally:
+        srv.close()
+
+
 def test_debug_paging_guard_in_decode_graph():
     """ROUNDTABLE_DEBUG_CHECKS: the captured step validates its own paging metadata on the device.
     Normal decoding never trips it; corrupted graph state does, at the next host sync point."""

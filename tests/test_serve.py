@@ -125,3 +125,51 @@ def test_continuous_batching_admits_midflight(server):
         t.join()
     assert server.sched.stats["admitted_midflight"] > before
     assert done["kort"] < done["lang"]
+
+
+def test_shared_system_prompt_kv(server):
+    """Clients sending the same system prompt share one resident copy of its KV: the shared
+    sequence holds it, each request's sequence references its full blocks, and greedy answers
+    equal those of a server that does not share."""
+    sys_prompt = "Je bent een knight van de ronde tafel. " * 30
+    body = lambda u: {"messages": [{"role": "system", "content": sys_prompt}, {"role": "user", "content": u}],
+                      "max_tokens": 6, "temperature": 0, "user": f"deel-{u}"}
+    outs = [json.loads(_post(server.url + "/v1/chat/completions", body(u))[1]) for u in ("een", "twee")]
+    e = server.engine
+    shared = [k for k in e.kv.seqs if k.startswith("@shared:sys:")]
+    assert shared, "no shared system-prompt sequence"
+    sq = e.kv.seqs[shared[0]]
+    full = sq.length // e.kv.block_size
+    assert full >= 2
+    for u in ("een", "twee"):
+        s = e.kv.seqs[f"session:deel-{u}"]
+        assert s.blocks[:full] == sq.blocks[:full]
+    plain = build_server("tiny-llama", weights="random:1", device="cpu", port=0, max_batch=4, max_tokens=8,
+                         num_blocks=256)
+    plain.share_system_prompts = False
+    plain.start()
+    try:
+        ref = [json.loads(_post(plain.url + "/v1/chat/completions", body(u))[1]) for u in ("een", "twee")]
+    finally:
+        plain.close()
+    assert [o["choices"][0]["message"]["content"] for o in outs] == \
+        [o["choices"][0]["message"]["content"] for o in ref]
+
+
+def test_shared_system_prompt_concurrent_batch(server):
+    sys_prompt = "Gedeelde systeemprompt voor iedereen. " * 25
+    res, errs = [], []
+
+    def go(i):
+        try:
+            res.append(_post(server.url + "/v1/chat/completions",
+                             {"messages": [{"role": "system", "content": sys_prompt},
+                                           {"role": "user", "content": f"vraag {i}"}], "max_tokens": 5})[0])
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=go, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and res == [200] * 4

@@ -260,10 +260,22 @@ class Engine:
     def shared_seq_key(key: str) -> str:
         return "@shared:" + key
 
+    MAX_SHARED_SEQS = 64   # resident shared prefixes (tables, system prompts); LRU beyond
+
     def sync_shared(self, key: str, shared: List[int]) -> Tuple[SeqState, List[int]]:
         """Roll the table's shared sequence back to its LCP with ``shared``; return (seq, delta to
-        prefill). The shared sequence is never decoded: it only holds the common KV blocks."""
-        s = self.kv.seq(self.shared_seq_key(key))
+        prefill). The shared sequence is never decoded: it only holds the common KV blocks.
+        Least-recently-used shared sequences beyond ``MAX_SHARED_SEQS`` are released (blocks a
+        member still references stay alive through their refcount)."""
+        sk = self.shared_seq_key(key)
+        lru = self.__dict__.setdefault("_shared_lru", {})
+        lru.pop(sk, None)
+        lru[sk] = None
+        while len(lru) > self.MAX_SHARED_SEQS:
+            old = next(iter(lru))
+            del lru[old]
+            self.kv.free_seq(old)
+        s = self.kv.seq(sk)
         n, lim, toks = 0, min(len(s.tokens), len(shared)), s.tokens
         while n < lim and toks[n] == shared[n]:
             n += 1
@@ -590,35 +602,76 @@ class Engine:
                                   kind="device")
 
     # ---- continuous batching (serve.py): admit / step in chunks / retire ----------------------------
+    def _on_stream(self):
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
     @torch.no_grad()
     def start_turns(self, turns: Sequence[Turn]) -> List[Tuple[SeqState, int, Dict[str, float]]]:
+        with self._on_stream():
+            return self._start_turns(turns)
+
+    def _start_turns(self, turns: Sequence[Turn]) -> List[Tuple[SeqState, int, Dict[str, float]]]:
         """Prefill ``turns`` (LCP reuse, delta only) and sample each first token, WITHOUT decoding:
         returns (sequence, first token, metrics). The first token's K/V is not in the cache yet —
         it is the input of the next :meth:`continue_decode`."""
-        targets = [self.encode_prompt(t.prompt) for t in turns]
+        enc = [self.encode_prompt_split(t.prompt) for t in turns]
+        targets = [ids for ids, _ in enc]
+        t0 = time.perf_counter()
+        keys, _shared, shared_pre = self._sync_groups(turns, enc)   # shared prefixes (system prompts)
         seqs, reused = [], []
         for t, ids in zip(turns, targets):
             sq, n = self.sync_prefix(t.seq_key, ids)
             seqs.append(sq)
             reused.append(n)
         deltas = [ids[n:] for ids, n in zip(targets, reused)]
-        t0 = time.perf_counter()
         logits = self.prefill(list(zip(seqs, deltas)))
         first = self._sample_host(logits, seqs, turns).tolist()
         ms = (time.perf_counter() - t0) * 1e3
-        self.stats["prefill_tokens"] += sum(len(d) for d in deltas)
+        self.stats["prefill_tokens"] += sum(len(d) for d in deltas) + sum(shared_pre.values())
         self.stats["prefill_s"] += ms / 1e3
         return [(sq, int(f), {"prompt_tokens": len(d) + n, "prefill_tokens": len(d), "reused_tokens": n,
                               "prefill_ms": ms}) for sq, f, d, n in zip(seqs, first, deltas, reused)]
 
+    def decode_groups_for(self, seqs: Sequence[SeqState], turns: Sequence[Turn]):
+        """(labels, shared blocks) of a decode batch from its turns' ``shared_key``s, or None:
+        sequences still holding their group's shared blocks decode them once per group."""
+        labels, blocks = [], []
+        for sq, t in zip(seqs, turns):
+            key = getattr(t.prompt, "shared_key", None)
+            sh = self.kv.seqs.get(self.shared_seq_key(key)) if key else None
+            nb = common_blocks(sq, sh) if sh is not None else 0
+            labels.append(key if nb > 0 else None)
+            blocks.append(nb)
+        for key in set(l for l in labels if l is not None):   # a group shares its members' minimum
+            m = min(b for l, b in zip(labels, blocks) if l == key)
+            blocks = [m if l == key else b for l, b in zip(labels, blocks)]
+        if not any(l is not None for l in labels):
+            return None
+        return labels, blocks
+
     @torch.no_grad()
     def continue_decode(self, seqs: Sequence[SeqState], turns: Sequence[Turn], last: Sequence[int],
                         steps: int) -> List[List[int]]:
+        with self._on_stream():
+            return self._continue_decode(seqs, turns, last, steps)
+
+    def _continue_decode(self, seqs: Sequence[SeqState], turns: Sequence[Turn], last: Sequence[int],
+                         steps: int) -> List[List[int]]:
         """Decode ``steps`` new tokens for every sequence of a (possibly changing) batch, given each
         sequence's last sampled token (not yet in the KV cache). Afterwards the cache holds every
         token except the newest one, so calls chain chunk by chunk while sequences join and leave."""
         if not seqs:
             return []
+        order = group_order([getattr(t.prompt, "shared_key", None) for t in turns])
+        if order != list(range(len(seqs))):     # group members adjacent in the batch
+            outs = self._continue_decode([seqs[i] for i in order], [turns[i] for i in order],
+                                         [last[i] for i in order], steps)
+            res: List[List[int]] = [[] for _ in seqs]
+            for j, i in enumerate(order):
+                res[i] = outs[j]
+            return res
+        groups = self.decode_groups_for(seqs, turns)
         first = torch.tensor(list(last), dtype=torch.int64, device=self.device)
         for sq in seqs:
             self.kv.ensure_capacity(sq, sq.length + steps + 1)
@@ -627,13 +680,14 @@ class Engine:
                       t.timeout_s) for t in turns]
         eos = self.tokenizer.stop_ids
         t0 = time.perf_counter()
-        runner = self._graph_for(len(seqs), max(sq.length for sq in seqs) + steps + 1) \
+        runner = self._graph_for(len(seqs), max(sq.length for sq in seqs) + steps + 1, grouped=groups is not None,
+                                 dist_greedy=self.dist_greedy(chunk)) \
             if self.on_gpu and self.ecfg.use_graphs else None
         with trace.range(f"decode chunk B={len(seqs)} steps={steps}"):
             if runner is not None:
-                toks = runner.run(self, seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos)
+                toks = runner.run(self, seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos, groups)
             else:
-                toks = self._decode_eager(seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos)
+                toks = self._decode_eager(seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos, groups)
         out = []
         for sq, tk, f in zip(seqs, toks, last):
             new = list(tk[1:steps + 1])

@@ -51,15 +51,25 @@ def _content_text(content: Any) -> str:
 def render_chat(messages: List[Dict[str, Any]]) -> str:
     """Plain role-tagged transcript ending in an open assistant turn (the bundled models
     have no chat special tokens; the tags match the roundtable's own prompt style)."""
-    parts = []
+    return "".join(s.text for s in chat_segments(messages)[0])
+
+
+def chat_segments(messages: List[Dict[str, Any]]):
+    """The :func:`render_chat` transcript as prompt segments, plus how many leading segments
+    are the conversation's system message(s) — the part many clients send identically."""
+    from .prompt import Segment
+    parts, n_sys, leading = [], 0, True
     for m in messages:
         role = str(m.get("role", "user"))
-        content = m.get("content", "")
-        if isinstance(content, list):  # OpenAI content parts
-            content = "".join(p.get("text", "") for p in content if isinstance(p, dict))
-        parts.append(f"### {ROLE_TAGS.get(role, role)}:\n{content}\n")
-    parts.append(f"### {ROLE_TAGS['assistant']}:\n")
-    return "\n".join(parts)
+        content = _content_text(m.get("content", ""))
+        sep = "\n" if parts else ""
+        parts.append(Segment(f"{sep}### {ROLE_TAGS.get(role, role)}:\n{content}\n"))
+        if leading and role == "system":
+            n_sys = len(parts)
+        else:
+            leading = False
+    parts.append(Segment(("\n" if parts else "") + f"### {ROLE_TAGS['assistant']}:\n"))
+    return parts, n_sys
 
 
 @dataclass
@@ -230,9 +240,11 @@ class RoundtableServer:
     _anon = itertools.count()
 
     def __init__(self, engine: Engine, model_name: str, host: str = "127.0.0.1", port: int = 8000,
-                 max_batch: int = 16, default_max_tokens: int = 512, timeout_s: float = 600.0):
+                 max_batch: int = 16, default_max_tokens: int = 512, timeout_s: float = 600.0,
+                 share_system_prompts: bool = True):
         self.engine = engine
         self.model_name = model_name
+        self.share_system_prompts = share_system_prompts
         self.default_max_tokens = default_max_tokens
         self.sched = Scheduler(engine, max_batch, timeout_s)
         self.started = time.time()
@@ -361,7 +373,15 @@ class RoundtableServer:
             text = render(norm)
             if text is not None:
                 return Prompt([Segment(text)], templated=True)
-        return render_chat(messages)
+        segs, n_sys = chat_segments(messages)
+        if n_sys and self.share_system_prompts:
+            # clients sending the same system prompt share ONE resident copy of its KV
+            # (engine shared-prefix groups: prefilled once, attention reads it once per step)
+            import hashlib
+            sys_text = "".join(x.text for x in segs[:n_sys])
+            key = "sys:" + hashlib.sha1(sys_text.encode("utf-8")).hexdigest()[:16]
+            return Prompt(segs, shared_key=key, shared_segments=n_sys)
+        return Prompt(segs)
 
     def sampling(self, body: Dict[str, Any]) -> SamplingParams:
         def num(key, default, cast):
