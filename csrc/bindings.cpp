@@ -29,7 +29,9 @@ int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, 
 int sample_workspace_floats(int B);
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream);
+                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
+                       int* split_ws, int64_t split_ws_ints);
+int split_workspace_ints(int max_split_tiles);
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
@@ -266,7 +268,7 @@ std::pair<const void*, void*> add_operands(const torch::Tensor& x, int64_t pro, 
 
 void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t pro, int64_t epi,
                  c10::optional<torch::Tensor> res, double eps, c10::optional<torch::Tensor> x2,
-                 c10::optional<torch::Tensor> xout) {
+                 c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws) {
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
   TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm: x [M,K], Ws [N,K]");
@@ -292,9 +294,17 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
     ldo = out.stride(0);
   }
   const auto addo = add_operands(x, pro, x2, xout);
+  int* sw = nullptr;
+  int64_t sw_n = 0;
+  if (split_ws.has_value()) {   // CU-balanced launch workspace (counters zero between calls)
+    TORCH_CHECK(split_ws->scalar_type() == torch::kInt32 && split_ws->is_contiguous() &&
+                    split_ws->device() == x.device(), "split_ws: contiguous int32 on x's device");
+    sw = split_ws->data_ptr<int>();
+    sw_n = split_ws->numel();
+  }
   const int rc = launch_skinny_gemm(epi == 1 ? nullptr : out.data_ptr(), x.data_ptr(), Ws.data_ptr(), rp, (int)M,
                                     (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, nullptr, addo.first,
-                                    addo.second, cur_stream());
+                                    addo.second, cur_stream(), sw, sw_n);
   TORCH_CHECK(rc == 0, "skinny_gemm: unsupported configuration (rc=", rc, ")");
 }
 
@@ -524,7 +534,9 @@ void kv_block_copy(torch::Tensor k, torch::Tensor v, torch::Tensor src, torch::T
 PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm, "decode GEMM (M<=16), shuffled weights, fused norm / resid / swiglu",
         py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("epi"), py::arg("res") = py::none(),
-        py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none());
+        py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none(),
+        py::arg("split_ws") = py::none());
+  m.def("split_workspace_ints", &split_workspace_ints, "int32 words of a skinny_gemm split_ws for R split tiles");
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
         py::arg("rope_heads") = 0, py::arg("head_dim") = 0, py::arg("swiglu") = false);
   m.def("kv_block_copy", &kv_block_copy, py::arg("k"), py::arg("v"), py::arg("src"), py::arg("dst"));

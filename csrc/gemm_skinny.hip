@@ -32,6 +32,42 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(GemmArgs p) {
   gemm_tile<PRO, EPI, NW, U, false>(p, blockIdx.x, sm, st0, false, blockIdx.x == 0);
 }
 
+// CU-balanced launch for tile counts that are not a multiple of the CU count (gate_up of
+// Llama-3-8B / Mistral-7B: 896 tiles on 256 CUs = 3.5 per CU, so half the CUs stream a 4th
+// tile while the rest idle): the last R = T mod CUs tiles run as two K-halves each (SplitX in
+// skinny_core.h), the other T - R whole. Every CU then gets the same bytes (3 tiles + one
+// half-tile at 896/256). Workgroups [0, 2R) are the halves (dispatched first, so their
+// hand-offs finish under the whole tiles' streams), [2R, T + R) the whole tiles.
+// tools/exp_balance.hip: swiglu 768 / 896 / 1024 tiles = 31.0 / 37.6 / 40.5 us (896 is 1.8 us
+// above the line through its neighbours).
+constexpr int SPLIT_CTRS = 256;   // counter words at the head of the split workspace
+template <int PRO, int EPI, int NW, int U>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_bal_kernel(GemmArgs p, int* __restrict__ ws, int R) {
+  __shared__ GemmSmem<nacc<EPI>(), NW> sm;
+  Stage<PRO, EPI, U> st0;
+  const int T = p.N / 16;
+  const int b = blockIdx.x;
+  if (b < 2 * R) {
+    const int r = b >> 1;
+    const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)r * 2 * SPLIT_STRIDE, ws + r, b & 1};
+    gemm_tile<PRO, EPI, NW, U, false>(p, T - R + r, sm, st0, false, false, &sx);
+  } else {
+    gemm_tile<PRO, EPI, NW, U, false>(p, b - 2 * R, sm, st0, false, false);
+  }
+}
+
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cache[dev] = n > 0 ? n : -1;
+  }
+  return cache[dev] > 0 ? cache[dev] : 0;
+}
+
 // Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j] (optionally W * gamma[k] folded in)
 // If rope_rows > 0, output row r < rope_rows takes source row h*D + (p>>1) + (p&1)*D/2
 // (r = h*D + p): the pair-interleaved q/k order the ROPE epilogue expects.
@@ -105,10 +141,43 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+int split_workspace_ints(int max_split_tiles) { return SPLIT_CTRS + max_split_tiles * 2 * SPLIT_STRIDE; }
+
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream) {
+                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
+                       int* split_ws, int64_t split_ws_ints) {
   if (pro == PRO_NORM_ADD && x2 == nullptr) return -5;
   if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
+  // CU-balanced variant: whole plain/norm tiles + split remainder (not for NORM_ADD, whose
+  // workgroup 0 publishes the whole K row, nor ROPE, whose pairs are read across the tile)
+  if (split_ws != nullptr && pro != PRO_NORM_ADD && epi != EPI_ROPE && (K / 32) % 2 == 0 && K >= 64) {
+    const int cus = device_cus();
+    const int T = N / 16;
+    const int R = cus > 0 ? T % cus : 0;
+    if (cus > 0 && T > cus && R > 0 && R <= SPLIT_CTRS && split_ws_ints >= split_workspace_ints(R)) {
+      const GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
+                          eps, {}, nullptr, nullptr};
+      const dim3 grid(T + R);
+      if (pro == PRO_NORM && epi == EPI_SWIGLU)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_SWIGLU, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else if (pro == PRO_PLAIN && epi == EPI_SWIGLU)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_SWIGLU, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else if (pro == PRO_NORM && epi == EPI_STORE)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_STORE, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else if (pro == PRO_PLAIN && epi == EPI_STORE)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_STORE, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else if (pro == PRO_PLAIN && epi == EPI_RESID)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_RESID, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else
+        return -2;
+      return 0;
+    }
+  }
   RopeEpi re{};
   if (epi == EPI_ROPE) {
     if (rope == nullptr) return -3;
@@ -180,5 +249,5 @@ int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, i
                             hipStream_t stream) {
   const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS};
   return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, x2, xo,
-                            stream);
+                            stream, nullptr, 0);
 }

@@ -63,6 +63,17 @@ constexpr int nacc() { return EPI == EPI_SWIGLU ? 2 : 1; }
 
 RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// Split tile (CU-balanced launch, gemm_skinny.hip): the two K-halves of one 16-column tile run
+// as two workgroups; each leaves its row sums (v, up, sum of squares) in `part` with
+// write-through stores, the second to arrive (tile counter) adds the other half's and runs the
+// epilogue, then re-arms the counter. Per split tile: 2 halves x SPLIT_STRIDE floats.
+constexpr int SPLIT_STRIDE = 16 * 16 * 2 + 16;   // v[16][16], up[16][16], ssq[16]
+struct SplitX {
+  float* part;    // this tile's [2][SPLIT_STRIDE]
+  int* ctr;       // this tile's arrival counter (0 between launches)
+  int half;       // 0: k-steps [0, mid), 1: [mid, nsteps)
+};
+
 // 16-bit store, optionally write-through (sc1) for consumers in the same launch
 template <bool SC1>
 RT_DEVICE void st16(uint16_t* p, float v) {
@@ -193,11 +204,16 @@ RT_DEVICE void gemm_prefetch(const GemmArgs& p, int tile, Stage<PRO, EPI, U>& st
 template <int PRO, int EPI, int NW, int U, bool SC1>
 RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>& sm, Stage<PRO, EPI, U>& st0,
                          bool prefetched,
-                         bool publish_xo) {
+                         bool publish_xo, const SplitX* sx = nullptr) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int M = p.M, N = p.N, K = p.K;
-  const int nsteps = K / 32;
+  const int ksteps = K / 32;
+  // k-step range of this workgroup: all of K, or one half of a split tile. `nsteps` below is
+  // the range END (loads clamp to it), `s_lo` its start.
+  const int kmid = ksteps / 2;
+  const int s_lo = (sx != nullptr && sx->half == 1) ? kmid : 0;
+  const int nsteps = (sx != nullptr && sx->half == 0) ? kmid : ksteps;
   const bool row_ok = r < M;
   const size_t lane_elem = (size_t)(row_ok ? r : 0) * K + 8 * g;
   const XSrc xr = make_xsrc<SC1>(p.x, lane_elem);
@@ -205,7 +221,7 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   uint16_t* xo_r =
       (PRO == PRO_NORM_ADD && publish_xo && row_ok && p.xo != nullptr) ? p.xo + (size_t)r * K + 8 * g : nullptr;
   const XSrc xo_s = make_xsrc<SC1>(PRO == PRO_NORM_ADD && p.xo != nullptr ? p.xo : p.x, lane_elem);
-  const short8* wt = p.Ws + (size_t)tile * nsteps * ((EPI == EPI_SWIGLU) ? 128 : 64);
+  const short8* wt = p.Ws + (size_t)tile * ksteps * ((EPI == EPI_SWIGLU) ? 128 : 64);
   const short8* wt2 = nullptr;
 
   float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
@@ -215,12 +231,13 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   // block (a break between them lets MachineSink move each stage's loads down next to their
   // consumer); every issue is unconditional, so the waits are counted, not vmcnt(0).
   constexpr int SPAN = NW * U;
-  const int nst = wid < nsteps ? (nsteps - wid + SPAN - 1) / SPAN : 0;
-  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane);
-  issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, wid, nsteps);
+  const int w0 = s_lo + wid;   // this wave's first k-step
+  const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
+  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, w0, nsteps, lane);
+  issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, w0, nsteps);
   int j = 0;
   for (; j + 1 < nst; j += 2) {
-    const int s = wid + SPAN * j;
+    const int s = w0 + SPAN * j;
     issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane);
     issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
     consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
@@ -228,7 +245,7 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
     issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
     consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
   }
-  if (j < nst) consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, wid + SPAN * j, nsteps, xo_r, xo_s);
+  if (j < nst) consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps, xo_r, xo_s);
 
   // C layout: acc[i] = C[m = 4g + i][n = r]
 #pragma unroll
@@ -243,22 +260,47 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   }
   __syncthreads();
   const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
-  if (threadIdx.x < 256 && m < M) {
-    float v = 0.f, ss = 0.f;
+  const bool live = threadIdx.x < 256 && m < M;
+  float v = 0.f, ss = 0.f, up = 0.f;
+  if (live) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       v += sm.red[w][0][m][n];
       if constexpr (PRO != PRO_PLAIN) ss += sm.sq[w][m];
+      if constexpr (EPI == EPI_SWIGLU) up += sm.red[w][(EPI == EPI_SWIGLU) ? 1 : 0][m][n];
     }
+  }
+  if (sx != nullptr) {   // split tile: hand the half's sums over, the second arrival finishes
+    float* mine = sx->part + sx->half * SPLIT_STRIDE;
+    const float* other = sx->part + (1 - sx->half) * SPLIT_STRIDE;
+    if (live) {
+      __hip_atomic_store(mine + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (EPI == EPI_SWIGLU)
+        __hip_atomic_store(mine + 256 + threadIdx.x, up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (n == 0) __hip_atomic_store(mine + 512 + m, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(sx->ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm.sq[0][0] = prev == 1 ? 1.f : 0.f;   // LDS flag: this workgroup arrived second
+      if (prev == 1) __hip_atomic_store(sx->ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (sm.sq[0][0] == 0.f) return;   // first half in: the other workgroup finishes the tile
+    if (live) {
+      v += __hip_atomic_load(other + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (EPI == EPI_SWIGLU)
+        up += __hip_atomic_load(other + 256 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ss += __hip_atomic_load(other + 512 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (live) {
     float inv = 1.f;
     if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss / (float)K + p.eps);
     v *= inv;
     const int col = tile * 16 + n;
     if constexpr (EPI == EPI_SWIGLU) {
-      const int u1 = (EPI == EPI_SWIGLU) ? 1 : 0;
-      float up = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) up += sm.red[w][u1][m][n];
       up *= inv;
       st16<SC1>(p.out + (size_t)m * p.ldo + col, silu(v) * up);
     } else if constexpr (EPI == EPI_RESID) {

@@ -45,6 +45,38 @@ def test_skinny_gemm_modes(M, N, K):
     close(got, exp.to(DEV), 0.05, 0.03)
 
 
+@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("N,K", [(14336, 4096), (300 * 16, 1024), (257 * 16, 2048)])
+def test_skinny_gemm_balanced_split(M, N, K):
+    """CU-balanced launch (tiles mod CUs run as two K-halves): same results as the fp32
+    reference on every epilogue, and the workspace counters re-arm (three calls agree)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert (N // 16) % cus != 0
+    x = bf(M, K, seed=61)
+    gam = bf(K, seed=62)
+    ws = ops.split_workspace(DEV)
+    W2 = bf(2 * N, K, scale=0.05, seed=63)
+    Ws2 = ops.shuffle_weight(W2, gam, swiglu=True)
+    exp = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W2.cpu(), gam.cpu()), 1, 2).to(DEV)
+    outs = [ops.skinny_gemm(x, Ws2, ops.PRO_NORM, ops.EPI_SWIGLU, split_ws=ws) for _ in range(3)]
+    for o in outs:
+        close(o, exp, 0.05, 0.03)
+        assert torch.equal(o, outs[0])
+    assert int(ws[:256].abs().sum()) == 0, "split counters must re-arm to zero"
+    W = bf(N, K, scale=0.05, seed=64)
+    Wg = ops.shuffle_weight(W, gam)
+    close(ops.skinny_gemm(x, Wg, ops.PRO_NORM, split_ws=ws),
+          ref.skinny_gemm(x.cpu(), ref.fold_gamma(W.cpu(), gam.cpu()), 1, eps=1e-5).to(DEV), 0.05, 0.02)
+    Ws = ops.shuffle_weight(W)
+    res = bf(M, N, seed=65)
+    res_ref = res.cpu().clone()
+    ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=ws)
+    ref.skinny_gemm(x.cpu(), W.cpu(), 0, 1, res=res_ref)
+    close(res, res_ref.to(DEV), 0.06, 0.02)
+    # no workspace: the plain launch gives the same SwiGLU output up to summation order
+    close(ops.skinny_gemm(x, Ws2, ops.PRO_NORM, ops.EPI_SWIGLU), outs[0], 0.02, 0.02)
+
+
 def test_shuffle_layout():
     N, K = 32, 64
     W = torch.arange(N * K, device=DEV).reshape(N, K).to(torch.float32).to(torch.bfloat16)

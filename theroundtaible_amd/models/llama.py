@@ -109,6 +109,8 @@ class LlamaModel:
                         d[name] = ops.shuffle_weight(lw[name], lw[norm] if norm else None, **kw)
                         if drop_originals:
                             lw[name] = None
+                    # gate_up's tile count (ffn/16) is rarely a multiple of the CU count: balanced launch
+                    d["gu_split_ws"] = ops.split_workspace(d["w_gate_up"].device)
                     layers.append(d)
                 lm = ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])
                 if drop_originals:
@@ -177,7 +179,8 @@ class LlamaModel:
                                      self.head_dim, eps)
             a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)
             ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
-            g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps)
+            g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps,
+                                split_ws=lw.get("gu_split_ws"))
             ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
         logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
         return logits[:, :cfg.vocab]

@@ -270,16 +270,29 @@ def unshuffle_weight(Ws: torch.Tensor, rope_heads: int = 0, head_dim: int = 0, s
     return out
 
 
+# CU-balanced skinny GEMM workspace: 256 counter words + 2 K-halves x 528 floats per split
+# tile, up to 255 split tiles (tile count mod CU count); csrc/gemm_skinny.hip split_workspace_ints
+SPLIT_WS_INTS = 256 + 255 * 2 * (16 * 16 * 2 + 16)
+
+
+def split_workspace(device) -> torch.Tensor:
+    """Zeroed workspace for one call site of :func:`skinny_gemm` ``split_ws`` (one per weight:
+    concurrent launches must not share it; its counters return to zero after every call)."""
+    return torch.zeros(SPLIT_WS_INTS, dtype=torch.int32, device=device)
+
+
 def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: int = EPI_STORE,
                 res: Optional[torch.Tensor] = None, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
-                xout: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """Decode linear (M <= 16) on shuffled weights with fused RMSNorm prologue (gamma pre-folded)
     and residual / SwiGLU epilogue. Returns the output (None for RESID, which updates ``res``).
-    ``PRO_NORM_ADD``: normalizes ``bf16(x + x2)`` and writes that sum to ``xout`` (TP decode)."""
+    ``PRO_NORM_ADD``: normalizes ``bf16(x + x2)`` and writes that sum to ``xout`` (TP decode).
+    ``split_ws`` (:func:`split_workspace`): when the tile count is not a multiple of the CU count,
+    the remainder tiles run as two K-halves each so every CU streams the same bytes."""
     if _use_native(x):
         n = Ws.shape[0] // (2 if epi == EPI_SWIGLU else 1)
         out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device) if epi != EPI_RESID else x
-        native().skinny_gemm(out, x, Ws, pro, epi, res, eps, x2, xout)
+        native().skinny_gemm(out, x, Ws, pro, epi, res, eps, x2, xout, split_ws)
         return None if epi == EPI_RESID else out
     return ref.skinny_gemm(x, Ws, pro, epi, res, eps, x2, xout)
 

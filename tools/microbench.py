@@ -77,6 +77,7 @@ def bench_gemm(M):
         ("qkv  (norm+rope+cache)", (hq + 2 * hkv) * d, hid),
         ("o    (+resid)", hid, hq * d),
         ("gate_up (norm+swiglu)", 2 * ffn, hid),
+        ("gate_up balanced (norm+swiglu, split remainder)", 2 * ffn, hid),
         ("down (+resid)", hid, ffn),
         ("lm_head (norm)", vocab, hid),
         ("gate_up-plain (norm, unpaired)", 2 * ffn, hid),
@@ -91,6 +92,9 @@ def bench_gemm(M):
         elif name.startswith("o ") or name.startswith("down"):
             inp = x if name.startswith("o ") else g_in
             fn = lambda i, inp=inp: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
+        elif name.startswith("gate_up balanced"):
+            sws = ops.split_workspace(DEV)
+            fn = lambda i, sws=sws: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM, ops.EPI_SWIGLU, split_ws=sws)
         elif name.startswith("gate_up"):
             fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM, ops.EPI_SWIGLU)
         else:
