@@ -6,14 +6,21 @@
 // (seed, knight, position) (the engine passes each row's token position as `offset`).
 //
 // Each row is split into C chunks handled by C workgroups (a single workgroup per row is
-// LDS-atomic-bound: 2 x 128K histogram atomics on one CU), in five graph-capturable launches:
-//   1 stats  : per-chunk max/argmax                                  (grid B x C)
-//   2 hist   : coarse 2048-bin histogram of z over [-ZR, 0] (count + probability mass),
+// LDS-atomic-bound: 2 x 128K histogram atomics on one CU), in six graph-capturable launches:
+//   1 stats  : per-chunk max/argmax, and the chunk's best Gumbel score over ALL tokens (B x C)
+//   2 accept : fast path. j* = argmax(z + g) over the whole vocabulary is the nucleus sample
+//              whenever j* lies in the nucleus, i.e. when the mass of the tokens strictly more
+//              likely than j* is below p * total (then the argmax over the nucleus is j*).
+//              j* is itself a softmax draw, so that holds with probability >= top_p (95 % at
+//              top_p 0.95). One pass sums both masses; the last-arriving chunk decides, writes
+//              the token and raises the row's `done` flag. Greedy and unfiltered rows finish
+//              here too; launches 3-6 return at once for a done row.  (grid B x C)
+//   3 hist   : coarse 2048-bin histogram of z over [-ZR, 0] (count + probability mass),
 //              chunk-local in LDS then merged with one global atomic per non-empty bin
-//   3 select : per row, block-scan the histogram -> the bin where top-k (count) or top-p
+//   4 select : per row, block-scan the histogram -> the bin where top-k (count) or top-p
 //              (mass) crosses                                          (grid B)
-//   4 refine : 2048-bin sub-histogram of that one bin                 (grid B x C)
-//   5 final  : threshold from the sub-histogram, Gumbel-argmax over the chunk, then the
+//   5 refine : 2048-bin sub-histogram of that one bin                 (grid B x C)
+//   6 final  : threshold from the sub-histogram, Gumbel-argmax over the chunk, then the
 //              last-arriving chunk of each row reduces the partials   (grid B x C)
 // Threshold resolution ZR/4M ~ 7e-6 in z; every pass uses 16-byte vector loads (G13).
 // Bit-for-bit RNG twin: theroundtaible_amd/ops/reference.py::uniform_tensor.
@@ -28,7 +35,10 @@ constexpr float ZR = 30.f;  // exp(-30) * 128K < 1e-8 of the mass: ignored
 // per-row workspace layout (floats / ints interchangeable, 4 bytes each)
 constexpr int W_MAX = 0;                 // [C] chunk max
 constexpr int W_ARG = W_MAX + C;         // [C] chunk argmax (int)
-constexpr int W_HC = W_ARG + C;          // [NB] coarse count
+constexpr int W_GV = W_ARG + C;          // [C] chunk best Gumbel score v/T + g
+constexpr int W_GI = W_GV + C;           // [C] its token (int)
+// [W_HC, W_ROW) is zeroed by launch 1 (its chunks write only the words above)
+constexpr int W_HC = W_GI + C;           // [NB] coarse count
 constexpr int W_HM = W_HC + NB;          // [NB] coarse mass
 constexpr int W_SC = W_HM + NB;          // [NB] sub count
 constexpr int W_SM = W_SC + NB;          // [NB] sub mass
@@ -36,7 +46,10 @@ constexpr int W_SEL = W_SM + NB;         // bsel(int), by_count(int), need(float
 constexpr int W_PV = W_SEL + 4;          // [C] partial score
 constexpr int W_PI = W_PV + C;           // [C] partial index (int)
 constexpr int W_CNT = W_PI + C;          // arrival counter (int)
-constexpr int W_ROW = W_CNT + 4;         // floats per row (memset region: whole row)
+constexpr int W_DONE = W_CNT + 1;        // row sampled by the accept pass (int)
+constexpr int W_CNT2 = W_CNT + 2;        // accept-pass arrival counter (int)
+constexpr int W_SUM = W_CNT + 4;         // mass above j*, total mass (accept-pass accumulators)
+constexpr int W_ROW = W_SUM + 4;         // floats per row
 
 RT_DEVICE uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -119,7 +132,9 @@ RT_DEVICE float row_max(const float* ws) {
 // ---- 1: chunk max / argmax -----------------------------------------------------------------
 template <typename T, bool VEC>
 __global__ void __launch_bounds__(NT) smp_stats(float* __restrict__ ws, const T* __restrict__ logits, int V,
-                                                int64_t ld) {
+                                                int64_t ld, const float* __restrict__ temperature,
+                                                const int64_t* __restrict__ seeds,
+                                                const int64_t* __restrict__ offsets) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int b = blockIdx.x, c = blockIdx.y;
@@ -134,11 +149,90 @@ __global__ void __launch_bounds__(NT) smp_stats(float* __restrict__ ws, const T*
   int lo, hi;
   chunk_range(V, c, lo, hi);
   ArgMax a{-INFINITY, 0x7fffffff};
-  for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) { am_merge(a, v, i); });
+  const float temp = temperature[b];
+  if (temp > 0.f) {   // also the chunk's best Gumbel score over every token (accept pass)
+    const float invT = 1.f / temp;
+    const uint64_t key = mix64((uint64_t)seeds[b] ^ mix64((uint64_t)offsets[b]));
+    ArgMax gb{-INFINITY, 0x7fffffff};
+    for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) {
+      am_merge(a, v, i);
+      am_merge(gb, v * invT + gumbel(key, (uint32_t)i), i);
+    });
+    gb = block_argmax(gb, sv, si);
+    if (threadIdx.x == 0) {
+      w[W_GV + c] = gb.v;
+      reinterpret_cast<int*>(w)[W_GI + c] = gb.i;
+    }
+  } else {
+    for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) { am_merge(a, v, i); });
+  }
   a = block_argmax(a, sv, si);
   if (threadIdx.x == 0) {
     w[W_MAX + c] = a.v;
     reinterpret_cast<int*>(w)[W_ARG + c] = a.i;
+  }
+}
+
+// ---- 2: accept pass (fast path, see the header) -------------------------------------------------
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(NT) smp_accept(int64_t* __restrict__ out, float* __restrict__ ws,
+                                                 const T* __restrict__ logits, int V, int64_t ld,
+                                                 const float* __restrict__ temperature,
+                                                 const float* __restrict__ top_p, const int* __restrict__ top_k) {
+  __shared__ float red[8];
+  const int b = blockIdx.x, c = blockIdx.y;
+  float* w = ws + (size_t)b * W_ROW;
+  int* wi = reinterpret_cast<int*>(w);
+  const float temp = temperature[b];
+  const int k = top_k[b];
+  const float p = top_p[b];
+  const bool use_k = k > 0 && k < V;
+  if (!(temp > 0.f) || (!use_k && !(p < 1.f))) {   // greedy, or nothing filtered: decided now
+    if (c == 0 && threadIdx.x == 0) {
+      ArgMax r{-INFINITY, 0x7fffffff};
+      for (int j = 0; j < C; ++j) {
+        if (temp > 0.f) am_merge(r, w[W_GV + j], wi[W_GI + j]);
+        else am_merge(r, w[W_MAX + j], wi[W_ARG + j]);
+      }
+      if (r.i < 0 || r.i >= V) {   // no finite score: the row argmax
+        r = ArgMax{-INFINITY, 0x7fffffff};
+        for (int j = 0; j < C; ++j) am_merge(r, w[W_MAX + j], wi[W_ARG + j]);
+      }
+      out[b] = r.i;
+      wi[W_DONE] = 1;
+    }
+    return;
+  }
+  if (use_k) return;   // top-k rows take the histogram path
+  ArgMax g{-INFINITY, 0x7fffffff};
+  for (int j = 0; j < C; ++j) am_merge(g, w[W_GV + j], wi[W_GI + j]);
+  if (g.i < 0 || g.i >= V) return;   // no finite score: the histogram path decides
+  const float mx = row_max(w), invT = 1.f / temp;
+  const T* row = logits + (size_t)b * ld;
+  const float vj = rt::DT<T>::load(row + g.i);
+  int lo, hi;
+  chunk_range(V, c, lo, hi);
+  float above = 0.f, total = 0.f;
+  for_chunk<T, VEC>(row, lo, hi, [&](int, float v) {
+    const float e = __expf((v - mx) * invT);
+    total += e;
+    above += v > vj ? e : 0.f;
+  });
+  above = rt::block_sum(above, red);
+  total = rt::block_sum(total, red);
+  if (threadIdx.x == 0) {
+    atomicAdd(&w[W_SUM], above);
+    atomicAdd(&w[W_SUM + 1], total);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&wi[W_CNT2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == C - 1) {   // every chunk's sums are in: decide the row
+      const float A = __hip_atomic_load(&w[W_SUM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float Z = __hip_atomic_load(&w[W_SUM + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (A < p * Z) {
+        out[b] = g.i;
+        __hip_atomic_store(&wi[W_DONE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -153,6 +247,7 @@ __global__ void __launch_bounds__(NT) smp_hist(float* __restrict__ ws, const T* 
   const float temp = temperature[b];
   const int k = top_k[b];
   if (!(temp > 0.f) || !((k > 0 && k < V) || top_p[b] < 1.f)) return;
+  if (reinterpret_cast<const int*>(w)[W_DONE]) return;   // sampled by the accept pass
   int bsel = 0;
   if constexpr (SUB) {
     bsel = reinterpret_cast<const int*>(w)[W_SEL];
@@ -247,7 +342,7 @@ __global__ void __launch_bounds__(1024) smp_select(float* __restrict__ ws, int V
   int* wi = reinterpret_cast<int*>(w);
   const int k = top_k[b];
   const float p = top_p[b];
-  if (!(temperature[b] > 0.f) || !((k > 0 && k < V) || p < 1.f)) {
+  if (!(temperature[b] > 0.f) || !((k > 0 && k < V) || p < 1.f) || wi[W_DONE]) {
     if (threadIdx.x == 0) wi[W_SEL] = NB;
     return;
   }
@@ -305,14 +400,7 @@ __global__ void __launch_bounds__(1024) smp_final(int64_t* __restrict__ out, flo
   float* w = ws + (size_t)b * W_ROW;
   int* wi = reinterpret_cast<int*>(w);
   const float temp = temperature[b];
-  if (!(temp > 0.f)) {  // greedy: argmax over the chunk maxima
-    if (c == 0 && threadIdx.x == 0) {
-      ArgMax a{-INFINITY, 0x7fffffff};
-      for (int j = 0; j < C; ++j) am_merge(a, w[W_MAX + j], wi[W_ARG + j]);
-      out[b] = a.i;
-    }
-    return;
-  }
+  if (wi[W_DONE]) return;   // greedy / unfiltered / accepted: out[b] written by launch 2
   const float mx = row_max(w), invT = 1.f / temp, scale = NB / ZR;
   float zthr = -INFINITY;
   const int bsel = wi[W_SEL];
@@ -379,7 +467,10 @@ int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, 
   const dim3 g2(B, C);
 #define RT_SMP(TT, VV)                                                                                              \
   do {                                                                                                              \
-    hipLaunchKernelGGL((smp_stats<TT, VV>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row);             \
+    hipLaunchKernelGGL((smp_stats<TT, VV>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,             \
+                       temperature, seeds, offsets);                                                                \
+    hipLaunchKernelGGL((smp_accept<TT, VV>), g2, dim3(NT), 0, stream, out, ws, (const TT*)logits, V, ld_row,        \
+                       temperature, top_p, top_k);                                                                  \
     hipLaunchKernelGGL((smp_hist<TT, VV, false>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,        \
                        temperature, top_p, top_k);                                                                  \
     hipLaunchKernelGGL(smp_select, dim3(B), dim3(1024), 0, stream, ws, V, temperature, top_p, top_k);              \

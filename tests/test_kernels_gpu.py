@@ -286,6 +286,27 @@ def test_sample_matches_reference():
     assert torch.equal(got, again)
 
 
+def test_sample_fast_path_matches_reference():
+    """Accept pass (csrc/sampling.hip launch 2): the whole-vocabulary Gumbel argmax is taken
+    when it lies in the nucleus, the histogram path decides otherwise; both must agree with the
+    fp64 reference over many draws (Llama-3 vocabulary, peaked and flat rows)."""
+    B, V = 16, 128256
+    logits = bf(B, V, scale=3.0, seed=77).float()
+    logits[::2] *= 3.0          # peaked rows: small nuclei, frequent fallbacks
+    temp = torch.full((B,), 0.7, device=DEV)
+    top_p = torch.full((B,), 0.9, device=DEV)
+    top_k = torch.zeros(B, dtype=torch.int32, device=DEV)
+    hits = total = 0
+    for rep in range(4):
+        seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 7919 + rep
+        offs = torch.arange(B, dtype=torch.int64, device=DEV) + 1000 * rep
+        got = ops.sample(logits, temp, top_p, top_k, seeds, offs).cpu()
+        exp = ref.sample(logits.cpu(), temp.cpu(), top_p.cpu(), top_k.cpu(), seeds.cpu(), offs.cpu())
+        hits += int((got == exp).sum())
+        total += B
+    assert hits >= total - 2, (hits, total)
+
+
 def test_sample_top_p_nucleus():
     V = 1000
     logits = torch.full((1, V), -10.0, device=DEV)
