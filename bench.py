@@ -258,6 +258,8 @@ def main() -> int:
             with open(args.out, "w") as f:
                 f.write(line + "\n")
     cl.barrier()
+    from theroundtaible_amd.parallel.cluster import shutdown_cluster
+    shutdown_cluster()
     return 0
 
 

@@ -62,3 +62,20 @@ def test_four_rank_tp4_llama70b_shapes_on_shared_gpu():
                   "--layout", "shared"), nproc=4)
     assert "tp4" in out["config"]["parallelism"] and out["config"]["model"].startswith("llama3-70b")
     assert out["detail"]["decode_tokens"] == 2 * 8 * 2 and out["detail"]["failed_turns"] == 0, out["_log"]
+
+
+def test_rccl_data_plane_single_rank():
+    """The RCCL (backend "nccl") calls of the scaling bench and the TP decode path on real
+    hardware: eager communicator init with device_id, C1 all-gather, barrier(device_ids), and
+    all_reduce + all_gather captured in a hipGraph (tools/nccl_check.py; world 1 on this box,
+    the same script runs at world 8 on a node)."""
+    gc.collect()
+    torch.cuda.empty_cache()
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "nccl_check.py")]
+    env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="nccl", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["ok"] and rec["backend"] == "nccl" and rec["checks"] >= 9 and rec["ranks_ok"] == 1, rec

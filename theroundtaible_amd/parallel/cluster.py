@@ -50,7 +50,7 @@ class Cluster:
         return out
 
     def barrier(self) -> None:
-        if self.distributed:
+        if self.distributed or self.backend == "nccl":   # (a 1-rank RCCL world: tools/nccl_check.py)
             if self.backend == "nccl":
                 dist.barrier(device_ids=[self.local_rank])
             else:
@@ -92,8 +92,11 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     if use_gpu:
         torch.cuda.set_device(gpu_index)
     c = Cluster(rank=rank, world=world, local_rank=local, device=device)
-    if world > 1:
+    # a 1-rank world normally runs without a process group; ROUNDTABLE_DIST_BACKEND=nccl forces an
+    # RCCL one (exercises the RCCL data plane on a 1-GPU box, tools/nccl_check.py)
+    if world > 1 or (forced == "nccl" and use_gpu):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
         backend = forced if forced in ("nccl", "gloo") else ("nccl" if use_gpu else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
@@ -107,6 +110,6 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
 
 def shutdown_cluster() -> None:
     global _CLUSTER
-    if _CLUSTER is not None and _CLUSTER.distributed and dist.is_initialized():
+    if _CLUSTER is not None and dist.is_initialized():
         dist.destroy_process_group()
     _CLUSTER = None
