@@ -8,7 +8,8 @@
 #include <cstdio>
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
-                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream);
+                       int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
+                       int* split_ws, int64_t split_ws_ints);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -37,17 +38,17 @@ static int failures = 0;
 int main() {
   // decode GEMM: M outside [1, 16], K not a multiple of 32, N not a multiple of 16, missing operands
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 0, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr) == -1);
+                            nullptr, nullptr, nullptr, 0) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 17, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr) == -1);
+                            nullptr, nullptr, nullptr, 0) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 48, 16, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr) == -1);
+                            nullptr, nullptr, nullptr, 0) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 24, 64, 24, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr) == -1);
+                            nullptr, nullptr, nullptr, 0) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 2, 0, nullptr, nullptr,
-                            nullptr, nullptr) == -5);   // NORM_ADD without its second operand
+                            nullptr, nullptr, nullptr, 0) == -5);   // NORM_ADD without its second operand
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 0, 3, nullptr, nullptr,
-                            nullptr, nullptr) == -3);   // ROPE epilogue without its parameters
+                            nullptr, nullptr, nullptr, 0) == -3);   // ROPE epilogue without its parameters
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 16, 48, 0, 0, 0, nullptr) == -1);
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 32, 64, 64, 128, 0, nullptr) == -1);   // rope rows > N
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 48, 64, 0, 0, 1, nullptr) == -1);      // SwiGLU halves of 24 rows
