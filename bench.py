@@ -175,8 +175,12 @@ def main() -> int:
                       "round_mode": args.round_mode, "prompt_layout": args.layout},
             "chronicle": ".roundtable/chronicle.md", "adapter_config": {}})
         backends = {k["adapter"]: RemoteKnight(pool, k["name"], k["name"], k["adapter"]) for k in knights}
+        # every rank runs every table (SPMD), but only the rank leading the table's first knight
+        # writes its session files: per-rank host work stays one table's as N grows
+        persist = placement[knights[0]["name"]][0] == cl.rank
         orchs.append(Orchestrator(cfg, backends, workdir, options=RunOptions(shuffle_seed=1000 + t,
-                                                                             max_new_tokens=args.new_tokens),
+                                                                             max_new_tokens=args.new_tokens,
+                                                                             persist=persist),
                                   store_root=workdir))
 
     timing = {}

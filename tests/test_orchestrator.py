@@ -241,3 +241,17 @@ def test_shared_layout_continuation_keeps_prefix(tmp_path):
     h1 = "".join(s.text for s in first.segments[:first.shared_segments])
     h2 = "".join(s.text for s in nxt.segments[:nxt.shared_segments])
     assert h2.startswith(h1) and "THE KING HAS SENT YOU BACK" in h2[len(h1):]
+
+
+def test_mirror_orchestrator_writes_nothing_and_decides_the_same(tmp_path):
+    """RunOptions(persist=False): an SPMD rank's mirror of a table another rank persists drops
+    every session / chronicle write but reaches the same decision from the same replies."""
+    sc = {k: [consensus_reply(6, f"{k} twijfelt."), consensus_reply(9, f"{k} is akkoord.", proposal=f"plan {k}")]
+          for k in ("Claude", "Gemini", "GPT")}
+    a = Orchestrator(config(), backends(sc), str(tmp_path / "a"), options=RunOptions(shuffle_seed=3)).run("Spiegel")
+    os.makedirs(tmp_path / "b")
+    b = Orchestrator(config(), backends(sc), str(tmp_path / "b"),
+                     options=RunOptions(shuffle_seed=3, persist=False)).run("Spiegel")
+    assert (a.consensus, a.rounds, a.decision, a.lead_knight) == (b.consensus, b.rounds, b.decision, b.lead_knight)
+    assert os.path.isdir(a.session_path) and b.session_path == "<mirror>"
+    assert os.listdir(tmp_path / "b") == []

@@ -110,6 +110,22 @@ class RunOptions:
     prompt_layout: Optional[str] = None    # override config.rules.prompt_layout
     max_new_tokens: Optional[int] = None   # per-turn cap passed to engine backends
     write_chronicle: bool = True
+    # False: an SPMD mirror of a table another rank persists — the session/chronicle writes (and
+    # their fsyncs) are dropped, reads still go to the project (bench.py / cli.py non-leader ranks)
+    persist: bool = True
+
+
+class _MirrorStore:
+    """Store facade of a non-persisting orchestrator: reads pass through, writes are dropped."""
+    _WRITES = frozenset({"append_round_entry", "append_metrics", "update_status", "write_discussion",
+                         "write_decisions", "append_to_chronicle"})
+
+    def __getattr__(self, name):
+        if name == "create_session":
+            return lambda root, topic: "<mirror>"
+        if name in self._WRITES:
+            return lambda *a, **k: None
+        return getattr(store, name)
 
 
 class Orchestrator:
@@ -123,6 +139,7 @@ class Orchestrator:
         self.store_root = store_root or project_root   # where session/chronicle writes go (SPMD: rank 0 only)
         self.ui = ui
         self.opt = options or RunOptions()
+        self.store = store if self.opt.persist else _MirrorStore()
         self.backend_factory = backend_factory
         self.rng = random.Random(self.opt.shuffle_seed)
         self.failures: List[Tuple[str, str, str]] = []   # (knight, error kind, message) per failed turn
@@ -172,9 +189,9 @@ class Orchestrator:
                            timestamp=iso_now(), metrics=dict(res.metrics))
         all_rounds.append(entry)
         self._append_transcript(entry, res)
-        store.append_round_entry(session_path, entry)
+        self.store.append_round_entry(session_path, entry)
         if res.metrics:
-            store.append_metrics(session_path, {"knight": knight.name, "round": rnd, **res.metrics})
+            self.store.append_metrics(session_path, {"knight": knight.name, "round": rnd, **res.metrics})
         ui = self.ui
         div = ui.knight(knight.name, "─" * 50)
         ui.print(div)
@@ -242,16 +259,16 @@ class Orchestrator:
                     max_src = m
         ctx = build_context(self.root, topic, rules.ignore, cfg.chronicle, self.opt.read_source, max_src,
                             warn=ui.warn)
-        manifest = store.read_manifest(self.root)
-        ctx.manifest_summary = store.manifest_summary(manifest)
-        decrees = store.active_decrees(store.read_decree_log(self.root))
-        ctx.decrees = store.format_decrees_for_prompt(decrees)
+        manifest = self.store.read_manifest(self.root)
+        ctx.manifest_summary = self.store.manifest_summary(manifest)
+        decrees = self.store.active_decrees(self.store.read_decree_log(self.root))
+        ctx.decrees = self.store.format_decrees_for_prompt(decrees)
         if ctx.source_file_contents:
             ui.ok(f"  Context assembled (source: {round(len(ctx.source_file_contents) / 1024)}KB, "
                   f"manifest: {len(manifest['features'])} features, decrees: {len(decrees)})")
         else:
             ui.ok(f"  Context assembled (manifest: {len(manifest['features'])} features, decrees: {len(decrees)})")
-        session_path = continue_from.session_path if continue_from else store.create_session(self.store_root, topic)
+        session_path = continue_from.session_path if continue_from else self.store.create_session(self.store_root, topic)
         if continue_from:
             ui.print("\n  The King has spoken. Back to the table, knights!\n", "bold", "yellow")
         else:
@@ -300,7 +317,7 @@ class Orchestrator:
                 continue
             prompt = self._prompt(knight, self.ctx, visible, rnd, self.cont is not None, files, cmds)
             plan.append((knight, backend, TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens)))
-        store.update_status(self.session_path, phase="discussing", current_knight=None, round=rnd)
+        self.store.update_status(self.session_path, phase="discussing", current_knight=None, round=rnd)
         return plan
 
     def record_parallel(self, rnd: int, order: Sequence[KnightConfig],
@@ -321,7 +338,7 @@ class Orchestrator:
         if backend is None:
             self.ui.warn(f"  {knight.name} didn't show up today. Typical.")
             return None
-        store.update_status(self.session_path, phase="discussing", current_knight=knight.name, round=rnd)
+        self.store.update_status(self.session_path, phase="discussing", current_knight=knight.name, round=rnd)
         prompt = self._prompt(knight, self.ctx, self.all_rounds, rnd, self.cont is not None,
                               self.tool_state["files"], self.tool_state["commands"])
         msgs = THINKING.get(knight.name, ["is thinking...", "prepares their response..."])
@@ -374,9 +391,9 @@ class Orchestrator:
         cfg, rules, ui = self.config, self.config.rules, self.ui
         topic, session_path, all_rounds, latest = self.topic, self.session_path, self.all_rounds, self.latest
         self.round_ms.append(round_ms)
-        store.append_metrics(session_path, {"round": rnd, "round_ms": round_ms, "mode": self.round_mode,
+        self.store.append_metrics(session_path, {"round": rnd, "round_ms": round_ms, "mode": self.round_mode,
                                             "layout": self.layout})
-        store.write_discussion(session_path, all_rounds)
+        self.store.write_discussion(session_path, all_rounds)
         current = list(latest.values())
         tool_state = self.tool_state
         if check_consensus(current, rules.consensus_threshold):
@@ -398,11 +415,11 @@ class Orchestrator:
                 proposal = all_rounds[-1].response if all_rounds else "No proposal text available."
             proposal = proposal if isinstance(proposal, str) else _js_string(proposal)
             lead = select_lead_knight(cfg.knights, current)
-            store.write_decisions(session_path, topic, proposal, all_rounds)
-            store.update_status(session_path, phase="consensus_reached", consensus_reached=True, round=rnd,
+            self.store.write_decisions(session_path, topic, proposal, all_rounds)
+            self.store.update_status(session_path, phase="consensus_reached", consensus_reached=True, round=rnd,
                                 allowed_files=allowed if allowed else UNDEFINED, lead_knight=lead.name)
             if self.opt.write_chronicle:
-                store.append_to_chronicle(self.store_root, cfg.chronicle, topic=topic,
+                self.store.append_to_chronicle(self.store_root, cfg.chronicle, topic=topic,
                                           outcome=f"Consensus in {rnd} round(s). Lead Knight: {lead.name}.\n\n{proposal}",
                                           knights=[b.knight for b in current], date=iso_now()[:10])
             self.result = SessionResult(session_path, True, rnd, proposal, current, all_rounds,
@@ -414,10 +431,10 @@ class Orchestrator:
             ui.print("  Unfortunately, they agree that your idea is terrible.\n", "bold", "red")
             ui.print(summarize_consensus(current))
             rejection = "\n\n---\n\n".join(f"## {e.knight}\n\n{e.response}" for e in all_rounds if e.round == rnd)
-            store.write_decisions(session_path, topic, rejection, all_rounds)
-            store.update_status(session_path, phase="consensus_reached", consensus_reached=True, round=rnd)
+            self.store.write_decisions(session_path, topic, rejection, all_rounds)
+            self.store.update_status(session_path, phase="consensus_reached", consensus_reached=True, round=rnd)
             if self.opt.write_chronicle:
-                store.append_to_chronicle(self.store_root, cfg.chronicle, topic=topic,
+                self.store.append_to_chronicle(self.store_root, cfg.chronicle, topic=topic,
                                           outcome=f"Unanimous rejection in {rnd} round(s). All knights advise against this.",
                                           knights=[b.knight for b in current], date=iso_now()[:10])
             self.result = SessionResult(session_path, True, rnd, rejection, current, all_rounds,
@@ -433,7 +450,7 @@ class Orchestrator:
             return self.result
         self.ui.print("\n  The knights have agreed to disagree. Your move.", "bold", "yellow")
         self.ui.print(summarize_consensus(list(self.latest.values())))
-        store.update_status(self.session_path, phase="escalated", consensus_reached=False, round=self.end)
+        self.store.update_status(self.session_path, phase="escalated", consensus_reached=False, round=self.end)
         self.result = SessionResult(self.session_path, False, self.end, None, list(self.latest.values()),
                                     self.all_rounds, resolved_files=self.tool_state["files"],
                                     resolved_commands=self.tool_state["commands"])
