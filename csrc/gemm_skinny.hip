@@ -68,14 +68,28 @@ int device_cus() {
   return cache[dev] > 0 ? cache[dev] : 0;
 }
 
+// RT_WEIGHT_ORDER=0 pins tile-major weights everywhere (A/B against the shape rule; read once,
+// so shuffle and GEMM launches of one process agree)
+int forced_order() {
+  static const int v = [] {
+    const char* e = getenv("RT_WEIGHT_ORDER");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
 // Ws[t][s][l][j] = W[16t + (l&15)][32s + 8(l>>4) + j] (optionally W * gamma[k] folded in)
 // If rope_rows > 0, output row r < rope_rows takes source row h*D + (p>>1) + (p&1)*D/2
 // (r = h*D + p): the pair-interleaved q/k order the ROPE epilogue expects.
 // swiglu: N = 2I rows [gate; up], stored k-step-paired: Ws[t][s][h][l][j] = W[h*I + 16t + (l&15)][...]
 __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restrict__ W,
-                               const uint16_t* __restrict__ gamma, int N, int K, int rope_rows, int D, int swiglu) {
+                               const uint16_t* __restrict__ gamma, int N, int K, int rope_rows, int D, int swiglu,
+                               int force_order) {
   const int nsteps = K / 32;
   const int64_t total = (int64_t)(N / 16) * nsteps * 64;
+  const int T = swiglu ? N / 32 : N / 16;   // output tiles (SwiGLU: gate + up rows per tile)
+  const int order = force_order >= 0 ? force_order : weight_order(T, nsteps, swiglu != 0, rope_rows > 0);
+  const int recs = swiglu ? 128 : 64;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int l = (int)(i & 63);
     int64_t ts = i >> 6;
@@ -98,16 +112,19 @@ __global__ void shuffle_kernel(short8* __restrict__ Ws, const uint16_t* __restri
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (short)rt::f2bf(rt::bf2f((uint16_t)v[j]) * rt::bf2f((uint16_t)gv[j]));
     }
-    Ws[i] = v;
+    Ws[rec_index((int)t, s, T, nsteps, order, recs) + h * 64 + l] = v;
   }
 }
 
 // Exact inverse of shuffle_kernel's permutation (gamma, if any, stays folded): the row-major
 // weight for the prefill GEMMs when only the shuffled copy is kept resident (70B on one GPU).
 __global__ void unshuffle_kernel(uint16_t* __restrict__ W, const short8* __restrict__ Ws, int N, int K, int rope_rows,
-                                 int D, int swiglu) {
+                                 int D, int swiglu, int force_order) {
   const int nsteps = K / 32;
   const int64_t total = (int64_t)(N / 16) * nsteps * 64;
+  const int T = swiglu ? N / 32 : N / 16;
+  const int order = force_order >= 0 ? force_order : weight_order(T, nsteps, swiglu != 0, rope_rows > 0);
+  const int recs = swiglu ? 128 : 64;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int l = (int)(i & 63);
     int64_t ts = i >> 6;
@@ -124,7 +141,7 @@ __global__ void unshuffle_kernel(uint16_t* __restrict__ W, const short8* __restr
       row = hh * D + (p >> 1) + (p & 1) * (D >> 1);
     }
     const int k0 = 32 * s + 8 * (l >> 4);
-    *reinterpret_cast<short8*>(W + (size_t)row * K + k0) = Ws[i];
+    *reinterpret_cast<short8*>(W + (size_t)row * K + k0) = Ws[rec_index((int)t, s, T, nsteps, order, recs) + h * 64 + l];
   }
 }
 }  // namespace
@@ -137,7 +154,7 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
   const int64_t total = (int64_t)(N / 16) * (K / 32) * 64;
   const int64_t grid = (total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536;
   hipLaunchKernelGGL(unshuffle_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (uint16_t*)W, (const short8*)Ws,
-                     N, K, rope_rows, D, swiglu);
+                     N, K, rope_rows, D, swiglu, forced_order());
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -155,8 +172,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     const int T = N / 16;
     const int R = cus > 0 ? T % cus : 0;
     if (cus > 0 && T > cus && R > 0 && R <= SPLIT_CTRS && split_ws_ints >= split_workspace_ints(R)) {
-      const GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
-                          eps, {}, nullptr, nullptr};
+      GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
+                    eps, {}, nullptr, nullptr};
+      args.kmajor = forced_order();
       const dim3 grid(T + R);
       if (pro == PRO_NORM && epi == EPI_SWIGLU)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_SWIGLU, 4, 2>), grid, dim3(256), 0, stream, args,
@@ -211,8 +229,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
       default: RT_SGV(P, E, 4, 4); break;                                                                    \
     }                                                                                                        \
   } while (0)
-  const GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
-                      eps, re, (const uint16_t*)x2, (uint16_t*)xo};
+  GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
+                eps, re, (const uint16_t*)x2, (uint16_t*)xo};
+  args.kmajor = forced_order();
 #define RT_SGV(P, E, NWV, UV) \
   hipLaunchKernelGGL((skinny_gemm_kernel<P, E, NWV, UV>), grid, dim3(NWV * 64), 0, stream, args)
   if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SG(PRO_PLAIN, EPI_STORE);
@@ -239,7 +258,7 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
   int64_t grid = (total + 255) / 256;
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(shuffle_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (short8*)Ws, (const uint16_t*)W,
-                     (const uint16_t*)gamma, N, K, rope_rows, D, swiglu);
+                     (const uint16_t*)gamma, N, K, rope_rows, D, swiglu, forced_order());
   return 0;
 }
 

@@ -51,6 +51,9 @@ struct GemmArgs {
   RopeEpi re;
   const uint16_t* x2;  // NORM_ADD
   uint16_t* xo;        // NORM_ADD: where workgroup `xo_wg` publishes x + x2
+  // weight record order (see weight_order): -1 = the shape's rule, as shuffle_weight wrote it;
+  // 0 / c > 0 pinned (layout experiments, tools/exp_balance.hip)
+  int kmajor = -1;
 };
 
 template <int NACC, int NW>   // NACC = accumulators per lane (2 for SwiGLU gate + up)
@@ -125,20 +128,72 @@ struct Stage {
   short8 b[(PRO == PRO_NORM_ADD) ? U : 1];
 };
 
+// short8 records per k-step of one tile (SwiGLU: gate + up)
+template <int EPI>
+constexpr size_t krec() { return (EPI == EPI_SWIGLU) ? 128 : 64; }
+
+// Weight record order, chosen from the shape so that the shuffle (gemm_skinny.hip) and every
+// GEMM launch agree without carrying a layout tag: 0 = tile-major (one contiguous panel per
+// tile); c > 0 = k-chunks of 2^(c-1) steps (all tiles' chunks for one k range adjacent, so the
+// concurrently streaming workgroups spread over every HBM channel instead of camping on a few
+// long panels). tools/exp_balance.hip layouts, MI355X, M = 3: down (K 14336, 1 tile per CU)
+// 20.97 -> 19.70 us k-major; qkv 11.25 -> 10.82 chunks of 4; gate_up 39.2-39.9 -> 38.7-39.0
+// chunks of 16; lm_head 157.3 -> 148.3 chunks of 16; o (K 4096) unchanged, kept tile-major.
+__host__ __device__ inline int weight_order(int tiles, int ksteps, bool swiglu, bool rope) {
+  int order = 0;
+  if (swiglu) order = 5;
+  else if (rope) order = 3;
+  else if (tiles >= 4096) order = 5;
+  else if (ksteps >= 384) order = 1;
+  if (order > 0 && ksteps % (1 << (order - 1)) != 0) order = 0;   // chunks must tile K exactly
+  return order;
+}
+
+// index of the first record of (tile t, k-step s) in a layout of T tiles x ks steps
+__host__ __device__ inline size_t rec_index(int t, int s, int T, int ks, int order, int recs) {
+  if (order <= 0) return ((size_t)t * ks + s) * recs;
+  const int lc = order - 1, C = 1 << lc;
+  return ((size_t)(s >> lc) * T * C + (size_t)t * C + (s & (C - 1))) * recs;
+}
+
+struct WStride {
+  int lc;          // log2(k-steps per chunk) (30: tile-major, one chunk)
+  size_t cstride;  // records between consecutive chunks of one tile
+  RT_DEVICE size_t off(int s, size_t rec) const {
+    return (size_t)(s >> lc) * cstride + (size_t)(s & ((1 << lc) - 1)) * rec;
+  }
+};
+
 template <int PRO, int EPI, int NW, int U>
 RT_DEVICE void issue_w(Stage<PRO, EPI, U>& st, const short8* __restrict__ wt, const short8* __restrict__ wt2, int s0,
-                       int nsteps, int lane) {
+                       int nsteps, int lane, WStride ws) {
   // SwiGLU weights are stored k-step-paired ([tile][step][gate|up][64 lanes][8]): one wave streams
   // 2 KiB contiguous per step instead of two 1-KiB streams 117 MB apart (`wt2` unused)
-  constexpr size_t kStride = (EPI == EPI_SWIGLU) ? 128 : 64;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     // unconditional (steps past the end re-read the last one: an L2 hit) so hipcc counts the
     // loads and waits vmcnt(next stage) before a stage's MFMAs instead of draining vmcnt(0)
     const int s = min(s0 + NW * u, nsteps - 1);
-    st.w[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + lane);
-    if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt + (size_t)s * kStride + 64 + lane);
+    const size_t o = ws.off(s, krec<EPI>());
+    st.w[u] = __builtin_nontemporal_load(wt + o + lane);
+    if constexpr (EPI == EPI_SWIGLU) st.w2[u] = __builtin_nontemporal_load(wt + o + 64 + lane);
   }
+}
+
+// first record of `tile` and the distance between its k-steps, for either weight order
+template <int EPI>
+RT_DEVICE const short8* tile_base(const GemmArgs& p, int tile, WStride& ws) {
+  const size_t T = (size_t)p.N / 16, ks = (size_t)p.K / 32;
+  const int order = p.kmajor >= 0 ? p.kmajor : weight_order((int)T, (int)ks, EPI == EPI_SWIGLU, EPI == EPI_ROPE);
+  if (order <= 0) {
+    ws.lc = 30;
+    ws.cstride = 0;
+    return p.Ws + (size_t)tile * ks * krec<EPI>();
+  }
+  ws.lc = order - 1;
+  const size_t chunk = (size_t)1 << ws.lc;
+  ws.cstride = T * chunk * krec<EPI>();
+  return p.Ws + (size_t)tile * chunk * krec<EPI>();
 }
 
 template <int PRO, int EPI, int NW, int U, bool SC1>
@@ -194,9 +249,10 @@ template <int PRO, int EPI, int NW, int U>
 RT_DEVICE void gemm_prefetch(const GemmArgs& p, int tile, Stage<PRO, EPI, U>& st0) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nsteps = p.K / 32;
-  const short8* wt = p.Ws + (size_t)tile * nsteps * ((EPI == EPI_SWIGLU) ? 128 : 64);
+  WStride sstride;
+  const short8* wt = tile_base<EPI>(p, tile, sstride);
   const short8* wt2 = nullptr;
-  issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane);
+  issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane, sstride);
 }
 
 // One 16-column tile. `st0` may hold this tile's prefetched stage-0 weights (prefetched=true).
@@ -221,7 +277,8 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   uint16_t* xo_r =
       (PRO == PRO_NORM_ADD && publish_xo && row_ok && p.xo != nullptr) ? p.xo + (size_t)r * K + 8 * g : nullptr;
   const XSrc xo_s = make_xsrc<SC1>(PRO == PRO_NORM_ADD && p.xo != nullptr ? p.xo : p.x, lane_elem);
-  const short8* wt = p.Ws + (size_t)tile * ksteps * ((EPI == EPI_SWIGLU) ? 128 : 64);
+  WStride sstride;
+  const short8* wt = tile_base<EPI>(p, tile, sstride);
   const short8* wt2 = nullptr;
 
   float4_ acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
@@ -233,15 +290,15 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   constexpr int SPAN = NW * U;
   const int w0 = s_lo + wid;   // this wave's first k-step
   const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
-  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, w0, nsteps, lane);
+  if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, w0, nsteps, lane, sstride);
   issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, w0, nsteps);
   int j = 0;
   for (; j + 1 < nst; j += 2) {
     const int s = w0 + SPAN * j;
-    issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane);
+    issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane, sstride);
     issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
     consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
-    issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane);
+    issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane, sstride);
     issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
     consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
   }

@@ -21,8 +21,10 @@ def close(a, b, atol, rtol=0.0):
 
 
 @pytest.mark.parametrize("M", [1, 3, 16])
-@pytest.mark.parametrize("N,K", [(256, 512), (4096, 4096), (1024, 14336), (48, 96)])
+@pytest.mark.parametrize("N,K", [(256, 512), (4096, 4096), (1024, 14336), (48, 96), (65536, 512)])
 def test_skinny_gemm_modes(M, N, K):
+    # weight orders (skinny_core.h weight_order): (1024, 14336) k-major, (65536, 512) k-chunks of
+    # 16 (lm_head rule), SwiGLU chunks of 16 where K allows, the rest tile-major
     x = bf(M, K, seed=51)
     W = bf(N, K, scale=0.05, seed=52)
     gam = bf(K, seed=53)

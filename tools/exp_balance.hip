@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 using namespace skinny;
@@ -41,35 +42,52 @@ __global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed) {
   } while (0)
 }  // namespace
 
-int main() {
-  const int M = 3, K = 4096;
-  const int tiles[] = {256, 384, 448, 512, 640, 768, 896, 960, 1024, 1152, 1280};
-  uint16_t *x, *out;
+int main(int argc, char** argv) {
+  const int M = 3;
+  uint16_t *x, *out, *res;
   CK(hipMalloc(&x, (size_t)16 * 16384 * 2));
-  CK(hipMalloc(&out, (size_t)16 * 32768 * 2));
+  CK(hipMalloc(&out, (size_t)16 * 131072 * 2));
+  CK(hipMalloc(&res, (size_t)16 * 131072 * 2));
   hipLaunchKernelGGL(fill_kernel, dim3(256), dim3(256), 0, 0, x, (size_t)16 * 16384, 7);
-  // rotate over enough weight copies (>= 1 GiB) that the 256 MB MALL cannot serve repeats
-  const int copies = 6;
-  std::vector<uint16_t*> w(copies);
-  const size_t wmax = (size_t)1280 * 16 * 2 * K;   // swiglu: 2 rows per output column
-  for (int c = 0; c < copies; ++c) {
-    CK(hipMalloc(&w[c], wmax * 2));
-    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, w[c], wmax, 11 + c);
-  }
+  hipLaunchKernelGGL(fill_kernel, dim3(256), dim3(256), 0, 0, res, (size_t)16 * 131072, 9);
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  for (int kind = 0; kind < 2; ++kind) {   // 0 swiglu 4x2 (gate_up), 1 norm 4x2 plain store (qkv-like)
-    for (int t : tiles) {
-      const int N = t * 16;
+  const bool layouts = argc > 1 && argv[1][0] == 'l';
+  struct Shape { const char* name; int kind; int tiles; int K; };
+  // kind 0 swiglu (norm, 4x2), 1 norm store (4x2), 2 plain resid (4x4)
+  std::vector<Shape> shapes;
+  if (layouts) {
+    shapes = {{"o", 2, 256, 4096}, {"down", 2, 256, 14336}, {"qkv-like", 1, 384, 4096},
+              {"gate_up", 0, 896, 4096}, {"lm_head", 1, 8016, 4096}};
+  } else {
+    for (int t : {256, 384, 448, 512, 640, 768, 896, 960, 1024, 1152, 1280}) shapes.push_back({"swiglu", 0, t, 4096});
+    for (int t : {256, 384, 448, 512, 640, 768, 896, 960, 1024, 1152, 1280}) shapes.push_back({"norm", 1, t, 4096});
+  }
+  for (const Shape& sh : shapes) {
+    const int t = sh.tiles, K = sh.K, N = t * 16;
+    const size_t welems = (size_t)N * K * (sh.kind == 0 ? 2 : 1);
+    const int copies = (int)std::max<size_t>(2, (size_t)(1.5e9 / (welems * 2.0)) + 1);
+    std::vector<uint16_t*> w(copies);
+    for (int c = 0; c < copies; ++c) {
+      CK(hipMalloc(&w[c], welems * 2));
+      hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, w[c], welems, 11 + c);
+    }
+    const int kms[] = {0, 1, 3, 4, 5};   // tile-major, k-major, k-chunks of 4 / 8 / 16 steps
+    for (int kmi = 0; kmi < (layouts ? 5 : 1); ++kmi) {
+      const int km = kms[kmi];
       auto launch = [&](int i) {
-        GemmArgs p{out, x, (const short8*)w[i % copies], nullptr, M, N, K, N, 1e-5f, {}, nullptr, nullptr};
-        if (kind == 0)
+        GemmArgs p{sh.kind == 0 ? out : (sh.kind == 1 ? out : nullptr), x, (const short8*)w[i % copies],
+                   sh.kind == 2 ? res : nullptr, M, N, K, N, 1e-5f, {}, nullptr, nullptr};
+        p.kmajor = km;
+        if (sh.kind == 0)
           hipLaunchKernelGGL((plain_kernel<PRO_NORM, EPI_SWIGLU, 4, 2>), dim3(t), dim3(256), 0, s, p);
-        else
+        else if (sh.kind == 1)
           hipLaunchKernelGGL((plain_kernel<PRO_NORM, EPI_STORE, 4, 2>), dim3(t), dim3(256), 0, s, p);
+        else
+          hipLaunchKernelGGL((plain_kernel<PRO_PLAIN, EPI_RESID, 4, 4>), dim3(t), dim3(256), 0, s, p);
       };
       hipGraph_t g;
       hipGraphExec_t ge;
@@ -91,13 +109,15 @@ int main() {
         if (ms < best) best = ms;
       }
       const double us = best * 1e3 / R;
-      const double bytes = (double)N * K * 2 * (kind == 0 ? 2 : 1);
-      printf("%-8s tiles=%5d (%.2f per CU)  %7.2f us  %5.2f TB/s  %6.3f us per tile-per-CU\n",
-             kind == 0 ? "swiglu" : "norm", t, t / 256.0, us, bytes / us / 1e6, us / (t / 256.0));
+      char lay[32];
+      snprintf(lay, sizeof lay, km == 0 ? "tile-major" : (km == 1 ? "k-major" : "k-chunk %d"), 1 << (km - 1));
+      printf("%-9s %-11s tiles=%5d (%.2f per CU) K=%5d  %8.2f us  %5.2f TB/s\n", sh.name, layouts ? lay : "", t,
+             t / 256.0, K, us, welems * 2.0 / us / 1e6);
       fflush(stdout);
       CK(hipGraphExecDestroy(ge));
       CK(hipGraphDestroy(g));
     }
+    for (auto p : w) CK(hipFree(p));
   }
   return 0;
 }
