@@ -75,8 +75,8 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&w[c], welems * 2));
       hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, w[c], welems, 11 + c);
     }
-    const int kms[] = {0, 1, 3, 4, 5};   // tile-major, k-major, k-chunks of 4 / 8 / 16 steps
-    for (int kmi = 0; kmi < (layouts ? 5 : 1); ++kmi) {
+    const int kms[] = {0, 1, 2, 3, 4, 5, 6, 7};   // tile-major, k-major, k-chunks of 2 .. 64 steps
+    for (int kmi = 0; kmi < (layouts ? 8 : 1); ++kmi) {
       const int km = kms[kmi];
       auto launch = [&](int i) {
         GemmArgs p{sh.kind == 0 ? out : (sh.kind == 1 ? out : nullptr), x, (const short8*)w[i % copies],
