@@ -292,6 +292,22 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
   if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, w0, nsteps, lane, sstride);
   issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, w0, nsteps);
+  // Epilogue operands that do not depend on the GEMM are loaded NOW, so their round trips hide
+  // under the k-loop instead of following the last MFMA: the residual element (RESID) and the
+  // K/V slot, position and cos/sin pair (ROPE). Unconditional, rows clamped (no branch for the
+  // waitcnt pass to merge); the epilogue thread (em, en) is the one that uses them.
+  const int em = min((int)(threadIdx.x >> 4), M - 1), en = threadIdx.x & 15;
+  float e_res = 0.f, e_c = 0.f, e_s = 0.f;
+  int64_t e_slot = 0;
+  if constexpr (EPI == EPI_RESID) e_res = ld16<SC1>(p.res + (size_t)em * N + tile * 16 + en);
+  if constexpr (EPI == EPI_ROPE) {
+    const RopeEpi& re = p.re;
+    const int pp = (tile * 16 + en) % re.D;
+    e_slot = re.slots[em];
+    const float* cs = re.cos_sin + (size_t)re.positions[em] * re.D;
+    e_c = cs[pp >> 1];
+    e_s = cs[(re.D >> 1) + (pp >> 1)];
+  }
   int j = 0;
   for (; j + 1 < nst; j += 2) {
     const int s = w0 + SPAN * j;
@@ -362,12 +378,12 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
       st16<SC1>(p.out + (size_t)m * p.ldo + col, silu(v) * up);
     } else if constexpr (EPI == EPI_RESID) {
       uint16_t* rp = p.res + (size_t)m * N + col;
-      st16<SC1>(rp, v + ld16<SC1>(rp));
+      st16<SC1>(rp, v + e_res);
     } else if constexpr (EPI == EPI_ROPE) {
       const RopeEpi& re = p.re;
       const int D = re.D, half = D >> 1;
       const int h = col / D, pp = col - h * D;
-      const int64_t slot = re.slots[m];
+      const int64_t slot = e_slot;
       const int64_t blk = slot / re.BS;
       const int off = (int)(slot - blk * re.BS);
       if (h < re.Hq + re.Hkv) {
@@ -376,8 +392,7 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
         for (int w = 0; w < NW; ++w) partner += sm.red[w][0][m][n ^ 1];
         partner *= inv;
         const int i = pp >> 1, hi = pp & 1;
-        const float* cs = re.cos_sin + (size_t)re.positions[m] * D;
-        const float c = cs[i], sn = cs[half + i];
+        const float c = e_c, sn = e_s;
         // pair (x1 = d i, x2 = d i+D/2): y1 = x1 c - x2 s ; y2 = x2 c + x1 s
         const float y = hi ? fmaf(v, c, partner * sn) : fmaf(v, c, -partner * sn);
         const int d = i + hi * half;
