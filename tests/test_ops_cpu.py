@@ -113,3 +113,14 @@ def test_debug_env_mode():
     assert env["AMD_SERIALIZE_KERNEL"] == "3" and env["ROUNDTABLE_DEBUG_CHECKS"] == "1"
     assert env["HIP_LAUNCH_BLOCKING"] == "0"          # explicit settings win
     assert not apply_debug_env({})
+
+
+def test_split_workspace_matches_native_layout():
+    """ops.SPLIT_WS_INTS (Python allocation of the CU-balanced GEMM workspace) covers what the
+    launcher needs for the largest remainder (255 split tiles); the extension imports on a CPU
+    host, so the check runs here."""
+    import pytest
+    if not ops.native_available():
+        pytest.skip("native extension not built")
+    assert ops.SPLIT_WS_INTS >= ops.native().split_workspace_ints(255)
+    assert ops.split_workspace("cpu").numel() == ops.SPLIT_WS_INTS
