@@ -259,3 +259,42 @@ def test_bench_consensus_round_variant():
     d = out["detail"]
     assert d["consensus_reached"] == 1 and d["consensus_round"] == 3
     assert d["decode_tokens"] == 3 * 8 * 2 and d["forced_tokens"] > 0
+
+
+def _overlap_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from theroundtaible_amd.parallel.cluster import Cluster
+        from theroundtaible_amd.parallel.exchange import TokenExchange
+        c = Cluster(rank=rank, world=world, backend="gloo", cpu_group=dist.new_group(backend="gloo"))
+        ex = TokenExchange(c, rows=1, width=16, device="cpu")
+        order = []
+        ex.start([(rank, [rank] * (rank + 2))])          # token all-gather in flight ...
+        order.append("started")
+        meta = c.all_gather_object({"rank": rank})       # ... while the metadata round runs
+        order.append("metadata")
+        got = ex.wait()
+        order.append("tokens")
+        q.put((rank, order, [m["rank"] for m in meta], got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c1_token_gather_overlaps_metadata_round():
+    """C1 ordering (knights/distributed.py): the static token all-gather is issued first and
+    left in flight, the gloo metadata round completes, then the tokens are collected."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, m, g)) for r, o, m, g in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        order, meta, got = res[r]
+        assert order == ["started", "metadata", "tokens"] and meta == [0, 1]
+        assert got == {0: [0, 0], 1: [1, 1, 1]}
