@@ -208,11 +208,13 @@ def main() -> int:
     dec = pre = reused = forced = 0
     # engine time per timed round (the slowest turn of the round: turns of one engine batch run
     # together) vs the round's wall clock: the rest is host work (prompts, parse, files, C1)
-    eng_ms = {}
+    eng_ms, pre_ms, dec_ms = {}, {}, {}
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
                 eng_ms[e.round] = max(eng_ms.get(e.round, 0.0), float(e.metrics.get("turn_ms", 0.0)))
+                pre_ms[e.round] = max(pre_ms.get(e.round, 0.0), float(e.metrics.get("prefill_ms", 0.0)))
+                dec_ms[e.round] = max(dec_ms.get(e.round, 0.0), float(e.metrics.get("decode_ms", 0.0)))
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
@@ -253,6 +255,8 @@ def main() -> int:
                    "consensus_reached": sum(1 for o in orchs if o.result is not None and o.result.consensus),
                    "forced_tokens": forced,
                    "engine_ms_per_round": round(sum(eng_ms.values()) / n_timed, 2),
+                   "engine_prefill_ms_per_round": round(sum(pre_ms.values()) / n_timed, 2),
+                   "engine_decode_ms_per_round": round(sum(dec_ms.values()) / n_timed, 2),
                    "host_ms_per_round": round(ms_round - sum(eng_ms.values()) / n_timed, 2)},
     }
     if cl.rank == 0:
