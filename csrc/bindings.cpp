@@ -42,7 +42,9 @@ int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_
 int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
                         int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream);
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
-                          const int64_t* next, int B, int max_steps, hipStream_t stream);
+                          const int64_t* next, int B, int max_steps, int64_t* slots, int64_t* offsets, void* res,
+                          const int* block_tables, const void* embed, int max_blocks, int BS, int H, int64_t vocab,
+                          hipStream_t stream);
 int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, const void* wo, const void* wgu,
                         const void* wd, const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                         const int64_t* slots, const int* block_tables, const int* ctx_lens, float* part_o,
@@ -392,7 +394,9 @@ void decode_prep(torch::Tensor slots, torch::Tensor offsets, torch::Tensor res, 
 }
 
 void decode_advance(torch::Tensor out, torch::Tensor ids, torch::Tensor positions, torch::Tensor ctx_lens,
-                    torch::Tensor step, torch::Tensor next) {
+                    torch::Tensor step, torch::Tensor next, c10::optional<torch::Tensor> slots,
+                    c10::optional<torch::Tensor> offsets, c10::optional<torch::Tensor> res,
+                    c10::optional<torch::Tensor> block_tables, c10::optional<torch::Tensor> embed, int64_t block_size) {
   check_type(out, torch::kInt64, "out");
   check_type(ids, torch::kInt64, "ids");
   check_type(positions, torch::kInt64, "positions");
@@ -403,9 +407,38 @@ void decode_advance(torch::Tensor out, torch::Tensor ids, torch::Tensor position
   TORCH_CHECK(out.dim() == 2 && out.size(1) == B && next.numel() == B && positions.numel() == B &&
                   ctx_lens.numel() == B,
               "decode_advance: shapes");
-  launch_decode_advance(out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), positions.data_ptr<int64_t>(),
-                        ctx_lens.data_ptr<int>(), step.data_ptr<int64_t>(), next.data_ptr<int64_t>(), (int)B,
-                        (int)out.size(0), cur_stream());
+  int64_t* sp = nullptr;
+  int64_t* op = nullptr;
+  void* rp = nullptr;
+  const int* btp = nullptr;
+  const void* ep = nullptr;
+  int maxb = 0, H = 0;
+  int64_t V = 0;
+  if (res.has_value() && res->defined()) {   // fused next-step prep (decode_prep semantics)
+    TORCH_CHECK(slots.has_value() && offsets.has_value() && block_tables.has_value() && embed.has_value(),
+                "decode_advance: prep needs slots, offsets, block_tables, embed");
+    check_type(*slots, torch::kInt64, "slots");
+    check_type(*offsets, torch::kInt64, "offsets");
+    check_type(*block_tables, torch::kInt32, "block_tables");
+    check_bf16(*res, "res");
+    check_bf16(*embed, "embed");
+    TORCH_CHECK(slots->numel() >= B && offsets->numel() >= B && block_tables->size(0) >= B && res->dim() == 2 &&
+                    res->size(0) == B && embed->dim() == 2 && res->size(1) == embed->size(1) && block_size > 0,
+                "decode_advance: prep shapes");
+    sp = slots->data_ptr<int64_t>();
+    op = offsets->data_ptr<int64_t>();
+    rp = res->data_ptr();
+    btp = block_tables->data_ptr<int>();
+    ep = embed->data_ptr();
+    maxb = (int)block_tables->size(1);
+    H = (int)embed->size(1);
+    V = embed->size(0);
+  }
+  const int rc = launch_decode_advance(out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), positions.data_ptr<int64_t>(),
+                                       ctx_lens.data_ptr<int>(), step.data_ptr<int64_t>(), next.data_ptr<int64_t>(),
+                                       (int)B, (int)out.size(0), sp, op, rp, btp, ep, maxb, (int)block_size, H, V,
+                                       cur_stream());
+  TORCH_CHECK(rc == 0, "decode_advance: unsupported configuration (rc=", rc, ")");
 }
 
 // Debug paging guard (csrc/decode_step.hip): err[0] |= violation code; capturable.
@@ -558,7 +591,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("oneshot_clear_error", [](int64_t id) { return oneshot_clear_error((int)id); });
   m.def("oneshot_set_poll_limit", [](int64_t id, int64_t limit) { return oneshot_set_poll_limit((int)id, limit); });
   m.def("oneshot_destroy", [](int64_t id) { oneshot_destroy((int)id); });
-  m.def("decode_advance", &decode_advance);
+  m.def("decode_advance", &decode_advance, py::arg("out"), py::arg("ids"), py::arg("positions"), py::arg("ctx_lens"),
+        py::arg("step"), py::arg("next"), py::arg("slots") = py::none(), py::arg("offsets") = py::none(),
+        py::arg("res") = py::none(), py::arg("block_tables") = py::none(), py::arg("embed") = py::none(),
+        py::arg("block_size") = 0);
   m.def("paging_guard", &paging_guard, py::arg("block_tables"), py::arg("ctx_lens"), py::arg("positions"),
         py::arg("slots"), py::arg("err"), py::arg("num_blocks"), py::arg("block_size"));
   m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));

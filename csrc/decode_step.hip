@@ -6,6 +6,9 @@
 //                    res[b, :] = embed[ids[b], :]                          (embedding gather)
 //   decode_advance : out[step, b] = next[b]; ids[b] = next[b]; pos[b] += 1; ctx[b] += 1;
 //                    step += 1                                              (after sampling)
+//                    and, given the prep operands, the NEXT step's decode_prep from the new
+//                    ids / positions (the captured step then has one bookkeeping launch; the
+//                    first step of a turn is prepped once, outside the graph)
 //
 // Everything the next replay needs stays on the device, so a hipGraph replay takes no host
 // input. One workgroup per batch row; the embedding row copy is 16 B per lane.
@@ -19,7 +22,8 @@ __global__ void __launch_bounds__(256) decode_prep_kernel(
   const int b = blockIdx.x;
   const int64_t pos = positions[b];
   if (threadIdx.x == 0) {
-    const int64_t blk = block_tables[(size_t)b * max_blocks + pos / BS];
+    const int64_t bi = pos / BS;   // past the table: a slot that is never written
+    const int64_t blk = bi < max_blocks ? block_tables[(size_t)b * max_blocks + bi] : 0;
     slots[b] = blk * BS + pos % BS;
     offsets[b] = pos + 1;
   }
@@ -30,17 +34,44 @@ __global__ void __launch_bounds__(256) decode_prep_kernel(
   for (int i = threadIdx.x; i < H / 8; i += blockDim.x) dst[i] = src[i];
 }
 
-__global__ void __launch_bounds__(64) decode_advance_kernel(int64_t* __restrict__ out, int64_t* __restrict__ ids,
-                                                            int64_t* __restrict__ positions, int* __restrict__ ctx_lens,
-                                                            int64_t* __restrict__ step, const int64_t* __restrict__ next,
-                                                            int B, int max_steps) {
+struct PrepArgs {   // next-step prep (all null: advance only)
+  int64_t* slots;
+  int64_t* offsets;
+  uint16_t* res;
+  const int* block_tables;
+  const uint16_t* embed;
+  int max_blocks, BS, H;
+  int64_t vocab;
+};
+
+__global__ void __launch_bounds__(256) decode_advance_kernel(int64_t* __restrict__ out, int64_t* __restrict__ ids,
+                                                             int64_t* __restrict__ positions, int* __restrict__ ctx_lens,
+                                                             int64_t* __restrict__ step, const int64_t* __restrict__ next,
+                                                             int B, int max_steps, PrepArgs pa) {
   const int64_t st = *step;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const int64_t t = next[b];
     if (st < max_steps) out[st * B + b] = t;
     ids[b] = t;
-    positions[b] += 1;
+    const int64_t p = positions[b] + 1;
+    positions[b] = p;
     ctx_lens[b] += 1;
+    if (pa.slots != nullptr) {   // past the table (a turn's last step) the slot is never used
+      const int64_t bi = p / pa.BS;
+      const int64_t blk = bi < pa.max_blocks ? pa.block_tables[(size_t)b * pa.max_blocks + bi] : 0;
+      pa.slots[b] = blk * pa.BS + p % pa.BS;
+      pa.offsets[b] = p + 1;
+    }
+  }
+  if (pa.res != nullptr) {       // next step's embedding rows, 16 B per lane
+    const int row8 = pa.H / 8;
+    for (int i = threadIdx.x; i < B * row8; i += blockDim.x) {
+      const int b = i / row8, j = i - b * row8;
+      int64_t tok = next[b];
+      tok = tok < 0 ? 0 : (tok >= pa.vocab ? pa.vocab - 1 : tok);
+      reinterpret_cast<uint4*>(pa.res)[(size_t)b * row8 + j] =
+          reinterpret_cast<const uint4*>(pa.embed)[(size_t)tok * row8 + j];
+    }
   }
   __syncthreads();  // every lane has read *step before lane 0 bumps it
   if (threadIdx.x == 0) *step = st + 1;
@@ -58,10 +89,18 @@ int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_
 }
 
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
-                          const int64_t* next, int B, int max_steps, hipStream_t stream) {
+                          const int64_t* next, int B, int max_steps, int64_t* slots, int64_t* offsets, void* res,
+                          const int* block_tables, const void* embed, int max_blocks, int BS, int H, int64_t vocab,
+                          hipStream_t stream) {
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(64), 0, stream, out, ids, positions, ctx_lens, step, next,
-                     B, max_steps);
+  const bool prep = res != nullptr;
+  if (prep && (slots == nullptr || offsets == nullptr || block_tables == nullptr || embed == nullptr || H % 8 ||
+               BS <= 0 || max_blocks <= 0 || vocab <= 0))
+    return -1;
+  const PrepArgs pa{prep ? slots : nullptr, prep ? offsets : nullptr, (uint16_t*)res, block_tables,
+                    (const uint16_t*)embed, max_blocks, BS, H, vocab};
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(256), 0, stream, out, ids, positions, ctx_lens, step, next,
+                     B, max_steps, pa);
   return 0;
 }
 

@@ -19,7 +19,9 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
 int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
                         int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream);
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
-                          const int64_t* next, int B, int max_steps, hipStream_t stream);
+                          const int64_t* next, int B, int max_steps, int64_t* slots, int64_t* offsets, void* res,
+                          const int* block_tables, const void* embed, int max_blocks, int BS, int H, int64_t vocab,
+                          hipStream_t stream);
 int prefill32_rows(int G);
 int launch_kv_block_copy(void* k, void* v, const int* src, const int* dst, int n, int L, int num_blocks,
                          int64_t block_elems, hipStream_t stream);
@@ -74,7 +76,7 @@ int main() {
   EXPECT(launch_unshuffle_weight(nullptr, nullptr, 32, 64, 64, 128, 0, nullptr) == -1);
   EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 2, 0, 16, 32, nullptr) == -1);
   EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 0, 4, 16, 32, nullptr) == 0);
-  EXPECT(launch_decode_advance(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 8, nullptr) == 0);
+  EXPECT(launch_decode_advance(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 8, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, nullptr) == 0);
   // prefill tile geometry
   EXPECT(prefill32_rows(4) == 64 && prefill32_rows(8) == 32 && prefill32_rows(1) == 256 && prefill32_rows(3) == 0);
   std::printf("host_check: %d failure(s)\n", failures);

@@ -344,3 +344,35 @@ def test_paging_guard_matches_reference():
         ops.paging_guard(bt.to(DEV), ctx.to(DEV), pos.to(DEV), slots.to(DEV), got, nb, bs)
         assert int(got.item()) == int(want[0]), (trial, kind)
         assert (kind == 0) == (int(want[0]) == 0)
+
+
+def test_decode_prep_and_fused_advance_match_reference():
+    """csrc/decode_step.hip: decode_prep and decode_advance (plain and with the fused next-step
+    prep) against the PyTorch semantics in ops/reference.py, including a row whose advanced
+    position runs past its block table."""
+    torch.manual_seed(3)
+    B, maxb, bs, H, V = 5, 4, 32, 4096, 1000
+    bt = torch.randint(0, 50, (B, maxb), dtype=torch.int32)
+    pos = torch.tensor([0, 31, 64, 100, maxb * bs - 1])
+    ids = torch.tensor([1, 999, 5, 1200, -3])
+    emb = torch.randn(V, H).bfloat16()
+    out = torch.zeros(8, B, dtype=torch.int64)
+    ctx = (pos + 1).to(torch.int32)
+    step = torch.zeros(1, dtype=torch.int64)
+    nxt = torch.tensor([7, 8, 9, 10, 11])
+    st_ref = [t.clone() for t in (out, ids, pos, ctx, step)]
+    st_gpu = [t.cuda() for t in (out, ids, pos, ctx, step)]
+    bufs_ref = [torch.zeros(B, dtype=torch.int64), torch.zeros(B, dtype=torch.int64), torch.zeros(B, H).bfloat16()]
+    bufs_gpu = [t.cuda() for t in bufs_ref]
+    ref.decode_prep(*bufs_ref, st_ref[1], st_ref[2], bt, emb, bs)
+    ops.decode_prep(*bufs_gpu, st_gpu[1], st_gpu[2], bt.cuda(), emb.cuda(), bs)
+    for a, b in zip(bufs_ref, bufs_gpu):
+        assert torch.equal(a, b.cpu())
+    ref.decode_advance(*st_ref, nxt, prep=(*bufs_ref, bt, emb, bs))
+    ops.decode_advance(*st_gpu, nxt.cuda(), prep=(*bufs_gpu, bt.cuda(), emb.cuda(), bs))
+    ref.decode_advance(*st_ref, nxt + 1)
+    ops.decode_advance(*st_gpu, nxt.cuda() + 1)
+    torch.cuda.synchronize()
+    for a, b in zip(st_ref + bufs_ref, st_gpu + bufs_gpu):
+        assert torch.equal(a, b.cpu())
+    assert bufs_ref[0][4].item() == (maxb * bs) % bs   # past the table: block 0

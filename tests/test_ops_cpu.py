@@ -75,6 +75,15 @@ def test_decode_prep_and_advance_reference():
     ops.decode_advance(out, ids, pos, ctx, step, torch.tensor([11, 12]))
     assert out[0].tolist() == [11, 12] and ids.tolist() == [11, 12]
     assert pos.tolist() == [34, 65] and ctx.tolist() == [35, 66] and step.item() == 1
+    # fused next-step prep: same result as a separate decode_prep on the advanced state
+    s2, o2, r2 = torch.zeros_like(slots), torch.zeros_like(offs), torch.zeros_like(res)
+    ops.decode_advance(out, ids, pos, ctx, step, torch.tensor([2, 0]), prep=(s2, o2, r2, bt, emb, 32))
+    ops.decode_prep(slots, offs, res, ids, pos, bt, emb, 32)
+    assert torch.equal(s2, slots) and torch.equal(o2, offs) and torch.equal(r2, res)
+    assert s2.tolist() == [7 * 32 + 3, 4 * 32 + 2] and torch.equal(r2, emb[[2, 0]])
+    # a position past the block table (after a turn's last step) maps into block 0, no fault
+    ops.decode_prep(slots, offs, res, ids, torch.tensor([96, 97]), bt, emb, 32)
+    assert slots.tolist() == [0, 1]
 
 
 def _guard_case():

@@ -3,8 +3,11 @@
 The captured region is the whole step: embedding, all layers (K1/K2/K3/K5 + GEMMs
 + TP all-reduces), lm_head, K6 sampling, then device-side bookkeeping so the next
 replay needs no host input: the sampled ids become the next inputs, positions /
-context lengths / the step counter advance, and the next slot mapping is derived
-from the (pre-allocated) block tables. Static buffers are refreshed once per turn.
+context lengths / the step counter advance, and the next slot mapping, sampler
+offsets and embedding rows are derived from the (pre-allocated) block tables in the
+same launch (fused path: csrc/decode_step.hip decode_advance with prep operands; the
+turn's first step is prepped once, eagerly, before the first replay). Static buffers
+are refreshed once per turn.
 
 Graphs are cached per (batch bucket, split-KV count); padded batch rows decode a
 dummy sequence living in a reserved scratch block and are discarded.
@@ -62,13 +65,21 @@ class DecodeGraph:
         self.graph = None
         self._capture()
 
+    def _fused(self) -> bool:
+        m = self.engine.model
+        return getattr(m, "accepts_hidden", False) and m.fused_decode_ok(self.input_ids)
+
+    def _prep(self):
+        """Eager prologue of a turn's first step: K/V slots, sampler offsets, embedding rows.
+        Later steps get theirs from the previous step's decode_advance."""
+        if self._fused():
+            ops.decode_prep(self.slots, self.offsets, self.hidden, self.input_ids, self.positions,
+                            self.block_tables, self.engine.model.w["embed"], self.bs)
+
     def _body(self):
         e = self.engine
-        fused = getattr(e.model, "accepts_hidden", False) and e.model.fused_decode_ok(self.input_ids)
+        fused = self._fused()
         if fused:
-            # one prologue launch: K/V slots, sampler offsets, embedding rows (csrc/decode_step.hip)
-            ops.decode_prep(self.slots, self.offsets, self.hidden, self.input_ids, self.positions,
-                            self.block_tables, e.model.w["embed"], self.bs)
             slots, offsets, hidden = self.slots, self.offsets, self.hidden
         else:
             bs = self.bs
@@ -88,8 +99,13 @@ class DecodeGraph:
             nxt = e.tp.greedy_gather(logits, e.cfg.vocab)
         else:
             nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets)
-        # one epilogue launch: record ids, advance positions / lengths / step
-        ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt)
+        # one epilogue launch: record ids, advance positions / lengths / step (+ next step's prep)
+        if fused:
+            ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt,
+                               prep=(self.slots, self.offsets, self.hidden, self.block_tables,
+                                     e.model.w["embed"], self.bs))
+        else:
+            ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt)
 
     def check_guard(self) -> None:
         code = int(self.guard_err.item())
@@ -116,10 +132,13 @@ class DecodeGraph:
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s), torch.no_grad():
+            self._prep()    # slots point into the scratch block, never a live sequence's
             for _ in range(2):  # warm up kernels / allocator / hipBLASLt heuristics outside capture
                 self._body()
         torch.cuda.current_stream(dev).wait_stream(s)
         self._reset_dummy()
+        with torch.no_grad():
+            self._prep()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g), torch.no_grad():
             self._body()
@@ -151,6 +170,8 @@ class DecodeGraph:
         self.top_p.copy_(torch.tensor([t.params.top_p for t in turns] + [1.0] * pad, dtype=torch.float32))
         self.top_k.copy_(torch.tensor([t.params.top_k for t in turns] + [0] * pad, dtype=torch.int32))
         self.seeds.copy_(torch.tensor([t.params.seq_seed(t.seq_key) for t in turns] + [0] * pad, dtype=torch.int64))
+        with torch.no_grad():
+            self._prep()
         need_tokens = any((not t.params.ignore_eos) or t.params.stop_on_consensus for t in turns)
         sync_every = engine.ecfg.sync_every
         first_host = first[:B].tolist()

@@ -339,12 +339,19 @@ def paging_guard_message(code: int) -> str:
 
 
 def decode_advance(out: torch.Tensor, ids: torch.Tensor, positions: torch.Tensor, ctx_lens: torch.Tensor,
-                   step: torch.Tensor, nxt: torch.Tensor) -> None:
-    """Captured-step epilogue: record the sampled ids and advance positions / lengths / step."""
+                   step: torch.Tensor, nxt: torch.Tensor, prep=None) -> None:
+    """Captured-step epilogue: record the sampled ids and advance positions / lengths / step.
+
+    prep = (slots, offsets, res, block_tables, embed, block_size) also runs the NEXT step's
+    decode_prep from the advanced ids / positions in the same launch."""
     if _use_native(ids):
-        native().decode_advance(out, ids, positions, ctx_lens, step, nxt)
+        if prep is None:
+            native().decode_advance(out, ids, positions, ctx_lens, step, nxt)
+        else:
+            slots, offsets, res, bt, embed, bs = prep
+            native().decode_advance(out, ids, positions, ctx_lens, step, nxt, slots, offsets, res, bt, embed, int(bs))
         return
-    ref.decode_advance(out, ids, positions, ctx_lens, step, nxt)
+    ref.decode_advance(out, ids, positions, ctx_lens, step, nxt, prep)
 
 
 def decode_layer(res: torch.Tensor, lw: dict, positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,

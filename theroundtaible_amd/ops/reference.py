@@ -270,17 +270,22 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
 
 
 def decode_prep(slots, offsets, res, ids, positions, block_tables, embed, block_size):
-    """Semantics of csrc/decode_step.hip::decode_prep (in place)."""
+    """Semantics of csrc/decode_step.hip::decode_prep (in place). A position past the block
+    table (only after a turn's last step; that slot is never written) maps into block 0."""
     pos = positions.long()
-    blk = block_tables.long().gather(1, (pos // block_size).unsqueeze(1)).squeeze(1)
+    bi = pos // block_size
+    inside = bi < block_tables.shape[1]
+    blk = block_tables.long().gather(1, torch.where(inside, bi, 0).unsqueeze(1)).squeeze(1)
+    blk = torch.where(inside, blk, 0)
     slots[:len(pos)] = blk * block_size + pos % block_size
     offsets[:len(pos)] = pos + 1
     tok = ids.long().clamp(0, embed.shape[0] - 1)
     res.copy_(embed[tok].to(res.dtype))
 
 
-def decode_advance(out, ids, positions, ctx_lens, step, nxt):
-    """Semantics of csrc/decode_step.hip::decode_advance (in place)."""
+def decode_advance(out, ids, positions, ctx_lens, step, nxt, prep=None):
+    """Semantics of csrc/decode_step.hip::decode_advance (in place); with prep operands
+    (slots, offsets, res, block_tables, embed, block_size) it then runs decode_prep."""
     st = int(step.item())
     if st < out.shape[0]:
         out[st] = nxt
@@ -288,6 +293,9 @@ def decode_advance(out, ids, positions, ctx_lens, step, nxt):
     positions.add_(1)
     ctx_lens.add_(1)
     step.add_(1)
+    if prep is not None:
+        slots, offsets, res, bt, embed, bs = prep
+        decode_prep(slots, offsets, res, ids, positions, bt, embed, bs)
 
 
 PAGING_GUARD_CODES = {1: "ctx_len outside [1, max_blocks*block_size]", 2: "block-table entry outside the KV pool",
