@@ -69,3 +69,32 @@ def test_attach_keeps_blocks_refcounted():
 def test_group_order_makes_members_adjacent():
     assert group_order(["a", None, "b", "a", "b", None]) == [0, 3, 1, 2, 4, 5]
     assert group_order([None, None]) == [0, 1]
+
+
+def test_lcp_matches_elementwise_scan():
+    import random
+    from theroundtaible_amd.engine.engine import lcp
+    rng = random.Random(5)
+    for _ in range(300):
+        n = rng.randrange(0, 10000)
+        a = [rng.randrange(3) for _ in range(n)]
+        b = a[:rng.randrange(0, n + 1)] + [rng.randrange(3) for _ in range(rng.randrange(0, 40))]
+        lim = rng.choice([None, rng.randrange(0, n + 2)])
+        m, end = 0, min(len(a), len(b)) if lim is None else min(lim, len(a), len(b))
+        while m < end and a[m] == b[m]:
+            m += 1
+        assert lcp(a, b, lim) == m and lcp(tuple(a), b, lim) == m
+
+
+def test_encode_prompt_split_head_length():
+    """The shared head's length is the sum of its segments' ids (pinned ids used as given),
+    the same as encoding the head on its own."""
+    e = _engine()
+    for t in _turns([], 1, "t0") + _turns([], 2, "t0"):
+        p = t.prompt
+        p.segments.append(Segment("vastgezet", ids=[5, 6, 7], tokenizer=e.tokenizer.family))
+        ids, n = e.encode_prompt_split(p)
+        head = Prompt(list(p.segments[:p.shared_segments]), templated=True)
+        want = len(e.encode_prompt(head)) + (len(e.tokenizer.chat_prefix or []) if not p.templated else 0)
+        assert n == min(want, len(ids) - 1) and ids == e.encode_prompt(p)
+        assert ids[-3:] == [5, 6, 7] or e.tokenizer.chat_suffix
