@@ -31,8 +31,18 @@ def _turns(transcript, rnd, key):
 def test_shared_layout_same_tokens_fewer_blocks():
     shared, private = _engine(), _engine()
     tr_s, tr_p = [], []
+    fwd = shared.model.forward
+    calls = []
+
+    def counted(*a, **k):
+        calls.append(a[3].kind)
+        return fwd(*a, **k)
+    shared.model.forward = counted
     for rnd in (1, 2, 3):
+        calls.clear()
         a = shared.run_turns(_turns(tr_s, rnd, "t0"))
+        # the shared span and the knights' own deltas are prefilled in ONE forward
+        assert calls.count("prefill") == 1, calls
         b = private.run_turns(_turns(tr_p, rnd, None))
         for x, y in zip(a, b):
             assert x.error is None and y.error is None

@@ -321,8 +321,25 @@ class Engine:
     @torch.no_grad()
     def prefill(self, items: Sequence[Tuple[SeqState, List[int]]]) -> torch.Tensor:
         """Append ``ids`` to each sequence's KV (chunked, varlen-batched). Returns last-token logits [S, V]."""
+        return self.prefill_reserved([self.reserve(s, ids) for s, ids in items])
+
+    def reserve(self, s: SeqState, ids: Sequence[int]) -> Tuple[SeqState, int, List[int]]:
+        """Append ``ids`` to ``s`` (tokens + KV blocks) ahead of their prefill: a shared
+        prefix reserved this way can be attached to its members and prefilled in the SAME
+        forward as their own deltas (items run in order; within a layer every K/V write
+        precedes the attention that reads it)."""
+        st = s.length
+        ids = list(ids)
+        self.kv.ensure_capacity(s, st + len(ids))
+        s.tokens.extend(ids)
+        return s, st, ids
+
+    def prefill_reserved(self, items: Sequence[Tuple[SeqState, int, List[int]]]) -> torch.Tensor:
+        """Compute the K/V of reserved spans (``reserve``) in order, chunked and varlen-batched;
+        returns each span's last-token logits [S, V]."""
         dev = self.device
-        pending = [(s, list(ids)) for s, ids in items]
+        pending = [(s, ids) for s, _, ids in items]
+        base = [st for _, st, _ in items]
         last_logits: List[Optional[torch.Tensor]] = [None] * len(pending)
         offs = [0] * len(pending)
         budget = self.ecfg.prefill_chunk
@@ -346,13 +363,11 @@ class Engine:
             tok, pos, slots, cu, starts, last = [], [], [], [0], [], []
             for i, take in batch:
                 s, ids = pending[i]
-                st = s.length
+                st = base[i] + offs[i]
                 chunk = ids[offs[i]:offs[i] + take]
-                self.kv.ensure_capacity(s, st + take)
                 tok += chunk
                 pos += list(range(st, st + take))
                 slots += self.kv.slots(s, st, st + take)
-                s.tokens.extend(chunk)
                 starts.append(st)
                 cu.append(cu[-1] + take)
                 last.append(cu[-1] - 1)
@@ -483,9 +498,11 @@ class Engine:
         return res  # type: ignore[return-value]
 
     def _sync_groups(self, turns: Sequence[Turn], enc: Sequence[Tuple[List[int], int]]):
-        """Prefill every shared-prefix group's common tokens ONCE into the group's shared
-        sequence and attach its full blocks to each member (``prompt_layout: shared``).
-        Returns (per-turn group key or None, {key: shared seq}, {key: shared prefill tokens})."""
+        """Reserve every shared-prefix group's new common tokens ONCE in the group's shared
+        sequence and attach its full blocks to each member (``prompt_layout: shared``); the
+        caller prefills the reserved spans first in the members' forward.
+        Returns (per-turn group key or None, {key: shared seq}, {key: shared prefill tokens},
+        reserved shared spans)."""
         keys = [getattr(t.prompt, "shared_key", None) if n > 0 else None for t, (_, n) in zip(turns, enc)]
         shared: Dict[str, SeqState] = {}
         pre: Dict[str, int] = {}
@@ -499,16 +516,19 @@ class Engine:
             shared[key] = sq
             pre[key] = len(delta)
             if delta:
-                items.append((sq, delta))
-        if items:
-            with trace.range("shared prefill"):
-                self.prefill(items)       # KV only; the shared sequence is never sampled
+                items.append(self.reserve(sq, delta))   # KV only; never sampled
         bs = self.kv.block_size
         for t, key in zip(turns, keys):
             if key is not None:
                 sq = shared[key]
                 self.attach_shared(self.kv.seq(t.seq_key), sq, sq.length // bs)
-        return keys, shared, pre
+        return keys, shared, pre, items
+
+    def _prefill_turns(self, shared_items, seqs: Sequence[SeqState], deltas: Sequence[List[int]]) -> torch.Tensor:
+        """One prefill over the reserved shared spans, then every turn's own delta; returns the
+        turns' last-token logits."""
+        logits = self.prefill_reserved(list(shared_items) + [self.reserve(s, d) for s, d in zip(seqs, deltas)])
+        return logits[len(shared_items):]
 
     def _run_turns_ordered(self, turns: Sequence[Turn]) -> List[TurnOutput]:
         t_start = time.perf_counter()
@@ -516,14 +536,14 @@ class Engine:
         targets = [ids for ids, _ in enc]
         self._sync()
         t0 = time.perf_counter()
-        keys, shared, shared_pre = self._sync_groups(turns, enc)
+        keys, shared, shared_pre, shared_items = self._sync_groups(turns, enc)
         seqs, reused = [], []
         for t, ids in zip(turns, targets):
             s, n = self.sync_prefix(t.seq_key, ids)
             seqs.append(s)
             reused.append(n)
         deltas = [ids[n:] for ids, n in zip(targets, reused)]
-        logits = self.prefill(list(zip(seqs, deltas)))
+        logits = self._prefill_turns(shared_items, seqs, deltas)
         first = self._sample_host(logits, seqs, turns)
         # blocks every member of a group still shares (a member rolled back into the shared
         # region has copied-on-write its tail): the grouped decode reads those once per group
@@ -627,14 +647,14 @@ class Engine:
         enc = [self.encode_prompt_split(t.prompt) for t in turns]
         targets = [ids for ids, _ in enc]
         t0 = time.perf_counter()
-        keys, _shared, shared_pre = self._sync_groups(turns, enc)   # shared prefixes (system prompts)
+        keys, _shared, shared_pre, shared_items = self._sync_groups(turns, enc)   # shared prefixes
         seqs, reused = [], []
         for t, ids in zip(turns, targets):
             sq, n = self.sync_prefix(t.seq_key, ids)
             seqs.append(sq)
             reused.append(n)
         deltas = [ids[n:] for ids, n in zip(targets, reused)]
-        logits = self.prefill(list(zip(seqs, deltas)))
+        logits = self._prefill_turns(shared_items, seqs, deltas)
         first = self._sample_host(logits, seqs, turns).tolist()
         ms = (time.perf_counter() - t0) * 1e3
         self.stats["prefill_tokens"] += sum(len(d) for d in deltas) + sum(shared_pre.values())
