@@ -38,6 +38,27 @@ def test_graph_decode_equals_eager():
     assert ops.native_available()
 
 
+def test_graph_decode_pipelined_stop(monkeypatch):
+    """graphs.DecodeGraph.run checks stops one chunk behind the replays (pinned async copies):
+    a stop condition met at 40 tokens ends the turn at the first checked chunk past it (49
+    tokens with sync_every 32), with the same tokens as an uninterrupted decode."""
+    import theroundtaible_amd.engine.engine as em
+    monkeypatch.setattr(em, "_finished", lambda out, params, eos, tok: len(out) >= 40)
+    sp = SamplingParams(temperature=0.0, max_new_tokens=200, ignore_eos=False, stop_on_consensus=False)
+    a = eng(use_graphs=True)
+    p = "Hallo tafel, wat is het plan voor vandaag?"
+    ta = a.run_turns([Turn("K1", p, sp), Turn("K2", p + " Anders.", sp)])
+    monkeypatch.setattr(em, "_finished", lambda out, params, eos, tok: False)
+    tb = eng(use_graphs=True).run_turns([Turn("K1", p, sp), Turn("K2", p + " Anders.", sp)])
+    for x, y in zip(ta, tb):
+        assert x.error is None and len(x.ids) <= 49
+        assert x.ids == y.ids[:len(x.ids)]
+    assert max(len(x.ids) for x in ta) == 49 or any(len(y.ids) < 49 for y in tb)
+    # the engine keeps serving after the discarded extra replays
+    tc = a.run_turns([Turn("K1", p, GREEDY)])
+    assert tc[0].error is None
+
+
 def test_resident_kv_reuse_matches_fresh():
     a = eng()
     p = "Onderwerp: caching."

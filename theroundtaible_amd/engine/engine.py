@@ -9,8 +9,9 @@ A knight turn on the engine:
 3. pre-allocate KV blocks for ``max_new_tokens`` and run the decode loop fully
    device-side: one hipGraph replay per token for the whole batch (embed -> 32 layers
    with K1/K2/K3/K5 -> lm_head -> K6 sampling -> next-input/slot/position update);
-   the host only replays and, every ``sync_every`` steps, reads back tokens for
-   EOS / consensus-JSON / wall-clock checks;
+   the host only replays and, every ``sync_every / 2`` steps, copies the tokens back
+   asynchronously and checks the previous copy (EOS / consensus JSON / wall clock)
+   while the GPU keeps replaying;
 4. detokenize; the generated ids are returned too (C1 token-id path), and the KV of
    the response stays resident for the knight's next turn.
 

@@ -63,6 +63,7 @@ class DecodeGraph:
             self._reset_groups()
         self.guard_err = torch.zeros(1, dtype=torch.int32, device=dev)   # debug paging guard (captured)
         self.graph = None
+        self._host_out: List[torch.Tensor] = []
         self._capture()
 
     def _fused(self) -> bool:
@@ -106,6 +107,12 @@ class DecodeGraph:
                                      e.model.w["embed"], self.bs))
         else:
             ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt)
+
+    def _host_buffer(self, k: int) -> torch.Tensor:
+        """Pinned [MAX_STEPS, B] int64 copy targets of the sampled ids (two, alternating)."""
+        while len(self._host_out) < 2:
+            self._host_out.append(torch.empty(MAX_STEPS, self.B, dtype=torch.int64, pin_memory=True))
+        return self._host_out[k]
 
     def check_guard(self) -> None:
         code = int(self.guard_err.item())
@@ -173,23 +180,38 @@ class DecodeGraph:
         with torch.no_grad():
             self._prep()
         need_tokens = any((not t.params.ignore_eos) or t.params.stop_on_consensus for t in turns)
-        sync_every = engine.ecfg.sync_every
+        # stop checks are pipelined: at every `chunk`-th replay the sampled ids so far are copied
+        # to pinned host memory behind an event, and the host inspects the PREVIOUS copy while
+        # the GPU keeps replaying — the queue never drains for a check (a synchronous read
+        # idled the GPU for the tokenizer decode of every reply, ~1 ms per check). A stop is
+        # seen at most 2 chunks (= sync_every) late, as before; extra replays past it are
+        # discarded (their K/V lies beyond the kept tokens and is truncated).
+        chunk = max(1, engine.ecfg.sync_every // 2) if need_tokens else engine.ecfg.sync_every
         first_host = first[:B].tolist()
         done_at = steps
+        pending = None
         for i in range(1, steps):
             self.graph.replay()
-            if i % sync_every == 0:
+            if i % chunk == 0:
                 if engine.debug_checks:
                     self.check_guard()
                 if time.perf_counter() > deadline:
                     engine._sync()
                     raise EngineTimeout("engine", "turn exceeded timeout_per_turn_seconds")
                 if need_tokens:
-                    got = self.out[:i, :B].t().tolist()
-                    outs = [[f] + g for f, g in zip(first_host, got)]
-                    if all(_finished(o, t.params, eos, engine.tokenizer) for o, t in zip(outs, turns)):
-                        done_at = i + 1
-                        break
+                    host = self._host_buffer((i // chunk) % 2)
+                    host[:i].copy_(self.out[:i], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    prev, pending = pending, (i, host, ev)
+                    if prev is not None:
+                        j, hbuf, pev = prev
+                        pev.synchronize()
+                        got = hbuf[:j, :B].t().tolist()
+                        outs = [[f] + g for f, g in zip(first_host, got)]
+                        if all(_finished(o, t.params, eos, engine.tokenizer) for o, t in zip(outs, turns)):
+                            done_at = j + 1
+                            break
         if engine.debug_checks:
             self.check_guard()
         n = done_at - 1
