@@ -35,7 +35,7 @@ int split_workspace_ints(int max_split_tiles);
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
-                            hipStream_t stream);
+                            hipStream_t stream, int* split_ws, int64_t split_ws_ints);
 int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
                        const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
                        int64_t vocab, hipStream_t stream);
@@ -314,7 +314,7 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
 void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, int64_t pro, torch::Tensor positions,
                       torch::Tensor cos_sin, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots,
                       int64_t Hq, int64_t Hkv, int64_t D, double eps, c10::optional<torch::Tensor> x2,
-                      c10::optional<torch::Tensor> xout) {
+                      c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws) {
   check_bf16(q_out, "q_out");
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
@@ -330,11 +330,19 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
   check_caches(k_cache, v_cache, Hkv, D);
   const auto addo = add_operands(x, pro, x2, xout);
+  int* sw = nullptr;
+  int64_t sw_n = 0;
+  if (split_ws.has_value()) {   // CU-balanced launch workspace (counters zero between calls)
+    TORCH_CHECK(split_ws->scalar_type() == torch::kInt32 && split_ws->is_contiguous() &&
+                    split_ws->device() == x.device(), "split_ws: contiguous int32 on x's device");
+    sw = split_ws->data_ptr<int>();
+    sw_n = split_ws->numel();
+  }
   const int rc = launch_skinny_gemm_rope(q_out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)M, (int)K, (int)pro,
                                          (float)eps, positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                          k_cache.data_ptr(), v_cache.data_ptr(), slots.data_ptr<int64_t>(), (int)Hq,
                                          (int)Hkv, (int)D, (int)k_cache.size(2), addo.first, addo.second,
-                                         cur_stream());
+                                         cur_stream(), sw, sw_n);
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
@@ -601,7 +609,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write",
         py::arg("q_out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("positions"), py::arg("cos_sin"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
-        py::arg("eps"), py::arg("x2") = py::none(), py::arg("xout") = py::none());
+        py::arg("eps"), py::arg("x2") = py::none(), py::arg("xout") = py::none(),
+        py::arg("split_ws") = py::none());
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);

@@ -165,18 +165,32 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
                        int* split_ws, int64_t split_ws_ints) {
   if (pro == PRO_NORM_ADD && x2 == nullptr) return -5;
   if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
+  RopeEpi re{};
+  if (epi == EPI_ROPE) {
+    if (rope == nullptr) return -3;
+    re = *static_cast<const RopeEpi*>(rope);
+    if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
+  }
   // CU-balanced variant: whole plain/norm tiles + split remainder (not for NORM_ADD, whose
-  // workgroup 0 publishes the whole K row, nor ROPE, whose pairs are read across the tile)
-  if (split_ws != nullptr && pro != PRO_NORM_ADD && epi != EPI_ROPE && (K / 32) % 2 == 0 && K >= 64) {
+  // workgroup 0 publishes the whole K row). ROPE finishes its pairs after the hand-off (partner =
+  // adjacent lane's combined sum); the decode path does not use it for qkv: Llama-3-8B qkv
+  // (384 tiles) measured 11.02 us plain vs 12.28 us balanced (profiles/experiments/README_r02.md)
+  if (split_ws != nullptr && pro != PRO_NORM_ADD && (K / 32) % 2 == 0 && K >= 64) {
     const int cus = device_cus();
     const int T = N / 16;
     const int R = cus > 0 ? T % cus : 0;
     if (cus > 0 && T > cus && R > 0 && R <= SPLIT_CTRS && split_ws_ints >= split_workspace_ints(R)) {
       GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
-                    eps, {}, nullptr, nullptr};
+                    eps, re, nullptr, nullptr};
       args.kmajor = forced_order();
       const dim3 grid(T + R);
-      if (pro == PRO_NORM && epi == EPI_SWIGLU)
+      if (pro == PRO_NORM && epi == EPI_ROPE)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_ROPE, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else if (pro == PRO_PLAIN && epi == EPI_ROPE)
+        hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_ROPE, 4, 2>), grid, dim3(256), 0, stream, args,
+                           split_ws, R);
+      else if (pro == PRO_NORM && epi == EPI_SWIGLU)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_SWIGLU, 4, 2>), grid, dim3(256), 0, stream, args,
                            split_ws, R);
       else if (pro == PRO_PLAIN && epi == EPI_SWIGLU)
@@ -195,12 +209,6 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
         return -2;
       return 0;
     }
-  }
-  RopeEpi re{};
-  if (epi == EPI_ROPE) {
-    if (rope == nullptr) return -3;
-    re = *static_cast<const RopeEpi*>(rope);
-    if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
   }
   // Variant = (waves per workgroup NW, k-steps per stage U). Since the pipeline's waits are
   // counted (skinny_core.h gemm_tile), 4 waves win on every decode shape: U = 2 for the wide
@@ -265,8 +273,8 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
-                            hipStream_t stream) {
+                            hipStream_t stream, int* split_ws, int64_t split_ws_ints) {
   const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS};
   return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, x2, xo,
-                            stream, nullptr, 0);
+                            stream, split_ws, split_ws_ints);
 }

@@ -368,6 +368,10 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
       ss += __hip_atomic_load(other + 512 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  // ROPE: the rotate-half partner (column n ^ 1, same row) is the adjacent lane's finished sum,
+  // whole or split alike (thread = 16 m + n); every lane takes part in the shuffle
+  float vpartner = 0.f;
+  if constexpr (EPI == EPI_ROPE) vpartner = __shfl_xor(v, 1, 64);
   if (live) {
     float inv = 1.f;
     if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss / (float)K + p.eps);
@@ -387,10 +391,7 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
       const int64_t blk = slot / re.BS;
       const int off = (int)(slot - blk * re.BS);
       if (h < re.Hq + re.Hkv) {
-        float partner = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) partner += sm.red[w][0][m][n ^ 1];
-        partner *= inv;
+        const float partner = vpartner * inv;
         const int i = pp >> 1, hi = pp & 1;
         const float c = e_c, sn = e_s;
         // pair (x1 = d i, x2 = d i+D/2): y1 = x1 c - x2 s ; y2 = x2 c + x1 s

@@ -152,6 +152,47 @@ def test_skinny_gemm_rope_epilogue(M, hq, hkv, d):
     close(q_r, q2, 0.05, 0.02)
 
 
+@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("hq,hkv,K", [(32, 8, 4096), (40, 8, 1024)])
+def test_skinny_gemm_rope_balanced_split(M, hq, hkv, K):
+    """CU-balanced qkv launch (remainder tiles as two K-halves; the rotate-half partner is read
+    after the hand-off): q / K / V cache equal the fp32 reference, three calls agree bit for bit,
+    counters re-arm, and the plain launch agrees up to summation order."""
+    d = 128
+    N = (hq + 2 * hkv) * d
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert (N // 16) > cus and (N // 16) % cus != 0
+    x = bf(M, K, seed=81)
+    W = bf(N, K, scale=0.05, seed=82)
+    gam = bf(K, seed=83)
+    cos_sin = ref.rope_cos_sin(4096, d, 500000.0, DEV)
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int64)
+    nb = 8
+    slots = torch.randperm(nb * 32, device=DEV)[:M].to(torch.int64)
+    Ws = ops.shuffle_weight(W, gam, rope_heads=hq + hkv, head_dim=d)
+    ws = ops.split_workspace(DEV)
+    runs = []
+    for i in range(4):
+        kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+        q = ops.skinny_gemm_rope(x, Ws, ops.PRO_NORM, positions, cos_sin, kc, vc, slots, hq, hkv, d, 1e-5,
+                                 split_ws=ws if i < 3 else None)
+        runs.append((q, kc, vc))
+    assert int(ws[:256].abs().sum()) == 0, "split counters must re-arm to zero"
+    kc_r = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16)
+    vc_r = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16)
+    Wp = ref.fold_gamma(W.cpu(), gam.cpu(), hq + hkv, d)
+    q_r = ref.skinny_gemm_rope(x.cpu(), Wp, 1, positions.cpu(), cos_sin.cpu(), kc_r, vc_r, slots.cpu(), hq, hkv, d,
+                               1e-5)
+    for q, kc, vc in runs[:3]:
+        close(q, q_r.to(DEV), 0.05, 0.02)
+        close(kc, kc_r.to(DEV), 0.05, 0.02)
+        close(vc, vc_r.to(DEV), 0.05, 0.02)
+        assert torch.equal(q, runs[0][0]) and torch.equal(kc, runs[0][1]) and torch.equal(vc, runs[0][2])
+    for a, b in zip(runs[0], runs[3]):
+        close(a, b, 0.02, 0.02)
+
+
 def test_norm_add_prologue():
     """TP decode prologue: normalize bf16(x + x2), workgroup 0 publishes the sum."""
     M, N, K = 3, 512, 4096

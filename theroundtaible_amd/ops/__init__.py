@@ -300,14 +300,15 @@ def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: in
 def skinny_gemm_rope(x: torch.Tensor, Ws: torch.Tensor, pro: int, positions: torch.Tensor, cos_sin: torch.Tensor,
                      k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor, n_heads: int,
                      n_kv_heads: int, head_dim: int, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
-                     xout: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Decode qkv projection (+ optional RMSNorm prologue) with RoPE and the paged K/V cache
     write fused into the epilogue; returns q [M, n_heads, head_dim]. ``Ws`` must come from
-    ``shuffle_weight(Wqkv, gamma, rope_heads=n_heads + n_kv_heads, head_dim=head_dim)``."""
+    ``shuffle_weight(Wqkv, gamma, rope_heads=n_heads + n_kv_heads, head_dim=head_dim)``.
+    ``split_ws``: CU-balanced launch as in :func:`skinny_gemm` (not with ``PRO_NORM_ADD``)."""
     if _use_native(x):
         q = torch.empty(x.shape[0], n_heads, head_dim, dtype=x.dtype, device=x.device)
         native().skinny_gemm_rope(q, x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
-                                  head_dim, eps, x2, xout)
+                                  head_dim, eps, x2, xout, split_ws)
         return q
     return ref.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
                                 head_dim, eps, x2, xout)

@@ -75,6 +75,7 @@ def bench_gemm(M):
     slots = torch.arange(M, device=DEV, dtype=torch.int64) + 40
     shapes = [
         ("qkv  (norm+rope+cache)", (hq + 2 * hkv) * d, hid),
+        ("qkv balanced (norm+rope+cache, split remainder)", (hq + 2 * hkv) * d, hid),
         ("o    (+resid)", hid, hq * d),
         ("gate_up (norm+swiglu)", 2 * ffn, hid),
         ("gate_up balanced (norm+swiglu, split remainder)", 2 * ffn, hid),
@@ -87,7 +88,11 @@ def bench_gemm(M):
         copies = max(2, math.ceil(2**30 / nbytes))
         Ws = [ops.shuffle_weight(bf(N, K, scale=0.02), swiglu=name.startswith("gate_up")) for _ in range(copies)]
         # (the launcher reads RT_SKINNY_CFG once: compare variants from separate processes)
-        if name.startswith("qkv"):
+        if name.startswith("qkv balanced"):
+            sws = ops.split_workspace(DEV)
+            fn = lambda i, sws=sws: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM, pos, cs, kc, vc, slots, hq,
+                                                         hkv, d, split_ws=sws)
+        elif name.startswith("qkv"):
             fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d)
         elif name.startswith("o ") or name.startswith("down"):
             inp = x if name.startswith("o ") else g_in
