@@ -93,7 +93,16 @@ class TPInfo:
         return g[best, torch.arange(B, device=local.device), 1].long()
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
-        """Concatenate shards along the last dim (vocab-parallel logits)."""
+        """Concatenate shards along the last dim (vocab-parallel logits).
+
+        Sampled (temperature / top-p) TP decode keeps this gather on purpose: an exact
+        distributed nucleus needs the global max, then a mass histogram, then (refinement) a
+        second histogram and finally a (value, id) gather — four dependent collectives of a few
+        µs latency each on xGMI — while this is ONE all-gather of ``B * V * 4`` bytes (1.5 MB at
+        B = 3, Llama-3 vocab: ~10 µs spread over the tp-1 peer links). A Gumbel-argmax "accept"
+        shortcut (csrc/sampling.hip) needs a fallback for rejected rows, which a captured graph
+        cannot branch into, so it would not remove the gather either. Greedy decode, where one
+        (value, id) pair per rank is exact, uses :meth:`greedy_gather`."""
         if self.size == 1:
             return x
         src = x.contiguous().cpu() if self._host_staged(x) else x.contiguous()
