@@ -4,12 +4,20 @@
 Workload (one "step" = one complete discussion round):
   * knights are Llama-3-8B (bf16, random-init weights: there are no checkpoints), 3 per
     table, a table = one 3-knight ``discuss`` (BASELINE config 2 / metric "3-knight discuss");
-  * N GPUs host N tables (3N knights), 3 knights per GPU batched in one decode hipGraph.
-    ``--placement packed`` (default): table t lives on GPU t, so its knights share one copy
-    of the discussion's KV (``shared`` layout); every rank still runs every table's
-    orchestrator (SPMD) and each round's responses are all-gathered over RCCL (C1).
-    ``striped``: knight j of table t on rank (3t + j) mod N, every response crossing xGMI.
-    Per-GPU work is fixed as N grows: ``scaling: weak``;
+  * ``--scaling strong`` (default): ONE table whatever N is — its 3 knights batched in one
+    decode hipGraph on ONE engine that is tensor-parallel over all N GPUs (Megatron split,
+    split-K shard GEMMs, K9 one-shot all-reduce over xGMI, vocab-parallel lm_head). Total work
+    is fixed, so ``ms_per_round`` at N = 1/2/4/8 is the BASELINE wall-clock curve of the same
+    discussion (the reference's per-round cost is its sequential knight loop,
+    /root/reference/src/orchestrator.ts:347-536);
+  * ``--scaling weak``: N GPUs host N tables (3N knights), 3 knights per GPU group.
+    ``--placement packed``: table t lives on GPU t, so its knights share one copy of the
+    discussion's KV (``shared`` layout); every rank still runs every table's orchestrator
+    (SPMD) and each round's responses are all-gathered over RCCL (C1). ``striped``: knight j
+    of table t on rank (3t + j) mod N, every response crossing xGMI;
+  * ``--simulate-tp N`` (cost model only, never a measurement of N GPUs): one process computes
+    rank 0's shard of a tp=N engine with every collective replaced by a local no-op
+    (parallel/tp.py SimulatedTP); tools/tp_cost.py adds the measured collective latencies;
   * ``parallel`` round mode, ``shared`` prompt layout (``--layout append`` is the
     round-1 layout), the real orchestrator (prompt assembly, consensus parse,
     discussion.md/metrics writes) inside the timed region;
@@ -48,7 +56,15 @@ def parse():
     p.add_argument("--model", default="llama3-8b")
     p.add_argument("--knights-per-gpu", type=int, default=3,
                    help="knights hosted per GPU (per TP group when --tp > 1)")
-    p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree of every knight (BASELINE config 5: 4)")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="strong (default): one 3-knight table, one engine tensor-parallel over all N GPUs; "
+                        "weak: N tables, one GPU group each")
+    p.add_argument("--tp", type=int, default=0,
+                   help="tensor-parallel degree of every knight (0 = N under --scaling strong, 1 under weak; "
+                        "BASELINE config 5: 4)")
+    p.add_argument("--simulate-tp", type=int, default=0,
+                   help="COST MODEL ONLY: one process runs rank 0's shard of a tp=N engine, collectives replaced "
+                        "by local no-ops (the output is labelled simulated)")
     p.add_argument("--knights-per-table", type=int, default=3)
     p.add_argument("--new-tokens", type=int, default=512, help="decode tokens per knight turn")
     p.add_argument("--temperature", type=float, default=0.7)
@@ -63,6 +79,9 @@ def parse():
                    help="packed (default): a table's knights share one GPU group (batched decode + shared prefix "
                         "KV); striped: knight j of table t on group (kpt*t + j) mod groups (every response "
                         "crosses xGMI, no KV sharing)")
+    p.add_argument("--weights", default="random:1234",
+                   help="random:<seed> (per-rank shards, fast) | random-full:<seed> (unsharded tensors split per rank: "
+                        "a tp=N run has exactly the tp=1 weights; tests) | a checkpoint path")
     p.add_argument("--layers", type=int, default=None,
                    help="rehearsal only: override the model's layer count (reported in config.model)")
     p.add_argument("--weight-residency", default="auto", choices=["auto", "dual", "shuffled"])
@@ -116,7 +135,13 @@ def main() -> int:
                          f"report a {N}-GPU run as {args.gpus}")
     device = args.device or cl.device
     kpt = args.knights_per_table
-    T = max(1, args.tp)
+    sim = max(0, args.simulate_tp)
+    if sim and N != 1:
+        raise SystemExit("--simulate-tp runs ONE process (it models one rank of a tp group)")
+    T = args.tp if args.tp > 0 else (N if args.scaling == "strong" else 1)
+    if args.scaling == "strong":
+        # one table on one TP group: every GPU of the group hosts all of the table's knights
+        args.knights_per_gpu = kpt
     if N % T:
         raise SystemExit(f"--tp {T} must divide the {N} launched GPUs")
     n_groups = N // T                      # GPU groups; a knight lives on one group (T ranks)
@@ -138,14 +163,17 @@ def main() -> int:
     local_names = [n for n, ranks in placement.items() if cl.rank in ranks]
 
     tp = None
-    if T > 1:
+    if sim > 1:
+        from theroundtaible_amd.parallel.tp import SimulatedTP
+        tp = SimulatedTP(sim)
+    elif T > 1:
         import torch.distributed as dist
         from theroundtaible_amd.parallel.tp import TPInfo
         pgs = [dist.new_group(r) for r in group_ranks]   # collective: same order on every rank
         g = cl.rank // T
         tp = TPInfo(size=T, rank=cl.rank % T, group=pgs[g])
     t_load = time.perf_counter()
-    engine = Engine(EngineConfig(model=args.model, weights=f"random:{1234}", device=device,
+    engine = Engine(EngineConfig(model=args.model, weights=args.weights, device=device,
                                  use_graphs=not args.no_graphs and device != "cpu",
                                  dtype="bf16" if device != "cpu" else "fp32",
                                  kv_cache_fraction=args.kv_fraction, max_kv_tokens=args.max_kv_tokens,
@@ -222,6 +250,12 @@ def main() -> int:
                 pre += int(e.metrics.get("prefill_tokens", 0))
                 reused += int(e.metrics.get("reused_tokens", 0))
                 forced += int(e.metrics.get("forced_tokens", 0))
+    import hashlib
+    h = hashlib.sha256()
+    for o in orchs:
+        for e in o.all_rounds:
+            h.update(f"{e.round}|{e.knight}|{e.response}\n".encode())
+    transcript_sha = h.hexdigest()[:16]
     failures = [f for o in orchs for f in o.failures]
     if failures:
         print(f"[rank {cl.rank}] {len(failures)} failed knight turns; first: {failures[0]}", file=sys.stderr, flush=True)
@@ -230,11 +264,26 @@ def main() -> int:
     ms_round = elapsed / n_timed * 1e3
     value = dec / elapsed if elapsed > 0 else 0.0
     ref_bound_ms = kpt * 120_000.0
+    if args.scaling == "strong" and n_tables == 1:
+        metric = f"aggregate knight tokens/sec (one {kpt}-knight discuss, {args.round_mode} rounds)"
+    else:
+        metric = f"aggregate knight tokens/sec ({kpt}-knight discuss tables, {args.round_mode} rounds)"
+    if sim:
+        metric = f"SIMULATED rank-0 compute of tp{sim} (no communication; cost model input) — " + metric
+    if sim:
+        parallelism = f"simulated tp{sim} (rank 0 shard, collectives elided)"
+    elif T == 1:
+        parallelism = (f"knight-placement x{N} (tables {args.placement} over GPUs), C1 all-gather"
+                       if N > 1 else "single GPU")
+    elif n_groups == 1:
+        parallelism = f"tp{T}"
+    else:
+        parallelism = f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL"
     out = {
-        "metric": f"aggregate knight tokens/sec ({kpt}-knight discuss tables, {args.round_mode} rounds)",
+        "metric": metric,
         "value": round(value, 2), "unit": "tokens/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_round, 2), "ms_per_round": round(ms_round, 2),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
         "reference_bound_ms_per_round": ref_bound_ms, "speedup_vs_reference_bound": round(ref_bound_ms / ms_round, 1),
         "dtype": "bf16" if device != "cpu" else "fp32", "data": "synthetic prompts, random-init weights",
         "config": {"model": args.model + (f" ({args.layers} layers, rehearsal)" if args.layers else ""),
@@ -242,11 +291,12 @@ def main() -> int:
                    "knights_per_gpu": args.knights_per_gpu, "new_tokens_per_turn": args.new_tokens,
                    "global_batch": kpt * n_tables, "seq_len": args.new_tokens,
                    "round_mode": args.round_mode, "prompt_layout": args.layout,
-                   "placement": args.placement,
-                   "parallelism": (f"knight-placement x{N} (tables {args.placement} over GPUs), C1 all-gather"
-                                   if T == 1 else f"tp{T} knights x{n_groups} groups, C1 all-gather + C2/C3 RCCL")},
+                   "placement": args.placement, "tp": sim or T,
+                   "parallelism": parallelism},
         "detail": {"world": cl.world, "backend": cl.backend, "c1_ranks": cl.world if cl.distributed else 1,
-                   "failed_turns": len(failures), "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
+                   "simulated_tp": sim or None,
+                   "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),
+                   "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
                    "kv_blocks_used_rank0": engine.kv.num_blocks - engine.kv.alloc.num_free,

@@ -30,12 +30,13 @@ int sample_workspace_floats(int B);
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
                        int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
-                       int* split_ws, int64_t split_ws_ints);
+                       int* split_ws, int64_t split_ws_ints, int split_mode);
 int split_workspace_ints(int max_split_tiles);
+int splitk_parts(int T, int ks, int cus, int64_t ws_ints);
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
-                            hipStream_t stream, int* split_ws, int64_t split_ws_ints);
+                            hipStream_t stream, int* split_ws, int64_t split_ws_ints, int split_mode);
 int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
                        const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
                        int64_t vocab, hipStream_t stream);
@@ -45,15 +46,6 @@ int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* c
                           const int64_t* next, int B, int max_steps, int64_t* slots, int64_t* offsets, void* res,
                           const int* block_tables, const void* embed, int max_blocks, int BS, int H, int64_t vocab,
                           hipStream_t stream);
-int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, const void* wo, const void* wgu,
-                        const void* wd, const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
-                        const int64_t* slots, const int* block_tables, const int* ctx_lens, float* part_o,
-                        float* part_ml, int* split_counters, int* sync, int* err, long long* stamps, int M, int H,
-                        int I, int Hq, int Hkv, int head_dim, int BS, int max_blocks, int num_splits, float eps,
-                        float scale, hipStream_t stream);
-int decode_layer_grid();
-int launch_ring_gemm(void* out, const void* x, const void* Ws, int M, int N, int K, int grid, int variant,
-                     hipStream_t stream);
 int oneshot_create(int world, int rank, int cap_elems, char* handles);
 int oneshot_open(int id, const char* all_handles);
 int oneshot_capacity(int id);
@@ -62,7 +54,6 @@ int oneshot_error(int id);
 int oneshot_clear_error(int id);
 int oneshot_set_poll_limit(int id, long long limit);
 void oneshot_destroy(int id);
-int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
 int launch_kv_block_copy(void* k, void* v, const int* src, const int* dst, int n, int L, int num_blocks,
@@ -270,7 +261,7 @@ std::pair<const void*, void*> add_operands(const torch::Tensor& x, int64_t pro, 
 
 void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t pro, int64_t epi,
                  c10::optional<torch::Tensor> res, double eps, c10::optional<torch::Tensor> x2,
-                 c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws) {
+                 c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws, int64_t split_mode) {
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
   TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm: x [M,K], Ws [N,K]");
@@ -298,7 +289,7 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
   const auto addo = add_operands(x, pro, x2, xout);
   int* sw = nullptr;
   int64_t sw_n = 0;
-  if (split_ws.has_value()) {   // CU-balanced launch workspace (counters zero between calls)
+  if (split_ws.has_value()) {   // split-K / CU-balanced launch workspace (counters zero between calls)
     TORCH_CHECK(split_ws->scalar_type() == torch::kInt32 && split_ws->is_contiguous() &&
                     split_ws->device() == x.device(), "split_ws: contiguous int32 on x's device");
     sw = split_ws->data_ptr<int>();
@@ -306,7 +297,7 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
   }
   const int rc = launch_skinny_gemm(epi == 1 ? nullptr : out.data_ptr(), x.data_ptr(), Ws.data_ptr(), rp, (int)M,
                                     (int)N, (int)K, (int)ldo, (float)eps, (int)pro, (int)epi, nullptr, addo.first,
-                                    addo.second, cur_stream(), sw, sw_n);
+                                    addo.second, cur_stream(), sw, sw_n, (int)split_mode);
   TORCH_CHECK(rc == 0, "skinny_gemm: unsupported configuration (rc=", rc, ")");
 }
 
@@ -314,7 +305,8 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
 void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, int64_t pro, torch::Tensor positions,
                       torch::Tensor cos_sin, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots,
                       int64_t Hq, int64_t Hkv, int64_t D, double eps, c10::optional<torch::Tensor> x2,
-                      c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws) {
+                      c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws,
+                      int64_t split_mode) {
   check_bf16(q_out, "q_out");
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
@@ -332,7 +324,7 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   const auto addo = add_operands(x, pro, x2, xout);
   int* sw = nullptr;
   int64_t sw_n = 0;
-  if (split_ws.has_value()) {   // CU-balanced launch workspace (counters zero between calls)
+  if (split_ws.has_value()) {   // split-K / CU-balanced launch workspace (counters zero between calls)
     TORCH_CHECK(split_ws->scalar_type() == torch::kInt32 && split_ws->is_contiguous() &&
                     split_ws->device() == x.device(), "split_ws: contiguous int32 on x's device");
     sw = split_ws->data_ptr<int>();
@@ -342,22 +334,10 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
                                          (float)eps, positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                          k_cache.data_ptr(), v_cache.data_ptr(), slots.data_ptr<int64_t>(), (int)Hq,
                                          (int)Hkv, (int)D, (int)k_cache.size(2), addo.first, addo.second,
-                                         cur_stream(), sw, sw_n);
+                                         cur_stream(), sw, sw_n, (int)split_mode);
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
-// EXPERIMENT: loader-wave + LDS-ring decode GEMM (csrc/ring_gemm.hip), microbenchmarks only.
-void ring_gemm_exp(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t grid, int64_t variant) {
-  check_bf16(out, "out");
-  check_bf16(x, "x");
-  check_bf16(Ws, "Ws");
-  TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1) && out.size(0) == x.size(0) &&
-                  out.size(1) == Ws.size(0),
-              "ring_gemm_exp: shapes");
-  const int rc = launch_ring_gemm(out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)x.size(0), (int)Ws.size(0),
-                                  (int)x.size(1), (int)grid, (int)variant, cur_stream());
-  TORCH_CHECK(rc == 0, "ring_gemm_exp: unsupported configuration (rc=", rc, ")");
-}
 
 // K9 one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot_ar.hip).
 py::tuple py_oneshot_create(int64_t world, int64_t rank, int64_t cap_elems) {
@@ -476,54 +456,6 @@ void paging_guard(torch::Tensor block_tables, torch::Tensor ctx_lens, c10::optio
   TORCH_CHECK(rc == 0, "paging_guard: rc=", rc);
 }
 
-// Persistent decode layer (csrc/decode_layer.hip): one launch = qkv -> attention -> o -> gate_up -> down.
-void decode_layer(torch::Tensor res, torch::Tensor q, torch::Tensor a, torch::Tensor g, torch::Tensor wqkv,
-                  torch::Tensor wo, torch::Tensor wgu, torch::Tensor wd, torch::Tensor positions, torch::Tensor cos_sin,
-                  torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots, torch::Tensor block_tables,
-                  torch::Tensor ctx_lens, torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor split_counters,
-                  torch::Tensor sync, torch::Tensor err, int64_t Hq, int64_t Hkv, int64_t num_splits, double eps,
-                  double scale, c10::optional<torch::Tensor> stamps) {
-  for (auto* t : {&res, &q, &a, &g, &wqkv, &wo, &wgu, &wd}) check_bf16(*t, "decode_layer operand");
-  const int64_t M = res.size(0), H = res.size(1), I = g.size(1), D = q.size(-1);
-  TORCH_CHECK(res.dim() == 2 && g.dim() == 2 && g.size(0) == M && a.numel() == M * Hq * D && q.numel() == M * Hq * D,
-              "decode_layer: activation shapes");
-  TORCH_CHECK(wqkv.size(0) == (Hq + 2 * Hkv) * D && wqkv.size(1) == H && wo.size(0) == H && wo.size(1) == Hq * D &&
-                  wgu.size(0) == 2 * I && wgu.size(1) == H && wd.size(0) == H && wd.size(1) == I,
-              "decode_layer: weight shapes");
-  check_caches(k_cache, v_cache, Hkv, D);
-  check_type(positions, torch::kInt64, "positions");
-  check_type(slots, torch::kInt64, "slots");
-  check_type(cos_sin, torch::kFloat32, "cos_sin");
-  check_type(block_tables, torch::kInt32, "block_tables");
-  check_type(ctx_lens, torch::kInt32, "ctx_lens");
-  check_type(part_o, torch::kFloat32, "part_o");
-  check_type(part_ml, torch::kFloat32, "part_ml");
-  check_type(split_counters, torch::kInt32, "split_counters");
-  check_type(sync, torch::kInt32, "sync");
-  check_type(err, torch::kInt32, "err");
-  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M && ctx_lens.numel() >= M && block_tables.size(0) >= M,
-              "decode_layer: metadata rows");
-  TORCH_CHECK(part_o.numel() >= M * Hq * num_splits * D && part_ml.numel() >= M * Hq * num_splits * 4 &&
-                  split_counters.numel() >= M * Hkv && sync.numel() >= 5 && err.numel() >= 1,
-              "decode_layer: workspace too small");
-  const int rc = launch_decode_layer(
-      res.data_ptr(), q.data_ptr(), a.data_ptr(), g.data_ptr(), wqkv.data_ptr(), wo.data_ptr(), wgu.data_ptr(),
-      wd.data_ptr(), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), k_cache.data_ptr(), v_cache.data_ptr(),
-      slots.data_ptr<int64_t>(), block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), part_o.data_ptr<float>(),
-      part_ml.data_ptr<float>(), split_counters.data_ptr<int>(), sync.data_ptr<int>(), err.data_ptr<int>(),
-      stamps.has_value() ? (long long*)stamps->data_ptr<int64_t>() : nullptr, (int)M,
-      (int)H, (int)I, (int)Hq, (int)Hkv, (int)D, (int)k_cache.size(2), (int)block_tables.size(1), (int)num_splits,
-      (float)eps, (float)scale, cur_stream());
-  TORCH_CHECK(rc == 0, "decode_layer: unsupported configuration (rc=", rc, ")");
-}
-
-// Pull a tensor's bytes into the MALL ahead of its consumer (side-stream warm-up).
-void prefetch(torch::Tensor t, int64_t nwg, torch::Tensor sink) {
-  check_gpu(t, "t");
-  check_type(sink, torch::kInt32, "sink");
-  launch_prefetch(t.data_ptr(), t.numel() * t.element_size(), (int)nwg, (uint32_t*)sink.data_ptr(), cur_stream());
-}
-
 void shuffle_weight(torch::Tensor Ws, torch::Tensor W, c10::optional<torch::Tensor> gamma, int64_t rope_heads,
                     int64_t head_dim, bool swiglu) {
   check_bf16(Ws, "Ws");
@@ -576,21 +508,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("skinny_gemm", &skinny_gemm, "decode GEMM (M<=16), shuffled weights, fused norm / resid / swiglu",
         py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("epi"), py::arg("res") = py::none(),
         py::arg("eps") = 1e-5, py::arg("x2") = py::none(), py::arg("xout") = py::none(),
-        py::arg("split_ws") = py::none());
+        py::arg("split_ws") = py::none(), py::arg("split_mode") = 3);
   m.def("split_workspace_ints", &split_workspace_ints, "int32 words of a skinny_gemm split_ws for R split tiles");
+  m.def("splitk_parts", [](int64_t T, int64_t ks, int64_t cus, int64_t ws_ints) {
+    return splitk_parts((int)T, (int)ks, (int)cus, ws_ints);
+  }, "split-K part count the launcher picks for T tiles x ks k-steps on `cus` CUs (0 = none)");
   m.def("shuffle_weight", &shuffle_weight, py::arg("Ws"), py::arg("W"), py::arg("gamma") = py::none(),
         py::arg("rope_heads") = 0, py::arg("head_dim") = 0, py::arg("swiglu") = false);
   m.def("kv_block_copy", &kv_block_copy, py::arg("k"), py::arg("v"), py::arg("src"), py::arg("dst"));
   m.def("unshuffle_weight", &unshuffle_weight, py::arg("W"), py::arg("Ws"), py::arg("rope_heads") = 0,
         py::arg("head_dim") = 0, py::arg("swiglu") = false);
   m.def("decode_prep", &decode_prep);
-  m.def("decode_layer", &decode_layer, py::arg("res"), py::arg("q"), py::arg("a"), py::arg("g"), py::arg("wqkv"),
-        py::arg("wo"), py::arg("wgu"), py::arg("wd"), py::arg("positions"), py::arg("cos_sin"), py::arg("k_cache"),
-        py::arg("v_cache"), py::arg("slots"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("part_o"),
-        py::arg("part_ml"), py::arg("split_counters"), py::arg("sync"), py::arg("err"), py::arg("Hq"),
-        py::arg("Hkv"), py::arg("num_splits"), py::arg("eps"), py::arg("scale"), py::arg("stamps") = py::none());
-  m.def("decode_layer_grid", &decode_layer_grid);
-  m.def("ring_gemm_exp", &ring_gemm_exp, py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("grid") = 0, py::arg("variant") = 0);
   m.def("oneshot_create", &py_oneshot_create, py::arg("world"), py::arg("rank"), py::arg("cap_elems"));
   m.def("oneshot_open", &py_oneshot_open, py::arg("id"), py::arg("all_handles"), py::arg("world"));
   m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
@@ -605,12 +533,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("block_size") = 0);
   m.def("paging_guard", &paging_guard, py::arg("block_tables"), py::arg("ctx_lens"), py::arg("positions"),
         py::arg("slots"), py::arg("err"), py::arg("num_blocks"), py::arg("block_size"));
-  m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));
   m.def("skinny_gemm_rope", &skinny_gemm_rope, "qkv decode GEMM with fused RoPE + paged K/V cache write",
         py::arg("q_out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("positions"), py::arg("cos_sin"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
         py::arg("eps"), py::arg("x2") = py::none(), py::arg("xout") = py::none(),
-        py::arg("split_ws") = py::none());
+        py::arg("split_ws") = py::none(), py::arg("split_mode") = 3);
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);

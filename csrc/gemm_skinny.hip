@@ -49,11 +49,37 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_bal_kernel(GemmArgs p, in
   const int b = blockIdx.x;
   if (b < 2 * R) {
     const int r = b >> 1;
-    const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)r * 2 * SPLIT_STRIDE, ws + r, b & 1};
+    const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)r * 2 * SPLIT_STRIDE, ws + r, b & 1, 2};
     gemm_tile<PRO, EPI, NW, U, false>(p, T - R + r, sm, st0, false, false, &sx);
   } else {
     gemm_tile<PRO, EPI, NW, U, false>(p, b - 2 * R, sm, st0, false, false);
   }
+}
+
+// Split-K launch for shapes with FEWER tiles than CUs — the tensor-parallel shard GEMMs (Llama-3-8B
+// at tp 8: qkv 48 tiles, gate_up 112; tp 4: 96 / 224). One tile per workgroup would stream the
+// weights with a fraction of the chip, so every tile's K range is cut into S parts (T x S
+// workgroups, SplitX hand-off, last arriver combines in index order and runs the epilogue).
+// Placement (speed only, never correctness): with T % 8 == 0 the S parts of a tile get block ids
+// b, b + 8, ... — one XCD under round-robin dispatch, so the combine reads same-XCD partials.
+// NORM_ADD: every part of tile 0 publishes its K range of x + x2.
+template <int PRO, int EPI, int NW, int U>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_splitk_kernel(GemmArgs p, int* __restrict__ ws, int S) {
+  __shared__ GemmSmem<nacc<EPI>(), NW> sm;
+  Stage<PRO, EPI, U> st0;
+  const int T = p.N / 16;
+  const int b = blockIdx.x;
+  int tile, part;
+  if ((T & 7) == 0) {
+    const int j = b >> 3;
+    tile = (j / S) * 8 + (b & 7);
+    part = j % S;
+  } else {
+    tile = b / S;
+    part = b % S;
+  }
+  const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)tile * S * SPLIT_STRIDE, ws + tile, part, S};
+  gemm_tile<PRO, EPI, NW, U, false>(p, tile, sm, st0, false, tile == 0, &sx);
 }
 
 int device_cus() {
@@ -160,9 +186,36 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
 
 int split_workspace_ints(int max_split_tiles) { return SPLIT_CTRS + max_split_tiles * 2 * SPLIT_STRIDE; }
 
+// Split-K part count for a T-tile, ks-k-step GEMM on `cus` CUs (0 = no split-K): enough parts
+// that T x S reaches `target` workgroups (default 2 per CU), each part >= 8 k-steps, T x S capped
+// by the workspace. RT_SPLITK=<S> pins S (1 = off), RT_SPLITK_TARGET=<wgs> moves the target
+// (microbenchmark sweeps; read once per process).
+int splitk_parts(int T, int ks, int cus, int64_t ws_ints) {
+  static const int pinned = [] {
+    const char* e = getenv("RT_SPLITK");
+    return e ? atoi(e) : 0;
+  }();
+  static const int target_env = [] {
+    const char* e = getenv("RT_SPLITK_TARGET");
+    return e ? atoi(e) : 0;
+  }();
+  if (cus <= 0 || T >= cus || T > SPLIT_CTRS || pinned == 1) return 0;
+  int S;
+  if (pinned > 1) {
+    S = pinned;
+  } else {
+    const int target = target_env > 0 ? target_env : 2 * cus;
+    S = (target + T - 1) / T;
+  }
+  S = S < ks / 8 ? S : ks / 8;
+  if (S > 16) S = 16;
+  while (S >= 2 && SPLIT_CTRS + (int64_t)T * S * SPLIT_STRIDE > ws_ints) --S;
+  return S >= 2 ? S : 0;
+}
+
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
                        int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
-                       int* split_ws, int64_t split_ws_ints) {
+                       int* split_ws, int64_t split_ws_ints, int split_mode) {
   if (pro == PRO_NORM_ADD && x2 == nullptr) return -5;
   if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
   RopeEpi re{};
@@ -171,11 +224,38 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     re = *static_cast<const RopeEpi*>(rope);
     if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
   }
-  // CU-balanced variant: whole plain/norm tiles + split remainder (not for NORM_ADD, whose
-  // workgroup 0 publishes the whole K row). ROPE finishes its pairs after the hand-off (partner =
-  // adjacent lane's combined sum); the decode path does not use it for qkv: Llama-3-8B qkv
-  // (384 tiles) measured 11.02 us plain vs 12.28 us balanced (profiles/experiments/README_r02.md)
-  if (split_ws != nullptr && pro != PRO_NORM_ADD && (K / 32) % 2 == 0 && K >= 64) {
+  // split-K (split_mode bit 1) when the shape has fewer tiles than CUs: tensor-parallel shards
+  if (split_ws != nullptr && (split_mode & 2)) {
+    const int T = N / 16;
+    const int S = splitk_parts(T, K / 32, device_cus(), split_ws_ints);
+    if (S >= 2) {
+      GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
+                    eps, re, (const uint16_t*)x2, (uint16_t*)xo};
+      args.kmajor = forced_order();
+      const dim3 grid(T * S);
+#define RT_SK(P, E) \
+  hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 4, 2>), grid, dim3(256), 0, stream, args, split_ws, S)
+      if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SK(PRO_PLAIN, EPI_STORE);
+      else if (pro == PRO_NORM && epi == EPI_STORE) RT_SK(PRO_NORM, EPI_STORE);
+      else if (pro == PRO_NORM_ADD && epi == EPI_STORE) RT_SK(PRO_NORM_ADD, EPI_STORE);
+      else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_SK(PRO_PLAIN, EPI_RESID);
+      else if (pro == PRO_NORM && epi == EPI_SWIGLU) RT_SK(PRO_NORM, EPI_SWIGLU);
+      else if (pro == PRO_NORM_ADD && epi == EPI_SWIGLU) RT_SK(PRO_NORM_ADD, EPI_SWIGLU);
+      else if (pro == PRO_NORM && epi == EPI_ROPE) RT_SK(PRO_NORM, EPI_ROPE);
+      else if (pro == PRO_NORM_ADD && epi == EPI_ROPE) RT_SK(PRO_NORM_ADD, EPI_ROPE);
+      else if (pro == PRO_PLAIN && epi == EPI_ROPE) RT_SK(PRO_PLAIN, EPI_ROPE);
+      else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_SK(PRO_PLAIN, EPI_SWIGLU);
+      else return -2;
+#undef RT_SK
+      return hipGetLastError() == hipSuccess ? 0 : -6;
+    }
+  }
+  // CU-balanced variant (split_mode bit 0): whole plain/norm tiles + split remainder (not for
+  // NORM_ADD, whose workgroup 0 publishes the whole K row). ROPE finishes its pairs after the
+  // hand-off (partner = adjacent lane's combined sum); the decode path does not use it for qkv:
+  // Llama-3-8B qkv (384 tiles) measured 11.02 us plain vs 12.28 us balanced
+  // (profiles/experiments/README_r02.md)
+  if (split_ws != nullptr && (split_mode & 1) && pro != PRO_NORM_ADD && (K / 32) % 2 == 0 && K >= 64) {
     const int cus = device_cus();
     const int T = N / 16;
     const int R = cus > 0 ? T % cus : 0;
@@ -273,8 +353,8 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
-                            hipStream_t stream, int* split_ws, int64_t split_ws_ints) {
+                            hipStream_t stream, int* split_ws, int64_t split_ws_ints, int split_mode) {
   const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS};
   return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, x2, xo,
-                            stream, split_ws, split_ws_ints);
+                            stream, split_ws, split_ws_ints, split_mode);
 }

@@ -66,15 +66,18 @@ constexpr int nacc() { return EPI == EPI_SWIGLU ? 2 : 1; }
 
 RT_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
 
-// Split tile (CU-balanced launch, gemm_skinny.hip): the two K-halves of one 16-column tile run
-// as two workgroups; each leaves its row sums (v, up, sum of squares) in `part` with
-// write-through stores, the second to arrive (tile counter) adds the other half's and runs the
-// epilogue, then re-arms the counter. Per split tile: 2 halves x SPLIT_STRIDE floats.
+// Split tile: the K range of one 16-column tile runs as `n` workgroups (k-steps
+// [ks*idx/n, ks*(idx+1)/n)); each leaves its row sums (v, up, sum of squares) in `part` with
+// write-through stores, the last to arrive (tile counter) sums all n parts IN INDEX ORDER (the
+// result does not depend on arrival order), runs the epilogue and re-arms the counter.
+// Used by the CU-balanced launch (n = 2 for the remainder tiles) and by split-K (tensor-parallel
+// shard shapes with fewer tiles than CUs). Per split tile: n x SPLIT_STRIDE floats.
 constexpr int SPLIT_STRIDE = 16 * 16 * 2 + 16;   // v[16][16], up[16][16], ssq[16]
 struct SplitX {
-  float* part;    // this tile's [2][SPLIT_STRIDE]
+  float* part;    // this tile's [n][SPLIT_STRIDE]
   int* ctr;       // this tile's arrival counter (0 between launches)
-  int half;       // 0: k-steps [0, mid), 1: [mid, nsteps)
+  int idx;        // this workgroup's part
+  int n;          // parts of the tile (>= 2)
 };
 
 // 16-bit store, optionally write-through (sc1) for consumers in the same launch
@@ -265,11 +268,10 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   const int r = lane & 15, g = lane >> 4;
   const int M = p.M, N = p.N, K = p.K;
   const int ksteps = K / 32;
-  // k-step range of this workgroup: all of K, or one half of a split tile. `nsteps` below is
+  // k-step range of this workgroup: all of K, or one part of a split tile. `nsteps` below is
   // the range END (loads clamp to it), `s_lo` its start.
-  const int kmid = ksteps / 2;
-  const int s_lo = (sx != nullptr && sx->half == 1) ? kmid : 0;
-  const int nsteps = (sx != nullptr && sx->half == 0) ? kmid : ksteps;
+  const int s_lo = sx != nullptr ? (int)((long)ksteps * sx->idx / sx->n) : 0;
+  const int nsteps = sx != nullptr ? (int)((long)ksteps * (sx->idx + 1) / sx->n) : ksteps;
   const bool row_ok = r < M;
   const size_t lane_elem = (size_t)(row_ok ? r : 0) * K + 8 * g;
   const XSrc xr = make_xsrc<SC1>(p.x, lane_elem);
@@ -343,9 +345,11 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
       if constexpr (EPI == EPI_SWIGLU) up += sm.red[w][(EPI == EPI_SWIGLU) ? 1 : 0][m][n];
     }
   }
-  if (sx != nullptr) {   // split tile: hand the half's sums over, the second arrival finishes
-    float* mine = sx->part + sx->half * SPLIT_STRIDE;
-    const float* other = sx->part + (1 - sx->half) * SPLIT_STRIDE;
+  if (sx != nullptr) {   // split tile: hand this part's sums over, the last arrival finishes
+    // hand-off (MI355X_MICROARCH, sc1 table row 1): 4-B sc1 payload stores -> every wave's
+    // vmcnt(0) -> barrier -> one agent atomic add; the last adder's waves load sc1 after the
+    // barrier that publishes its LDS flag
+    float* mine = sx->part + sx->idx * SPLIT_STRIDE;
     if (live) {
       __hip_atomic_store(mine + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if constexpr (EPI == EPI_SWIGLU)
@@ -356,16 +360,24 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
     __syncthreads();
     if (threadIdx.x == 0) {
       const int prev = __hip_atomic_fetch_add(sx->ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sm.sq[0][0] = prev == 1 ? 1.f : 0.f;   // LDS flag: this workgroup arrived second
-      if (prev == 1) __hip_atomic_store(sx->ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = prev == sx->n - 1;
+      sm.sq[0][0] = last ? 1.f : 0.f;   // LDS flag: this workgroup arrived last
+      if (last) __hip_atomic_store(sx->ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (sm.sq[0][0] == 0.f) return;   // first half in: the other workgroup finishes the tile
+    if (sm.sq[0][0] == 0.f) return;   // not last: another workgroup finishes the tile
     if (live) {
-      v += __hip_atomic_load(other + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if constexpr (EPI == EPI_SWIGLU)
-        up += __hip_atomic_load(other + 256 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ss += __hip_atomic_load(other + 512 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float v_own = v, up_own = up, ss_own = ss;
+      v = up = ss = 0.f;
+      for (int i = 0; i < sx->n; ++i) {   // fixed order: bit-identical whoever arrives last
+        const float* pi = sx->part + i * SPLIT_STRIDE;
+        const bool own = i == sx->idx;
+        v += own ? v_own : __hip_atomic_load(pi + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (EPI == EPI_SWIGLU)
+          up += own ? up_own : __hip_atomic_load(pi + 256 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (PRO != PRO_PLAIN)
+          ss += own ? ss_own : __hip_atomic_load(pi + 512 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   // ROPE: the rotate-half partner (column n ^ 1, same row) is the adjacent lane's finished sum,

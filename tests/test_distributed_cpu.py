@@ -43,7 +43,8 @@ def _tp_worker(rank, world, port, model, q, overrides=None):
 
 
 @pytest.mark.parametrize("model,tp,overrides", [("tiny-llama", 2, None), ("tiny-gpt2", 2, None),
-                                                 ("tiny-llama", 4, {"n_kv_heads": 4})])
+                                                 ("tiny-llama", 4, {"n_kv_heads": 4}),
+                                                 ("tiny-llama", 4, None)])     # 2 KV heads: replicated
 def test_tp_matches_tp1(model, tp, overrides):
     """TP=2/4 forward + greedy decode equal TP=1; the TP decode samples
     greedily with the per-rank argmax + (value, id) all-gather (C3), so identical tokens show the
@@ -160,7 +161,7 @@ def _bench(nproc, extra=()):
 
 
 def test_spmd_bench_two_ranks():
-    out = _bench(2)
+    out = _bench(2, ("--scaling", "weak"))
     assert out["n_gpus"] == 2 and out["config"]["knights"] == 6 and out["config"]["tables"] == 2
     assert out["detail"]["decode_tokens"] == 6 * 8 * 2
     assert out["value"] > 0 and out["scaling"] == "weak"
@@ -171,7 +172,7 @@ def test_spmd_bench_scaling_world_sizes(nproc):
     """The driver's scaling run (N = 4, 8 ranks) on the gloo/CPU path: 3 knights per rank, one
     table per rank sharing its prefix KV (default packed placement), every table's responses
     all-gathered to every rank in the C1 exchange."""
-    out = _bench(nproc)
+    out = _bench(nproc, ("--scaling", "weak"))
     assert out["n_gpus"] == nproc and out["config"]["tables"] == nproc and out["config"]["knights"] == 3 * nproc
     assert out["detail"]["decode_tokens"] == 3 * nproc * 8 * 2 and out["detail"]["failed_turns"] == 0
     assert out["config"]["placement"] == "packed" and out["config"]["prompt_layout"] == "shared"
@@ -179,7 +180,7 @@ def test_spmd_bench_scaling_world_sizes(nproc):
 
 def test_spmd_bench_striped_append_layout():
     """Round-1 placement and layout: knights of a table on different ranks, private KV."""
-    out = _bench(4, ("--placement", "striped", "--layout", "append"))
+    out = _bench(4, ("--scaling", "weak", "--placement", "striped", "--layout", "append"))
     assert out["config"]["tables"] == 4 and out["detail"]["failed_turns"] == 0
     assert out["detail"]["decode_tokens"] == 3 * 4 * 8 * 2
 
@@ -224,9 +225,41 @@ def test_spmd_bench_tp2():
     assert out["detail"]["decode_tokens"] == 2 * 8 * 2
 
 
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_strong_scaling_bench_one_table_tp(nproc):
+    """The default ``--scaling strong``: ONE 3-knight table whose engine is tensor-parallel over
+    all N ranks (VERDICT r2 next #1) — the same discussion at every N, so ms/round is the
+    BASELINE wall-clock curve; tiny-llama's 2 KV heads are replicated at tp 4."""
+    out = _bench(nproc)
+    assert out["scaling"] == "strong" and out["n_gpus"] == nproc
+    assert out["config"]["tables"] == 1 and out["config"]["knights"] == 3
+    assert out["config"]["parallelism"] == f"tp{nproc}" and out["config"]["tp"] == nproc
+    assert out["detail"]["decode_tokens"] == 3 * 8 * 2 and out["detail"]["failed_turns"] == 0
+
+
+def test_strong_scaling_matches_single_rank_tokens():
+    """Greedy tokens of the strong-scaled table at tp 2 equal the 1-rank run (same table, same
+    seed): the tensor-parallel engine changes the speed of the discussion, not its content."""
+    one = _bench_single(("--temperature", "0", "--weights", "random-full:5"))
+    two = _bench(2, ("--weights", "random-full:5"))
+    assert two["detail"]["decode_tokens"] == one["detail"]["decode_tokens"]
+    assert two["detail"]["transcript_sha"] == one["detail"]["transcript_sha"]
+
+
+def _bench_single(extra=()):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--model", "tiny-llama", "--steps", "2",
+           "--warmup", "1", "--new-tokens", "8", *extra]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
 def test_bench_gpus_flag_self_launches_ranks():
     """`python bench.py --gpus 4` without a launcher starts 4 ranks itself (child torchrun) and
-    reports them — never a silent 1-GPU run (VERDICT r1 #1)."""
+    reports them — never a silent 1-GPU run (VERDICT r1 #1). Default strong scaling: one table
+    of 3 knights on a tp4 engine (VERDICT r2 next #1)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--device", "cpu", "--model", "tiny-llama",
            "--steps", "1", "--warmup", "1", "--new-tokens", "4", "--temperature", "0"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
@@ -234,7 +267,8 @@ def test_bench_gpus_flag_self_launches_ranks():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out["n_gpus"] == 4 and out["config"]["tables"] == 4 and out["detail"]["world"] == 4
+    assert out["n_gpus"] == 4 and out["detail"]["world"] == 4
+    assert out["config"]["tables"] == 1 and out["config"]["knights"] == 3 and out["config"]["parallelism"] == "tp4"
 
 
 def test_bench_rejects_world_mismatch():

@@ -64,6 +64,52 @@ def test_four_rank_tp4_llama70b_shapes_on_shared_gpu():
     assert out["detail"]["decode_tokens"] == 2 * 8 * 2 and out["detail"]["failed_turns"] == 0, out["_log"]
 
 
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_strong_scaling_bench_on_shared_gpu(nproc):
+    """The default ``--scaling strong`` bench (ONE 3-knight table, engine tensor-parallel over
+    all ranks) rehearsed with N gloo ranks on one MI355X: sharded weights, split-K shard GEMMs,
+    K9 between the ranks, C3 greedy argmax, C1 exchange; tiny-llama's 2 KV heads replicate at 4."""
+    out = _bench(("--kv-fraction", "0.05"), nproc=nproc) if nproc == 4 else _bench(nproc=nproc)
+    assert out["scaling"] == "strong" and out["config"]["parallelism"] == f"tp{nproc}"
+    assert out["config"]["tables"] == 1 and out["config"]["knights"] == 3
+    assert out["detail"]["decode_tokens"] == 3 * 16 * 2 and out["detail"]["failed_turns"] == 0, out["_log"]
+    assert out["detail"]["k9_oneshot"], out["_log"]
+
+
+def _tp_check(nproc, model, layers, tokens=12):
+    gc.collect()
+    torch.cuda.empty_cache()
+    port = free_port()
+    out = os.path.join(ROOT, "gpurun_out", f"tp_check_{model}_{layers}l_tp{nproc}.pt")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "tp_check.py"),
+           "--model", model, "--layers", str(layers), "--tokens", str(tokens), "--out", out]
+    env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.parametrize("model,layers,tp", [("llama3-8b", 2, 2), ("llama3-8b", 2, 4), ("llama3-70b", 2, 4)])
+def test_tp_fused_decode_matches_tp1_on_shared_gpu(model, layers, tp):
+    """the tensor-parallel FUSED decode with real shards — split-K NORM_ADD
+    qkv / gate_up, ping-pong residual, K9 one-shot all-reduces between the ranks, vocab-parallel
+    lm_head — against a tp=1 engine with the same ``random-dev`` weights on the same GPU:
+    prefill and decode logits cosine > 0.999, greedy tokens identical, no failed turn, no
+    expired K9 wait. Llama-3-8B shapes (the strong-scaling bench) and Llama-3-70B (config 5)."""
+    ref = _tp_check(1, model, layers)
+    got = _tp_check(tp, model, layers)
+    assert got["world"] == tp and got["fused"] and got["k9"], got
+    assert ref["fused"] and ref["world"] == 1
+    assert all(e is None for e in got["errors"]) and not got["flag_errors"], got["errors"]
+    cos = torch.nn.functional.cosine_similarity
+    c_pre = float(cos(got["prefill_logits"][None], ref["prefill_logits"][None]))
+    c_dec = float(cos(got["decode_logits"][None], ref["decode_logits"][None]))
+    assert c_pre > 0.999 and c_dec > 0.999, (c_pre, c_dec)
+    assert got["ids"] == ref["ids"], (got["ids"], ref["ids"])
+
+
 def test_rccl_data_plane_single_rank():
     """The RCCL (backend "nccl") calls of the scaling bench and the TP decode path on real
     hardware: eager communicator init with device_id, C1 all-gather, barrier(device_ids), and

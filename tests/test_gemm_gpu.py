@@ -236,18 +236,96 @@ def test_tp_fused_decode_path_matches_tp1_fused():
     assert float(cos.min()) > 0.999
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4])
-def test_ring_gemm_experiment_matches(variant):
-    """The loader-wave LDS-ring GEMM experiment (csrc/ring_gemm.hip) stays numerically correct."""
-    M, N, K = 3, 512, 2048
-    x = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
-    W = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    for grid in (7, 32):        # several tiles per workgroup: ring reuse across tiles
-        out.zero_()
-        ops.native().ring_gemm_exp(out, x, ops.shuffle_weight(W), grid, variant)
-        want = x.float() @ W.float().t()
-        assert torch.allclose(out.float(), want, atol=2e-2, rtol=2e-2)
+
+def _cus():
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+# Llama-3-8B / 70B tensor-parallel shard shapes with fewer tiles than CUs (split-K launches):
+# (N, K) of qkv / gate_up rows at tp 8 and 4, plus odd tile counts (T % 8 != 0: plain placement)
+SPLITK_SHAPES = [(768, 4096), (1536, 4096), (1792, 4096), (80, 1024), (1200, 8192)]
+
+
+@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("N,K", SPLITK_SHAPES)
+def test_skinny_gemm_splitk_every_epilogue(M, N, K):
+    """Split-K (tiles < CUs, K cut into S parts, last arriver combines in index order): every
+    prologue / epilogue the decode path uses equals the fp32 reference, repeated calls are bit-
+    identical and the tile counters re-arm."""
+    T = N // 16
+    assert T < _cus() and ops.native().splitk_parts(T, K // 32, _cus(), ops.SPLIT_WS_INTS) >= 2
+    ws = ops.split_workspace(DEV)
+    x, x2 = bf(M, K, seed=91), bf(M, K, seed=92)
+    gam = bf(K, seed=93)
+    W = bf(N, K, scale=0.05, seed=94)
+    Ws, Wg = ops.shuffle_weight(W), ops.shuffle_weight(W, gam)
+    Wf = ref.fold_gamma(W.cpu(), gam.cpu())
+    # PLAIN / NORM store
+    outs = [ops.skinny_gemm(x, Ws, split_ws=ws) for _ in range(3)]
+    close(outs[0], ref.skinny_gemm(x.cpu(), W.cpu()).to(DEV), 0.05, 0.02)
+    assert all(torch.equal(o, outs[0]) for o in outs)
+    close(ops.skinny_gemm(x, Wg, ops.PRO_NORM, eps=1e-5, split_ws=ws),
+          ref.skinny_gemm(x.cpu(), Wf, 1, eps=1e-5).to(DEV), 0.05, 0.02)
+    # NORM_ADD (tp residual + partial): every part of tile 0 publishes its K range of x + x2
+    xo = torch.zeros_like(x)
+    xo_r = torch.zeros(M, K, dtype=torch.bfloat16)
+    got = ops.skinny_gemm(x, Wg, ops.PRO_NORM_ADD, eps=1e-5, x2=x2, xout=xo, split_ws=ws)
+    close(got, ref.skinny_gemm(x.cpu(), Wf, 2, eps=1e-5, x2=x2.cpu(), xout=xo_r).to(DEV), 0.05, 0.02)
+    assert torch.equal(xo, xo_r.to(DEV))
+    # RESID in place
+    res = bf(M, N, seed=95)
+    res_ref = res.cpu().clone()
+    ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=ws)
+    ref.skinny_gemm(x.cpu(), W.cpu(), 0, 1, res=res_ref)
+    close(res, res_ref.to(DEV), 0.06, 0.02)
+    # SwiGLU over [gate; up] (N rows each) with NORM and NORM_ADD prologues
+    W2 = bf(2 * N, K, scale=0.05, seed=96)
+    W2s = ops.shuffle_weight(W2, gam, swiglu=True)
+    W2f = ref.fold_gamma(W2.cpu(), gam.cpu())
+    close(ops.skinny_gemm(x, W2s, ops.PRO_NORM, ops.EPI_SWIGLU, split_ws=ws),
+          ref.skinny_gemm(x.cpu(), W2f, 1, 2).to(DEV), 0.05, 0.03)
+    close(ops.skinny_gemm(x, W2s, ops.PRO_NORM_ADD, ops.EPI_SWIGLU, x2=x2, split_ws=ws),
+          ref.skinny_gemm(x.cpu(), W2f, 2, 2, x2=x2.cpu()).to(DEV), 0.05, 0.03)
+    assert int(ws[:256].abs().sum()) == 0, "split counters must re-arm to zero"
+    # no workspace: one workgroup per tile, same result up to summation order
+    close(ops.skinny_gemm(x, Ws), outs[0], 0.02, 0.02)
+
+
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("hq,hkv,K", [(4, 1, 4096), (8, 2, 4096), (16, 2, 8192), (2, 1, 1024)])
+def test_skinny_gemm_rope_splitk(M, hq, hkv, K):
+    """qkv shard of a tensor-parallel knight (Llama-3-8B tp 8 / 4, 70B tp 4): split-K with the
+    NORM_ADD prologue and the RoPE + paged K/V epilogue equals the fp32 reference."""
+    d = 128
+    N = (hq + 2 * hkv) * d
+    assert N // 16 < _cus()
+    x, x2 = bf(M, K, seed=101), bf(M, K, seed=102)
+    W = bf(N, K, scale=0.05, seed=103)
+    gam = bf(K, seed=104)
+    cos_sin = ref.rope_cos_sin(4096, d, 500000.0, DEV)
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int64)
+    nb = 8
+    slots = torch.randperm(nb * 32, device=DEV)[:M].to(torch.int64)
+    Ws = ops.shuffle_weight(W, gam, rope_heads=hq + hkv, head_dim=d)
+    Wp = ref.fold_gamma(W.cpu(), gam.cpu(), hq + hkv, d)
+    ws = ops.split_workspace(DEV)
+    for pro in (ops.PRO_NORM, ops.PRO_NORM_ADD):
+        kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+        xo = torch.zeros_like(x)
+        kw = dict(x2=x2, xout=xo) if pro == ops.PRO_NORM_ADD else {}
+        q = ops.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, kc, vc, slots, hq, hkv, d, 1e-5, split_ws=ws, **kw)
+        kc_r = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16)
+        vc_r = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16)
+        kw_r = dict(x2=x2.cpu(), xout=torch.zeros(M, K, dtype=torch.bfloat16)) if pro == ops.PRO_NORM_ADD else {}
+        q_r = ref.skinny_gemm_rope(x.cpu(), Wp, pro, positions.cpu(), cos_sin.cpu(), kc_r, vc_r, slots.cpu(), hq, hkv,
+                                   d, 1e-5, **kw_r)
+        close(q, q_r.to(DEV), 0.05, 0.02)
+        close(kc, kc_r.to(DEV), 0.05, 0.02)
+        close(vc, vc_r.to(DEV), 0.05, 0.02)
+        if pro == ops.PRO_NORM_ADD:
+            assert torch.equal(xo, kw_r["xout"].to(DEV))
+    assert int(ws[:256].abs().sum()) == 0
 
 
 @pytest.mark.parametrize("N,K,rope,swiglu", [(6 * 128, 256, 4, False), (512, 4096, 0, True), (4096, 14336, 0, False)])

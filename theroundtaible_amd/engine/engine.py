@@ -608,9 +608,9 @@ class Engine:
             (self.stream or torch.cuda.current_stream(self.device)).synchronize()
 
     def device_flag_errors(self) -> List[str]:
-        """Read (and clear) the poll-expiry flags of the bounded device-side waits: the K9 one-shot
-        all-reduce's peer-flag wait and the persistent decode kernel's phase wait. A set flag means
-        the kernel proceeded on stale data, so the turn's output is wrong."""
+        """Read (and clear) the poll-expiry flag of the bounded device-side wait of the K9 one-shot
+        all-reduce (a peer's flag). A set flag means the kernel proceeded on stale data, so the
+        turn's output is wrong."""
         msgs: List[str] = []
         if not self.on_gpu:
             return msgs
@@ -618,11 +618,6 @@ class Engine:
         if os_ is not None and os_.error() > 0:
             os_.clear_error()
             msgs.append("K9 one-shot all-reduce: a peer's flag never arrived (poll expired)")
-        if getattr(self.model, "use_persistent", False):
-            for g in self.graphs.values():
-                if int(g.ws.err.item()):
-                    g.ws.err.zero_()
-                    msgs.append("persistent decode kernel: a phase wait expired")
         return msgs
 
     def check_device_flags(self) -> None:

@@ -14,7 +14,6 @@ Per layer (decode and prefill share the code; only the attention op differs):
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -53,7 +52,7 @@ class LlamaModel:
         self.device = device
         self.dtype = dtype
         self.n_heads = cfg.n_heads // self.tp.size
-        self.n_kv_heads = cfg.n_kv_heads // self.tp.size
+        self.n_kv_heads = self.tp.kv_heads(cfg.n_kv_heads)   # replicated when tp > KV heads
         self.head_dim = cfg.head_dim
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.cos_sin = rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device)
@@ -79,8 +78,6 @@ class LlamaModel:
                 and self.lm_rows % 16 == 0)
 
     use_fused = True
-    # one persistent launch per layer instead of five (csrc/decode_layer.hip)
-    use_persistent = os.environ.get("ROUNDTABLE_PERSISTENT_DECODE", "0") == "1"
     force_tp_path = False   # tests: run the tensor-parallel fused path at tp=1 (all-reduces are no-ops)
     _dec = None
 
@@ -109,8 +106,6 @@ class LlamaModel:
                         d[name] = ops.shuffle_weight(lw[name], lw[norm] if norm else None, **kw)
                         if drop_originals:
                             lw[name] = None
-                    # gate_up's tile count (ffn/16) is rarely a multiple of the CU count: balanced launch
-                    d["gu_split_ws"] = ops.split_workspace(d["w_gate_up"].device)
                     layers.append(d)
                 lm = ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])
                 if drop_originals:
@@ -121,7 +116,12 @@ class LlamaModel:
                     self._scratch = {}
                     if self.device.type == "cuda":
                         torch.cuda.empty_cache()
-                self._dec = {"layers": layers, "lm_head": lm}
+                # ONE split workspace for every decode GEMM of this model (they run in order on
+                # the engine's stream; counters re-arm at the end of each call): split-K for shard
+                # shapes with fewer tiles than CUs (tensor parallel), and the balanced launch of
+                # gate_up, whose tile count (ffn/16) is rarely a multiple of the CU count
+                ws = ops.split_workspace(lm.device) if lm.is_cuda else None
+                self._dec = {"layers": layers, "lm_head": lm, "split_ws": ws}
         return self._dec
 
     def _row_major(self, l: Optional[int], name: str) -> torch.Tensor:
@@ -164,25 +164,19 @@ class LlamaModel:
         # the residual stream is updated in place by every RESID epilogue
         res = hidden if hidden is not None else F.embedding(ids, self.w["embed"]).contiguous()
         B = ids.shape[0]
-        if self.use_persistent and self.head_dim == 128 and kv.block_size == 32:
-            ws = meta.workspace or ops.DecodeWorkspace(B, self.n_heads, self.head_dim, max(1, meta.num_splits),
-                                                       res.device)
-            for l, lw in enumerate(dec["layers"]):
-                ops.decode_layer(res, lw, positions, self.cos_sin, kv.k_layer(l), kv.v_layer(l), meta.slot_mapping,
-                                 meta.block_tables, meta.ctx_lens, self.n_heads, self.n_kv_heads, self.head_dim,
-                                 max(1, meta.num_splits), ws, eps, self.scale)
-            logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
-            return logits[:, :cfg.vocab]
+        sw, SK, ALL = dec["split_ws"], ops.SPLIT_K, ops.SPLIT_K | ops.SPLIT_BALANCE
         for l, lw in enumerate(dec["layers"]):
             q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kv.k_layer(l),
                                      kv.v_layer(l), meta.slot_mapping, self.n_heads, self.n_kv_heads,
-                                     self.head_dim, eps)
+                                     self.head_dim, eps, split_ws=sw, split_mode=SK)
             a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)
-            ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
-            g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps,
-                                split_ws=lw.get("gu_split_ws"))
-            ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
-        logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps)
+            ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=sw,
+                            split_mode=SK)
+            g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps, split_ws=sw,
+                                split_mode=ALL)
+            ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=sw, split_mode=SK)
+        logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps, split_ws=sw,
+                                 split_mode=SK)
         return logits[:, :cfg.vocab]
 
     def forward_decode_fused_tp(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
@@ -200,23 +194,25 @@ class LlamaModel:
         cur = 0
         B = ids.shape[0]
         h = None
+        # split-K wherever a shard has fewer tiles than CUs (qkv / gate_up at tp >= 2)
+        sk = dict(split_ws=dec["split_ws"], split_mode=ops.SPLIT_K)
         for l, lw in enumerate(dec["layers"]):
             kc, vc = kv.k_layer(l), kv.v_layer(l)
             if h is None:
                 q = ops.skinny_gemm_rope(bufs[cur], lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kc, vc,
-                                         meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps)
+                                         meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps, **sk)
             else:
                 q = ops.skinny_gemm_rope(bufs[cur], lw["wqkv"], ops.PRO_NORM_ADD, positions, self.cos_sin, kc, vc,
                                          meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps,
-                                         x2=h, xout=bufs[1 - cur])
+                                         x2=h, xout=bufs[1 - cur], **sk)
                 cur = 1 - cur
             a = self.attention(q, kc, vc, meta)
-            h = tp.all_reduce(ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_STORE))
+            h = tp.all_reduce(ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_STORE, **sk))
             g = ops.skinny_gemm(bufs[cur], lw["w_gate_up"], ops.PRO_NORM_ADD, ops.EPI_SWIGLU, eps=eps, x2=h,
-                                xout=bufs[1 - cur])
+                                xout=bufs[1 - cur], **sk)
             cur = 1 - cur
-            h = tp.all_reduce(ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_STORE))
-        logits = ops.skinny_gemm(bufs[cur], dec["lm_head"], ops.PRO_NORM_ADD, ops.EPI_STORE, eps=eps, x2=h)
+            h = tp.all_reduce(ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_STORE, **sk))
+        logits = ops.skinny_gemm(bufs[cur], dec["lm_head"], ops.PRO_NORM_ADD, ops.EPI_STORE, eps=eps, x2=h, **sk)
         if meta.local_logits:
             return logits
         logits = tp.all_gather_last(logits)

@@ -4,7 +4,10 @@
 generator seeded by (seed, tensor name, tp rank) — an 8B model materializes in well
 under a second on MI355X. ``random-full:<seed>`` builds the *unsharded* tensors on CPU
 first and then shards them, so TP=1 and TP=N see identical math (TP equivalence
-tests). A path loads HF-named safetensors (Llama/Mistral/GPT-2 naming) and shards it.
+tests). ``random-dev:<seed>`` does the same with the full tensors generated on the target
+device, one tensor at a time (GPU TP checks at 8B / 70B shapes, where CPU generation of the
+unsharded model would take minutes and tens of GB of host memory per rank).
+A path loads HF-named safetensors (Llama/Mistral/GPT-2 naming) and shards it.
 """
 from __future__ import annotations
 
@@ -87,7 +90,8 @@ def shard_tensor(name: str, w: torch.Tensor, kind: Optional[str], cfg: ModelConf
     if kind == "qkv":
         D = cfg.head_dim
         q, k, v = w.split([cfg.n_heads * D, cfg.n_kv_heads * D, cfg.n_kv_heads * D], dim=0)
-        return torch.cat([shard_rows(q, tp), shard_rows(k, tp), shard_rows(v, tp)])
+        h0, nh = tp.kv_head0(cfg.n_kv_heads), tp.kv_heads(cfg.n_kv_heads)
+        return torch.cat([shard_rows(q, tp), k[h0 * D:(h0 + nh) * D], v[h0 * D:(h0 + nh) * D]])
     raise ValueError(kind)
 
 
@@ -102,7 +106,7 @@ def local_shape(shape, kind, cfg: ModelConfig, tp: TPInfo):
     elif kind == "col":
         s[1] //= tp.size
     elif kind == "qkv":
-        s[0] = (cfg.n_heads // tp.size + 2 * (cfg.n_kv_heads // tp.size)) * cfg.head_dim
+        s[0] = (cfg.n_heads // tp.size + 2 * tp.kv_heads(cfg.n_kv_heads)) * cfg.head_dim
     return tuple(s)
 
 
@@ -111,16 +115,18 @@ def materialize(cfg: ModelConfig, spec: str, device, dtype=torch.bfloat16, tp: O
     tp = tp or TPInfo()
     lay = layout_for(cfg)
     out: Dict[str, torch.Tensor] = {}
-    if spec.startswith("random:") or spec.startswith("random-full:"):
-        full = spec.startswith("random-full:")
+    if spec.startswith(("random:", "random-full:", "random-dev:")):
+        full = spec.startswith(("random-full:", "random-dev:"))
+        gen_dev = torch.device(device) if spec.startswith("random-dev:") else torch.device("cpu")
         seed = int(spec.split(":", 1)[1] or 0)
         for name, (shape, init, kind) in lay.items():
             if full:
-                g = torch.Generator().manual_seed(_seed_for(seed, name, 0))
-                w = _init(shape, init, std, g, "cpu", torch.float32)
+                g = torch.Generator(device=gen_dev).manual_seed(_seed_for(seed, name, 0))
+                w = _init(shape, init, std, g, gen_dev, torch.float32)
                 if init == "normal" and name in ("embed", "wte"):
                     w = w * 10  # unit-ish scale residual stream for the embedding
                 out[name] = shard_tensor(name, w, kind, cfg, tp).to(device=device, dtype=dtype).contiguous()
+                del w
             else:
                 shp = local_shape(shape, kind, cfg, tp)
                 dev = torch.device(device)

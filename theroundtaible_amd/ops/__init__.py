@@ -270,29 +270,34 @@ def unshuffle_weight(Ws: torch.Tensor, rope_heads: int = 0, head_dim: int = 0, s
     return out
 
 
-# CU-balanced skinny GEMM workspace: 256 counter words + 2 K-halves x 528 floats per split
-# tile, up to 255 split tiles (tile count mod CU count); csrc/gemm_skinny.hip split_workspace_ints
-SPLIT_WS_INTS = 256 + 255 * 2 * (16 * 16 * 2 + 16)
+# split-K / CU-balanced skinny GEMM workspace: 256 tile counters + 528 floats per tile part, up
+# to 1024 parts (split-K: T x S; balanced: 2 x (tile count mod CU count));
+# csrc/gemm_skinny.hip splitk_parts / split_workspace_ints
+SPLIT_WS_INTS = 256 + 1024 * (16 * 16 * 2 + 16)
+SPLIT_K, SPLIT_BALANCE = 2, 1     # split_mode bits
 
 
 def split_workspace(device) -> torch.Tensor:
-    """Zeroed workspace for one call site of :func:`skinny_gemm` ``split_ws`` (one per weight:
-    concurrent launches must not share it; its counters return to zero after every call)."""
+    """Zeroed workspace for :func:`skinny_gemm` ``split_ws``. Launches on ONE stream may share it
+    (its counters return to zero at the end of every call); concurrent launches must not."""
     return torch.zeros(SPLIT_WS_INTS, dtype=torch.int32, device=device)
 
 
 def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: int = EPI_STORE,
                 res: Optional[torch.Tensor] = None, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
-                xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None,
+                split_mode: int = SPLIT_K | SPLIT_BALANCE) -> Optional[torch.Tensor]:
     """Decode linear (M <= 16) on shuffled weights with fused RMSNorm prologue (gamma pre-folded)
     and residual / SwiGLU epilogue. Returns the output (None for RESID, which updates ``res``).
     ``PRO_NORM_ADD``: normalizes ``bf16(x + x2)`` and writes that sum to ``xout`` (TP decode).
-    ``split_ws`` (:func:`split_workspace`): when the tile count is not a multiple of the CU count,
-    the remainder tiles run as two K-halves each so every CU streams the same bytes."""
+    ``split_ws`` (:func:`split_workspace`) enables, per ``split_mode`` bit: ``SPLIT_K`` — fewer
+    tiles than CUs (tensor-parallel shards): each tile's K range runs as S workgroups whose last
+    arriver combines; ``SPLIT_BALANCE`` — tile count not a multiple of the CU count: the remainder
+    tiles run as two K-halves so every CU streams the same bytes."""
     if _use_native(x):
         n = Ws.shape[0] // (2 if epi == EPI_SWIGLU else 1)
         out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device) if epi != EPI_RESID else x
-        native().skinny_gemm(out, x, Ws, pro, epi, res, eps, x2, xout, split_ws)
+        native().skinny_gemm(out, x, Ws, pro, epi, res, eps, x2, xout, split_ws, int(split_mode))
         return None if epi == EPI_RESID else out
     return ref.skinny_gemm(x, Ws, pro, epi, res, eps, x2, xout)
 
@@ -300,15 +305,16 @@ def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: in
 def skinny_gemm_rope(x: torch.Tensor, Ws: torch.Tensor, pro: int, positions: torch.Tensor, cos_sin: torch.Tensor,
                      k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor, n_heads: int,
                      n_kv_heads: int, head_dim: int, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
-                     xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None,
+                     split_mode: int = SPLIT_K | SPLIT_BALANCE) -> torch.Tensor:
     """Decode qkv projection (+ optional RMSNorm prologue) with RoPE and the paged K/V cache
     write fused into the epilogue; returns q [M, n_heads, head_dim]. ``Ws`` must come from
     ``shuffle_weight(Wqkv, gamma, rope_heads=n_heads + n_kv_heads, head_dim=head_dim)``.
-    ``split_ws``: CU-balanced launch as in :func:`skinny_gemm` (not with ``PRO_NORM_ADD``)."""
+    ``split_ws`` / ``split_mode``: as in :func:`skinny_gemm` (no balanced launch with ``PRO_NORM_ADD``)."""
     if _use_native(x):
         q = torch.empty(x.shape[0], n_heads, head_dim, dtype=x.dtype, device=x.device)
         native().skinny_gemm_rope(q, x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
-                                  head_dim, eps, x2, xout, split_ws)
+                                  head_dim, eps, x2, xout, split_ws, int(split_mode))
         return q
     return ref.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
                                 head_dim, eps, x2, xout)
@@ -353,23 +359,6 @@ def decode_advance(out: torch.Tensor, ids: torch.Tensor, positions: torch.Tensor
             native().decode_advance(out, ids, positions, ctx_lens, step, nxt, slots, offsets, res, bt, embed, int(bs))
         return
     ref.decode_advance(out, ids, positions, ctx_lens, step, nxt, prep)
-
-
-def decode_layer(res: torch.Tensor, lw: dict, positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,
-                 v_cache: torch.Tensor, slots: torch.Tensor, block_tables: torch.Tensor, ctx_lens: torch.Tensor,
-                 n_heads: int, n_kv_heads: int, head_dim: int, num_splits: int, ws: DecodeWorkspace, eps: float,
-                 scale: float, stamps: Optional[torch.Tensor] = None) -> None:
-    """One whole decode layer in ONE persistent launch (csrc/decode_layer.hip); updates ``res``
-    in place. ``lw``: the layer's shuffled weights (wqkv with rope rows, wo, w_gate_up, w_down)."""
-    M = res.shape[0]
-    if not _use_native(res):
-        raise RuntimeError("decode_layer is GPU-only (CPU runs the unfused reference path)")
-    q = torch.empty(M, n_heads, head_dim, dtype=res.dtype, device=res.device)
-    a = torch.empty(M, n_heads * head_dim, dtype=res.dtype, device=res.device)
-    g = torch.empty(M, lw["w_down"].shape[1], dtype=res.dtype, device=res.device)
-    native().decode_layer(res, q, a, g, lw["wqkv"], lw["wo"], lw["w_gate_up"], lw["w_down"], positions, cos_sin,
-                          k_cache, v_cache, slots, block_tables, ctx_lens, ws.partial_o, ws.partial_ml, ws.counters,
-                          ws.sync, ws.err, n_heads, n_kv_heads, int(num_splits), eps, scale, stamps)
 
 
 def silu_and_mul(x: torch.Tensor) -> torch.Tensor:

@@ -165,7 +165,7 @@ class GroupPlan:
 def _tp_ok(model: str, overrides: Optional[dict], tp: int) -> bool:
     from ..models.config import get_config
     c = get_config(model, **(overrides or {}))
-    return c.n_kv_heads % tp == 0 and c.n_heads % tp == 0 and c.ffn % tp == 0
+    return ((c.n_kv_heads % tp == 0 or tp % c.n_kv_heads == 0) and c.n_heads % tp == 0 and c.ffn % tp == 0)
 
 
 def plan_placement(knights: Sequence[dict], inv: Inventory, policy: Optional[PlacementPolicy] = None) -> List[GroupPlan]:

@@ -39,6 +39,20 @@ class TPInfo:
     def backend(self) -> str:
         return dist.get_backend(self.group) if self.size > 1 else "none"
 
+    def kv_heads(self, n_kv: int) -> int:
+        """KV heads held per rank: an even split, or ONE (replicated) when the group is wider
+        than the model's KV heads — ranks ``r`` with equal ``r * n_kv // size`` share a head
+        (GQA: their query heads all read it). Needs ``size % n_kv == 0`` then."""
+        if n_kv >= self.size:
+            return self.shard(n_kv)
+        if self.size % n_kv:
+            raise ValueError(f"tp={self.size} is neither a divisor nor a multiple of the {n_kv} KV heads")
+        return 1
+
+    def kv_head0(self, n_kv: int) -> int:
+        """First (global) KV head of this rank's shard."""
+        return self.rank * n_kv // self.size if n_kv < self.size else self.rank * self.shard(n_kv)
+
     def _host_staged(self, x: torch.Tensor) -> bool:
         # gloo (CPU CI, or the shared-GPU rehearsal mode of parallel/cluster.py) moves GPU
         # tensors through host memory explicitly; RCCL works on device memory directly
@@ -109,6 +123,38 @@ class TPInfo:
         parts: List[torch.Tensor] = [torch.empty_like(src) for _ in range(self.size)]
         dist.all_gather(parts, src, group=self.group)
         return torch.cat(parts, dim=-1).to(x.device)
+
+
+class SimulatedTP(TPInfo):
+    """Cost-model stand-in (``bench.py --simulate-tp N``, tools/tp_cost.py): ONE process computes
+    rank 0's shard of a tp=N knight — the exact per-rank GEMM / attention / sampler shapes, in
+    the captured decode graph — while every collective is replaced by a local op of the same
+    output shape and no communication: all-reduce is the identity, the vocab all-gather tiles the
+    local shard N times (the copy a gather would write). The communication time is added by the
+    cost model from measured collective latencies. Never used for a real multi-GPU run."""
+
+    def __init__(self, size: int):
+        super().__init__(size=size, rank=0, group=None)
+
+    def backend(self) -> str:
+        return "nccl"            # keep hipGraph capture on, as on a real RCCL group
+
+    def setup_oneshot(self) -> None:
+        self.oneshot = None
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        self.sim_all_reduces = getattr(self, "sim_all_reduces", 0) + 1
+        return x
+
+    def any_rank(self, flag: bool) -> bool:
+        return flag
+
+    def greedy_gather(self, local: torch.Tensor, vocab: int) -> torch.Tensor:
+        lim = max(1, min(local.shape[1], vocab))
+        return local[:, :lim].float().argmax(dim=1)
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        return x.repeat(1, self.size)
 
 
 def shard_rows(w: torch.Tensor, tp: TPInfo) -> torch.Tensor:

@@ -110,6 +110,58 @@ def bench_gemm(M):
         torch.cuda.empty_cache()
 
 
+def bench_gemm_tp(M, tp, model="llama3-8b"):
+    """The per-rank decode GEMMs of a tensor-parallel knight, exactly as forward_decode_fused_tp
+    issues them (NORM_ADD prologues, STORE epilogues before the all-reduce, split-K workspace):
+    qkv [(Hq+2Hkv)/tp * D, H], o [H, Hq*D/tp], gate_up [2 F/tp, H], down [H, F/tp], lm_head
+    [V/tp, H]. RT_SPLITK / RT_SPLITK_TARGET pin the split (read once per process)."""
+    from theroundtaible_amd.models.config import get_config
+    c = get_config(model)
+    hid, d = c.hidden, c.head_dim
+    hq, hkv, ffn = c.n_heads // tp, c.n_kv_heads // tp, c.ffn // tp
+    vs = -(-c.vocab // tp)
+    vs = -(-vs // 16) * 16
+    x, x2, xo = bf(M, hid), bf(M, hid), bf(M, hid)
+    a_in, g_in = bf(M, c.n_heads * d // tp), bf(M, ffn)
+    nb = 64
+    kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+    cs = ref.rope_cos_sin(8192, d, c.rope_theta, DEV)
+    pos = torch.arange(M, device=DEV, dtype=torch.int64) + 100
+    slots = torch.arange(M, device=DEV, dtype=torch.int64) + 40
+    sw = ops.split_workspace(DEV)
+    sk = dict(split_ws=sw, split_mode=ops.SPLIT_K)
+    shapes = [("qkv (norm_add+rope+cache)", (hq + 2 * hkv) * d, hid), ("o (store)", hid, hq * d),
+              ("gate_up (norm_add+swiglu)", 2 * ffn, hid), ("down (store)", hid, ffn), ("lm_head (norm_add)", vs, hid)]
+    total = 0.0
+    for name, N, K in shapes:
+        nbytes = N * K * 2
+        copies = max(2, math.ceil(2**30 / nbytes))
+        rope = name.startswith("qkv")
+        Ws = [ops.shuffle_weight(bf(N, K, scale=0.02), swiglu=name.startswith("gate_up"),
+                                 rope_heads=hq + hkv if rope else 0, head_dim=d if rope else 0) for _ in range(copies)]
+        if rope:
+            fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM_ADD, pos, cs, kc, vc, slots, hq, hkv, d,
+                                                x2=x2, xout=xo, **sk)
+        elif name.startswith("gate_up"):
+            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM_ADD, ops.EPI_SWIGLU, x2=x2, xout=xo, **sk)
+        elif name.startswith("lm_head"):
+            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM_ADD, ops.EPI_STORE, x2=x2, **sk)
+        else:
+            inp = a_in if name.startswith("o ") else g_in
+            fn = lambda i, inp=inp: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_STORE, **sk)
+        us = timed(fn)
+        T = N // 16 // (2 if name.startswith("gate_up") else 1)
+        S = ops.native().splitk_parts(T, K // 32, torch.cuda.get_device_properties(0).multi_processor_count,
+                                      ops.SPLIT_WS_INTS)
+        total += us * (1 if name.startswith("lm_head") else c.n_layers)
+        row(f"tp{tp} {name} M={M} N={N} K={K} tiles={T} splitk={S or 1}", us, nbytes, 2 * M * N * K)
+        del Ws
+        torch.cuda.empty_cache()
+    print(f"tp{tp} {model}: decode GEMMs per step (L x layer + lm_head) = {total:.1f} us", flush=True)
+    ROWS.append((f"tp{tp} {model} GEMMs per decode step", f"{total:.1f}", "", ""))
+
+
 def bench_attn(B, ctx, splits_list):
     hq, hkv, d = 32, 8, 128
     nblk = (ctx + 31) // 32
@@ -195,11 +247,16 @@ def main():
     ap.add_argument("--only", default="gemm,attn,sample,prefill")
     ap.add_argument("--splits", default="4,8,11,16,32")
     ap.add_argument("--shared", default="22000:1500", help="grouped attention: shared:private tokens list, comma-sep")
+    ap.add_argument("--tp", default="2,4,8", help="gemm_tp: tensor-parallel degrees of the shard shapes")
+    ap.add_argument("--model", default="llama3-8b", help="gemm_tp: model preset")
     a = ap.parse_args()
     only = set(a.only.split(","))
     torch.manual_seed(0)
     if "gemm" in only:
         bench_gemm(a.batch)
+    if "gemm_tp" in only:
+        for tp in (int(t) for t in a.tp.split(",")):
+            bench_gemm_tp(a.batch, tp, a.model)
     if "attn" in only:
         bench_attn(a.batch, a.ctx, [int(s) for s in a.splits.split(",")])
         bench_attn(a.batch, 1500, [4, 8, 11, 16])
