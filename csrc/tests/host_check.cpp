@@ -9,7 +9,8 @@
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
                        int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
-                       int* split_ws, int64_t split_ws_ints);
+                       int* split_ws, int64_t split_ws_ints, int split_mode);
+int splitk_parts(int T, int ks, int cus, int64_t ws_ints);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
@@ -40,17 +41,23 @@ static int failures = 0;
 int main() {
   // decode GEMM: M outside [1, 16], K not a multiple of 32, N not a multiple of 16, missing operands
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 0, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr, nullptr, 0) == -1);
+                            nullptr, nullptr, nullptr, 0, 3) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 17, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr, nullptr, 0) == -1);
+                            nullptr, nullptr, nullptr, 0, 3) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 48, 16, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr, nullptr, 0) == -1);
+                            nullptr, nullptr, nullptr, 0, 3) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 24, 64, 24, 1e-5f, 0, 0, nullptr, nullptr,
-                            nullptr, nullptr, nullptr, 0) == -1);
+                            nullptr, nullptr, nullptr, 0, 3) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 2, 0, nullptr, nullptr,
-                            nullptr, nullptr, nullptr, 0) == -5);   // NORM_ADD without its second operand
+                            nullptr, nullptr, nullptr, 0, 3) == -5);   // NORM_ADD without its second operand
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 64, 16, 1e-5f, 0, 3, nullptr, nullptr,
-                            nullptr, nullptr, nullptr, 0) == -3);   // ROPE epilogue without its parameters
+                            nullptr, nullptr, nullptr, 0, 3) == -3);   // ROPE epilogue without its parameters
+  // split-K part choice: only with fewer tiles than CUs, >= 8 k-steps per part, within the workspace
+  EXPECT(splitk_parts(384, 128, 256, 1 << 20) == 0);          // tp=1 qkv: tiles >= CUs, no split
+  EXPECT(splitk_parts(48, 128, 256, 1 << 20) >= 2);           // tp=8 qkv shard
+  EXPECT(splitk_parts(48, 8, 256, 1 << 20) == 0);             // one part of 8 k-steps only
+  EXPECT(splitk_parts(48, 128, 256, 256 + 2 * 528 * 48 - 1) == 0);   // workspace below 2 parts
+  EXPECT(splitk_parts(100, 128, 0, 1 << 20) == 0);            // unknown CU count
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 16, 48, 0, 0, 0, nullptr) == -1);
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 32, 64, 64, 128, 0, nullptr) == -1);   // rope rows > N
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 48, 64, 0, 0, 1, nullptr) == -1);      // SwiGLU halves of 24 rows

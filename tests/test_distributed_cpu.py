@@ -332,3 +332,55 @@ def test_c1_token_gather_overlaps_metadata_round():
         order, meta, got = res[r]
         assert order == ["started", "metadata", "tokens"] and meta == [0, 1]
         assert got == {0: [0, 0], 1: [1, 1, 1]}
+
+
+def _tp_project(tmp_path, knights_engine):
+    cfg = {"version": "1.0", "project": "spmd", "language": "nl",
+           "knights": [{"name": n, "adapter": f"local-llm-{n.lower()}", "capabilities": ["x"], "priority": i + 1}
+                       for i, n in enumerate(knights_engine)],
+           "rules": {"max_rounds": 1, "consensus_threshold": 9, "timeout_per_turn_seconds": 300,
+                     "escalate_to_user_after": 5, "auto_execute": False, "ignore": [".git"]},
+           "chronicle": ".roundtable/chronicle.md",
+           "engine": {"default_model": "tiny-llama", "weights": "random-full:4", "max_new_tokens": 6,
+                      "ignore_eos": True, "temperature": 0.0, "device": "cpu"},
+           "adapter_config": {f"local-llm-{n.lower()}": {"engine": eng} for n, eng in knights_engine.items()}}
+    os.makedirs(tmp_path / ".roundtable" / "sessions")
+    (tmp_path / ".roundtable" / "config.json").write_text(json.dumps(cfg))
+    (tmp_path / ".roundtable" / "chronicle.md").write_text("# Chronicle\n")
+
+
+def test_plain_cli_discuss_launches_tp_ranks(tmp_path):
+    """a plain ``python -m theroundtaible_amd discuss`` (no torchrun) with a
+    ``tp: 2`` knight starts the 2 ranks itself before any device call and the knight really runs
+    tensor-parallel: metrics.jsonl records tp=2 for its turns; rc 0; one session written."""
+    _tp_project(tmp_path, {"Groot": {"tp": 2}, "Klein": {}})
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-m", "theroundtaible_amd", "discuss", "TP onderwerp", "--no-read-codebase",
+                        "--choice", "4"], capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "Launching 2 ranks" in r.stderr
+    sessions = os.listdir(tmp_path / ".roundtable" / "sessions")
+    assert len(sessions) == 1
+    recs = [json.loads(l) for l in (tmp_path / ".roundtable" / "sessions" / sessions[0] / "metrics.jsonl")
+            .read_text().splitlines() if l.strip()]
+    tps = {m["knight"]: m.get("tp") for m in recs if "knight" in m}
+    assert tps == {"Groot": 2, "Klein": 1}, tps
+
+
+def test_tp_knight_outside_a_launcher_is_refused(tmp_path):
+    """The in-process backend factory never degrades a tp > 1 knight to tp 1."""
+    from theroundtaible_amd.config import load_config
+    from theroundtaible_amd.errors import ConfigError
+    from theroundtaible_amd.knights.registry import BackendFactory
+    _tp_project(tmp_path, {"Groot": {"tp": 2}})
+    with pytest.raises(ConfigError):
+        BackendFactory(load_config(str(tmp_path))).create("local-llm-groot")
+
+
+def test_ranks_needed_from_placement(tmp_path):
+    from theroundtaible_amd.config import load_config
+    from theroundtaible_amd.parallel.launch import ranks_needed
+    _tp_project(tmp_path, {"A": {"tp": 4}, "B": {"gpus": [5]}, "C": {}})
+    n, why, cpu = ranks_needed(load_config(str(tmp_path)))
+    assert n == 6 and "A tp=4" in why and cpu

@@ -352,3 +352,25 @@ def test_shuffled_only_residency_engine():
     oa = a.run_turns([Turn("x", "hallo tafel " * 30, sp)])[0]
     ob = b.run_turns([Turn("x", "hallo tafel " * 30, sp)])[0]
     assert oa.error is None and ob.error is None and len(ob.ids) == 6
+
+
+def test_shuffled_only_load_peak_is_one_weight_copy():
+    """shuffled-only residency frees each row-major linear as soon as its shuffled copy
+    exists (both references), so the load peak is ONE weight copy + one tensor — not the row-major
+    weights plus the full shuffled copy (a 70B knight on one GPU fits by only ~8 GB)."""
+    import gc
+    from theroundtaible_amd.engine import Engine, EngineConfig
+    from theroundtaible_amd.models.config import get_config
+    gc.collect()
+    torch.cuda.empty_cache()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    e = Engine(EngineConfig(model="llama3-8b", weights="random:5", device=DEV, weight_residency="shuffled",
+                            defer_kv=True, model_overrides={"n_layers": 4}))
+    assert e.model.shuffled_only
+    cfg = e.cfg
+    wbytes = cfg.n_params() * 2
+    biggest = cfg.vocab * cfg.hidden * 2
+    peak = torch.cuda.max_memory_allocated() - base
+    assert peak <= wbytes + 1.05 * biggest + (256 << 20), (peak / 2**30, wbytes / 2**30)
+    del e

@@ -75,6 +75,23 @@ def test_greedy_is_deterministic_and_session_reuses_kv(server):
     assert server.sched.stats["reused_tokens"] - before > 10   # the first exchange stayed resident
 
 
+def test_session_with_system_message_keeps_conversation_kv(server):
+    """with a system message (shared system-prompt prefix, on by default) the session's
+    next turn must still reuse the whole first exchange — attaching the shared system blocks may
+    not truncate a conversation that already holds them."""
+    body = {"max_tokens": 5, "temperature": 0, "user": "knight-sys"}
+    sys_msg = {"role": "system", "content": "Je bent een ridder van de ronde tafel. " * 12}
+    conv = [sys_msg, {"role": "user", "content": "Eerste vraag over de gedeelde systeemprompt."}]
+    r1 = json.loads(_post(server.url + "/v1/chat/completions", dict(body, messages=conv))[1])
+    conv2 = conv + [{"role": "assistant", "content": r1["choices"][0]["message"]["content"]},
+                    {"role": "user", "content": "En de tweede?"}]
+    prompt1 = r1["usage"]["prompt_tokens"]
+    before = server.sched.stats["reused_tokens"]
+    _post(server.url + "/v1/chat/completions", dict(body, messages=conv2))
+    # the first request's prompt (system + first question) was reused, not just the system blocks
+    assert server.sched.stats["reused_tokens"] - before >= prompt1 - 1
+
+
 def test_concurrent_requests_are_batched(server):
     results, errs = [], []
 
@@ -136,9 +153,10 @@ def test_shared_system_prompt_kv(server):
                       "max_tokens": 6, "temperature": 0, "user": f"deel-{u}"}
     outs = [json.loads(_post(server.url + "/v1/chat/completions", body(u))[1]) for u in ("een", "twee")]
     e = server.engine
-    shared = [k for k in e.kv.seqs if k.startswith("@shared:sys:")]
+    shared = [e.kv.seqs[k] for k in e.kv.seqs if k.startswith("@shared:sys:")]
     assert shared, "no shared system-prompt sequence"
-    sq = e.kv.seqs[shared[0]]
+    first = e.kv.seqs["session:deel-een"].blocks[:1]
+    sq = next(q for q in shared if q.blocks[:1] == first)    # (other tests' system prompts live too)
     full = sq.length // e.kv.block_size
     assert full >= 2
     for u in ("een", "twee"):

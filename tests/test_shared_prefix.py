@@ -108,3 +108,40 @@ def test_encode_prompt_split_head_length():
         want = len(e.encode_prompt(head)) + (len(e.tokenizer.chat_prefix or []) if not p.templated else 0)
         assert n == min(want, len(ids) - 1) and ids == e.encode_prompt(p)
         assert ids[-3:] == [5, 6, 7] or e.tokenizer.chat_suffix
+
+
+def test_flag_fault_drops_the_shared_prefix_too():
+    """an expired device wait ('flag' fault) during a shared-layout turn fails the
+    turn AND frees the table's shared sequence (its all-reduced KV may be stale); the next turn
+    prefills the shared prefix again instead of handing it to every member by LCP."""
+    e = Engine(EngineConfig(model="tiny-llama", device="cpu", dtype="fp32", num_blocks=512, weights="random:3",
+                            faults={1: "flag"}))
+    a = e.run_turns(_turns([], 1, "t0"))
+    assert all(x.error is None for x in a)
+    sk = e.shared_seq_key("t0@table")
+    assert sk in e.kv.seqs and e.kv.seqs[sk].length > 0
+    b = e.run_turns(_turns([], 1, "t0"))                      # call 1: injected poll expiry
+    assert all(x.error is not None and x.error.kind == "device" for x in b)
+    assert sk not in e.kv.seqs and sk not in e._shared_lru
+    c = e.run_turns(_turns([], 1, "t0"))
+    assert all(x.error is None for x in c)
+    assert c[0].metrics["prefill_tokens"] >= e.kv.seqs[sk].length   # shared prefix prefilled again
+    assert [x.ids for x in c] == [x.ids for x in a]
+
+
+def test_lru_never_evicts_a_shared_key_of_the_current_batch():
+    """with more distinct shared keys in one batch than MAX_SHARED_SEQS, the LRU
+    must not free a shared sequence the same batch reserved before its members attached."""
+    e = _engine()
+    e.MAX_SHARED_SEQS = 2
+    ctx = TurnContext(topic="LRU van gedeelde prefixen " * 6)
+    turns = []
+    for t in range(4):
+        p = build_turn_prompt_shared(KNIGHTS[0], KNIGHTS, ctx, [], 1, shared_key=f"tafel{t}")
+        turns.append(Turn(f"k{t}", p, SamplingParams(temperature=0.0, max_new_tokens=4, ignore_eos=True,
+                                                     stop_on_consensus=False)))
+    out = e.run_turns(turns)
+    assert all(o.error is None for o in out)
+    for t in range(4):          # every member still references live (allocated) blocks
+        for blk in e.kv.seqs[f"k{t}"].blocks:
+            assert e.kv.alloc.ref[blk] > 0

@@ -141,9 +141,10 @@ def _session(root: str, name: Optional[str]):
 def _generate(root: str, config, lead: str, prompt: str, args, ui: UI) -> str:
     if args.response_file:
         return read_text(args.response_file)
-    from ..knights.registry import BackendFactory
+    from ..cli import make_backends
     knight = next((k for k in config.knights if k.name == lead), None) or sorted(config.knights, key=lambda k: k.priority)[0]
-    backend = BackendFactory(config, device_override=args.device).create(knight.adapter)
+    backends, _ = make_backends(config, ui, args, only_knight=knight.name)
+    backend = backends.get(knight.adapter)
     if backend is None:
         raise ValidationError(f"lead knight {lead} has no usable backend ({knight.adapter})")
     from ..knights.base import TurnRequest
@@ -171,10 +172,13 @@ def apply_command(args, ui: UI) -> int:
     src, hashes = source_context(root, existing)
     prompt = build_apply_prompt(topic, decision, lead, allowed, src)
     dry = bool(args.dry_run)
-    if not dry:
+    from ..cli import is_writer
+    if not dry and is_writer():
         store.update_status(path, phase="applying")
     ui.print(f"\n  Lead Knight {lead} applies the decision{' (dry run)' if dry else ''}.\n", "bold")
     out = _generate(root, config, lead, prompt, args, ui)
+    if not is_writer():        # SPMD: the other ranks only took part in the lead knight's decode
+        return 0
     edits, warnings = rtdiff.parse(out)
     for w in warnings:
         ui.warn(f"  Warning: {w}")

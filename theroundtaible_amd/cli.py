@@ -24,13 +24,41 @@ from .utils.ui import UI
 _CLUSTER = None   # set when discuss/summon run under torchrun (one process per GPU, SPMD)
 
 
-def spmd_cluster():
-    """The torchrun cluster for SPMD commands (None for a single-process run)."""
+def spmd_cluster(config=None):
+    """The torchrun cluster for SPMD commands (None for a single-process run). A config whose
+    engine knights all run on the CPU gets gloo ranks (tests / CPU plumbing)."""
     global _CLUSTER
     if _CLUSTER is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         from .parallel.cluster import init_cluster
-        _CLUSTER = init_cluster(prefer_gpu=True)
+        cpu = False
+        if config is not None:
+            from .parallel.launch import ranks_needed
+            cpu = ranks_needed(config)[2]
+        _CLUSTER = init_cluster(prefer_gpu=not cpu)
     return _CLUSTER
+
+
+def make_backends(config, ui: UI, args, only_knight: Optional[str] = None):
+    """(backends, factory) for a command. Under torchrun (SPMD, parallel/launch.py self-launch):
+    every rank builds the engines placed on it and one RemoteKnight per adapter id
+    (knights/spmd.py); otherwise in-process engines (one per GPU / model). ``only_knight``: build
+    just that knight's backend (apply's lead knight)."""
+    cl = spmd_cluster(config)
+    if cl is not None and cl.distributed:
+        import copy
+        from .knights.spmd import build_spmd_backends
+        cfg = config
+        if only_knight is not None:
+            cfg = copy.copy(config)
+            cfg.knights = [k for k in config.knights if k.name == only_knight] or config.knights[:1]
+        backends, _pool = build_spmd_backends(cfg, cl, ui, getattr(args, "max_new_tokens", None))
+        return backends, None
+    if only_knight is not None:
+        from .knights.registry import BackendFactory
+        k = next((k for k in config.knights if k.name == only_knight), config.knights[0])
+        b = BackendFactory(config, device_override=getattr(args, "device", None)).create(k.adapter)
+        return ({k.adapter: b} if b is not None else {}), None
+    return _make_backends(config, ui, getattr(args, "device", None))
 
 
 def is_writer() -> bool:
@@ -246,6 +274,12 @@ def cmd_init(args, ui: UI) -> int:
     ui.print(f"    Project:   {project}")
     ui.print(f"    Language:  {language}")
     ui.print(f"    Knights:   {', '.join(k['name'] for k in knights)} ({args.model})")
+    from .config import load_config as _load
+    from .parallel.launch import ranks_needed
+    n, why, _cpu = ranks_needed(_load(root))
+    if n > 1:
+        ui.dim(f"\n  Placement needs {n} GPU ranks ({why}): `roundtable discuss` launches them itself "
+               f"(one process per GPU, torch.distributed over RCCL).")
     ui.dim('\n  The table is set. Run `roundtable discuss "your question"` to begin.\n')
     return 0
 
@@ -280,7 +314,7 @@ def discuss(topic: str, args, ui: UI) -> int:
     from .orchestrator import Orchestrator, RunOptions
     root = os.getcwd()
     config = load_config(root)
-    cl = spmd_cluster()
+    cl = spmd_cluster(config)
     if cl is not None and cl.rank != 0:
         ui = UI(quiet=True)
     ui.print(f'\n  Topic: "{topic}"\n', "bold")
@@ -289,9 +323,7 @@ def discuss(topic: str, args, ui: UI) -> int:
     if cl is not None and cl.distributed:
         # SPMD: every rank runs this program; knights run where they are placed (knights/spmd.py)
         import tempfile
-        from .knights.spmd import build_spmd_backends
-        backends, _pool = build_spmd_backends(config, cl, ui, args.max_new_tokens)
-        factory = None
+        backends, factory = make_backends(config, ui, args)
         if cl.rank != 0:
             store_root = tempfile.mkdtemp(prefix=f"roundtable-rank{cl.rank}-")   # mirror writes, discarded
         if args.seed is None:   # one speaking order for all ranks
@@ -714,9 +746,17 @@ def _update_notice(ui: UI) -> None:
 def main(argv: Optional[List[str]] = None) -> int:
     from .utils.debug import apply_debug_env
     apply_debug_env()          # ROUNDTABLE_DEBUG=1: serialized kernels + paging guards (before any HIP call)
+    raw_argv = list(sys.argv[1:] if argv is None else argv)
     args = build_parser().parse_args(argv)
     ui = UI(quiet=args.quiet)
     try:
+        if args.fn in (cmd_discuss, cmd_summon, cmd_apply, cmd_code_red):
+            # a knight placement with tp > 1 needs one process per GPU: re-run this command as a
+            # child torchrun BEFORE anything touches a GPU (parallel/launch.py)
+            from .parallel.launch import maybe_relaunch
+            rc = maybe_relaunch(raw_argv, quiet=args.quiet)
+            if rc is not None:
+                return rc
         rc = int(args.fn(args, ui) or 0)
         _update_notice(ui)
         return rc

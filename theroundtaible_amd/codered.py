@@ -122,10 +122,13 @@ def append_error_log(root: str, symptoms: str, status: str, key: Optional[str], 
 
 
 def code_red_command(args, ui: UI) -> int:
-    from .cli import _make_backends
+    from .cli import is_writer, make_backends, spmd_cluster
     root = os.getcwd()
     config = load_config(root)
-    backends, _ = _make_backends(config, ui, getattr(args, "device", None))
+    cl = spmd_cluster(config)
+    if cl is not None and cl.rank != 0:
+        ui = UI(quiet=True)
+    backends, _ = make_backends(config, ui, args)
     if not backends:
         raise ConfigError("No doctors available.")
     doctors = [k for k in sorted(config.knights, key=lambda k: k.priority) if k.adapter in backends]
@@ -161,6 +164,8 @@ def code_red_command(args, ui: UI) -> int:
             if key:
                 break
     status = "OPEN" if key else "PARKED"
+    if not is_writer():        # SPMD: rank 0 alone writes the project's error log
+        return 0
     cr = append_error_log(root, symptoms, status, key, list(latest.values()))
     if key:
         ui.ok(f"\n  Diagnosis converged: {key} — logged as {cr} (OPEN until fixed).")

@@ -274,17 +274,21 @@ class Engine:
 
     MAX_SHARED_SEQS = 64   # resident shared prefixes (tables, system prompts); LRU beyond
 
-    def sync_shared(self, key: str, shared: List[int]) -> Tuple[SeqState, List[int]]:
+    def sync_shared(self, key: str, shared: List[int], protect=()) -> Tuple[SeqState, List[int]]:
         """Roll the table's shared sequence back to its LCP with ``shared``; return (seq, delta to
         prefill). The shared sequence is never decoded: it only holds the common KV blocks.
         Least-recently-used shared sequences beyond ``MAX_SHARED_SEQS`` are released (blocks a
-        member still references stay alive through their refcount)."""
+        member still references stay alive through their refcount) — never one of ``protect``
+        (the keys of the batch being set up, whose blocks its members have yet to attach)."""
         sk = self.shared_seq_key(key)
         lru = self.__dict__.setdefault("_shared_lru", {})
         lru.pop(sk, None)
         lru[sk] = None
+        keep = {self.shared_seq_key(k) for k in protect} | {sk}
         while len(lru) > self.MAX_SHARED_SEQS:
-            old = next(iter(lru))
+            old = next((k for k in lru if k not in keep), None)
+            if old is None:
+                break
             del lru[old]
             self.kv.free_seq(old)
         s = self.kv.seq(sk)
@@ -302,6 +306,10 @@ class Engine:
         k = 0
         while k < min(len(s.blocks), nblocks) and s.blocks[k] == shared.blocks[k]:
             k += 1
+        if k == nblocks and s.length >= nblocks * bs:
+            # already holds every shared block (same ids = same K/V): keep the member's own tokens
+            # past the shared region — sync_prefix rolls them back by LCP if they changed
+            return nblocks * bs
         self.kv.truncate(s, min(s.length, k * bs))   # keeps <= k blocks, all shared ones
         for i in range(len(s.blocks), nblocks):
             self.kv.alloc.incref(shared.blocks[i])
@@ -406,7 +414,12 @@ class Engine:
         """Run one turn for each entry (distinct seq_keys), batched; per-turn errors are returned."""
         if not turns:
             return []
-        if not self.healthy and not self._recover():
+        unhealthy = not self.healthy
+        if self.tp.size > 1:
+            # ranks of a TP knight decide together: one rank recovering into the prefill
+            # collectives while another returns errors would hang the first
+            unhealthy = self.tp.any_rank(unhealthy)
+        if unhealthy and not self._recover():
             err = AdapterError("engine", "engine unhealthy after a previous device error", kind="device")
             return [TurnOutput("", [], {}, err) for _ in turns]
         call = self._calls
@@ -425,9 +438,17 @@ class Engine:
             return [TurnOutput("", [], {}, e) for _ in turns]
         except DeviceFlagError as e:
             # a bounded device-side wait expired: this turn's tokens are wrong. Fail the turn,
-            # drop its KV (the knight re-prefills next turn); the engine itself stays usable.
+            # drop its KV (the knight re-prefills next turn) AND every shared-prefix sequence the
+            # call prefilled — its all-reduces may have summed stale data, and sync_shared would
+            # hand that KV to every member of the table by LCP. The engine itself stays usable.
+            lru = self.__dict__.get("_shared_lru", {})
             for t in turns:
                 self.release(t.seq_key)
+                key = getattr(t.prompt, "shared_key", None)
+                if key is not None:
+                    sk = self.shared_seq_key(key)
+                    lru.pop(sk, None)
+                    self.kv.free_seq(sk)
             return [TurnOutput("", [], {}, AdapterError("engine", str(e), kind="device")) for _ in turns]
         except RuntimeError as e:
             msg = str(e)
@@ -442,16 +463,20 @@ class Engine:
         kernel; if it answers, drop every resident sequence and captured graph (their state may
         be stale) and serve again — knights re-prefill from the transcript on their next turn.
         At most ``max_recoveries`` attempts per engine; a dead device stays unhealthy."""
-        if self._recoveries >= self.max_recoveries or self._dead:
-            return False
-        self._recoveries += 1
-        try:
-            if self.on_gpu:
-                torch.cuda.synchronize(self.device)
-            x = torch.ones(64, 64, device=self.device, dtype=torch.float32)
-            if float((x @ x).sum().item()) != 64.0 ** 3:
-                return False
-        except RuntimeError:
+        ok = not (self._recoveries >= self.max_recoveries or self._dead)
+        if ok:
+            self._recoveries += 1
+            try:
+                if self.on_gpu:
+                    torch.cuda.synchronize(self.device)
+                x = torch.ones(64, 64, device=self.device, dtype=torch.float32)
+                ok = float((x @ x).sum().item()) == 64.0 ** 3
+            except RuntimeError:
+                ok = False
+        if self.tp.size > 1:
+            ok = not self.tp.any_rank(not ok)   # the whole group recovers, or none of it
+        if not ok:
+            self.healthy = False
             return False
         for key in list(self.kv.seqs):
             self.kv.free_seq(key)
@@ -508,12 +533,13 @@ class Engine:
         shared: Dict[str, SeqState] = {}
         pre: Dict[str, int] = {}
         items = []
-        for key in dict.fromkeys(k for k in keys if k is not None):
+        batch_keys = [k for k in dict.fromkeys(keys) if k is not None]
+        for key in batch_keys:
             members = [i for i, k in enumerate(keys) if k == key]
             common = enc[members[0]][0][:enc[members[0]][1]]
             for i in members[1:]:
                 common = common[:lcp(common, enc[i][0], enc[i][1])]
-            sq, delta = self.sync_shared(key, common)
+            sq, delta = self.sync_shared(key, common, protect=batch_keys)
             shared[key] = sq
             pre[key] = len(delta)
             if delta:
@@ -575,7 +601,7 @@ class Engine:
                 "shared_tokens": sh_blocks.get(key, 0) * self.kv.block_size if key is not None else 0,
                 "decode_tokens": len(g) - nf, "forced_tokens": nf, "prefill_ms": (t1 - t0) * 1e3,
                 "decode_ms": (t2 - t1) * 1e3, "decode_tok_s": (len(g) - nf) / max(t2 - t1, 1e-9), "batch": len(turns),
-                "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3}))
+                "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3, "tp": self.tp.size}))
         self.stats["prefill_tokens"] += sum(len(d) for d in deltas) + sum(shared_pre.values())
         self.stats["decode_tokens"] += sum(len(g) for g in gen) - sum(forced)
         self.stats["prefill_s"] += t1 - t0

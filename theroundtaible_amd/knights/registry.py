@@ -77,6 +77,14 @@ class BackendFactory:
         ac = self.config.adapter_config.get(adapter_id) or {}
         if isinstance(ac, dict) and wants_external(adapter_id, ac):
             return create_external(adapter_id, ac, name)
+        tp = int(st.get("tp", 1) or 1)
+        if tp > 1:
+            # never silently run a tensor-parallel knight at tp = 1 on its first GPU: the CLI
+            # launches the ranks itself (parallel/launch.py); anything else must run under torchrun
+            from ..errors import ConfigError
+            raise ConfigError(f"{adapter_id}: engine.tp={tp} needs one process per GPU of its group",
+                              hint="Run it through `roundtable discuss/summon/apply/code-red` (they launch the "
+                                   "ranks), or under `torchrun --nproc-per-node N -m theroundtaible_amd ...`.")
         weights = str(st.get("weights", "random:0"))
         model, overrides = resolve_model(st["model"], weights, st.get("model_overrides"))
         ecfg = EngineConfig(model=model, weights=weights,

@@ -82,12 +82,13 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         ekey = (st["model"], str(st.get("weights", "random:0")), str(st.get("dtype", "bf16")), tuple(ranks))
         if ekey not in engines:
             model, overrides = resolve_model(st["model"], str(st.get("weights", "random:0")), st.get("model_overrides"))
+            dev = "cpu" if str(st.get("device", "")) == "cpu" else cluster.device
             ecfg = EngineConfig(model=model, weights=str(st.get("weights", "random:0")),
-                                dtype=str(st.get("dtype", "bf16")), device=cluster.device,
+                                dtype=str(st.get("dtype", "bf16")), device=dev,
                                 block_size=int(st.get("kv_block_size", 32)),
                                 kv_cache_fraction=float(st.get("kv_cache_fraction", 0.85)),
                                 max_kv_tokens=st.get("max_kv_tokens"),
-                                use_graphs=bool(st.get("use_graphs", True)) and cluster.device.startswith("cuda"),
+                                use_graphs=bool(st.get("use_graphs", True)) and dev.startswith("cuda"),
                                 model_overrides=overrides)
             if not ecfg.device.startswith("cuda"):
                 ecfg.dtype = "fp32"

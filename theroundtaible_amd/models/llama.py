@@ -100,15 +100,20 @@ class LlamaModel:
         if self._dec is None:
             with torch.no_grad():
                 layers = []
-                for lw in self.layers:
+                for i, lw in enumerate(self.layers):
                     d = {}
                     for name, norm, kw in self._lin_specs():
                         d[name] = ops.shuffle_weight(lw[name], lw[norm] if norm else None, **kw)
                         if drop_originals:
+                            # drop BOTH references (the per-layer view and the flat dict) now, so the
+                            # allocator reuses this tensor's memory for the next shuffle: the load peak
+                            # stays one weight copy + one tensor
                             lw[name] = None
+                            self.w[f"layers.{i}.{name}"] = None
                     layers.append(d)
                 lm = ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])
                 if drop_originals:
+                    self.w["lm_head"] = None
                     for k in [k for k in self.w if k.startswith("layers.") and k.split(".", 2)[2] in
                               ("wqkv", "wo", "w_gate_up", "w_down")] + ["lm_head"]:
                         self.w[k] = None

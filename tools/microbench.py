@@ -183,9 +183,10 @@ def bench_attn(B, ctx, splits_list):
         row(f"decode attn B={B} ctx={ctx} splits={splits}", timed(fn), nbytes)
 
 
-def bench_attn_grouped(B, shared, private, splits_list):
-    """Shared-prefix groups: B knights read one `shared`-token prefix + `private` own tokens."""
-    hq, hkv, d = 32, 8, 128
+def bench_attn_grouped(B, shared, private, splits_list, hq=32, hkv=8):
+    """Shared-prefix groups: B knights read one `shared`-token prefix + `private` own tokens.
+    ``hq``/``hkv``: per-rank heads (tensor-parallel shards: 32/tp, 8/tp)."""
+    d = 128
     G = hq // hkv
     nsh, npr = shared // 32, (private + 31) // 32
     nblk = nsh + B * npr
@@ -208,7 +209,8 @@ def bench_attn_grouped(B, shared, private, splits_list):
             gt = groups if grouped else None
             fn = lambda i, ws=ws, splits=splits, out=out, gt=gt: ops.paged_attention_decode(
                 q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out, groups=gt)
-            row(f"decode attn {'grouped' if grouped else 'private'} B={B} shared={shared} own={private} splits={splits}",
+            row(f"decode attn {'grouped' if grouped else 'private'} hq={hq} hkv={hkv} B={B} shared={shared} "
+                f"own={private} splits={splits}",
                 timed(fn), nbytes if grouped else nbytes + (B - 1) * nsh * 32 * hkv * d * 4)
 
 
@@ -261,9 +263,10 @@ def main():
         bench_attn(a.batch, a.ctx, [int(s) for s in a.splits.split(",")])
         bench_attn(a.batch, 1500, [4, 8, 11, 16])
     if "gattn" in only:
-        for sp in a.shared.split(","):
-            sh, pr = (int(x) for x in sp.split(":"))
-            bench_attn_grouped(a.batch, sh, pr, [int(s) for s in a.splits.split(",")])
+        for tp in (int(t) for t in a.tp.split(",")):
+            for sp in a.shared.split(","):
+                sh, pr = (int(x) for x in sp.split(":"))
+                bench_attn_grouped(a.batch, sh, pr, [int(s) for s in a.splits.split(",")], 32 // tp, max(1, 8 // tp))
     if "sample" in only:
         bench_sample(a.batch)
     if "prefill" in only:
