@@ -3,8 +3,12 @@ against faked inventories (no GPU needed)."""
 import json
 
 from theroundtaible_amd.cli import main
-from theroundtaible_amd.parallel.placement import (GIB, GpuInfo, Inventory, kv_bytes_per_token, model_bytes,
-                                                   parse_topotype, plan_placement)
+from theroundtaible_amd.parallel.costmodel import split_plans
+from theroundtaible_amd.parallel.placement import (GIB, GpuInfo, Inventory, PlacementPolicy, kv_bytes_per_token,
+                                                   model_bytes, parse_topotype, plan_placement)
+
+PACK = PlacementPolicy(mode="pack")
+SPREAD = PlacementPolicy(mode="spread")
 
 
 def node(n=8, hbm=288):
@@ -19,17 +23,45 @@ def test_model_sizes():
     assert kv_bytes_per_token("llama3-8b") == 128 * 1024 and kv_bytes_per_token("llama3-70b") == 320 * 1024
 
 
-def test_same_model_knights_share_one_gpu():
-    plans = plan_placement([{"name": n, "model": "llama3-8b"} for n in "ABC"], node())
+def test_pack_policy_same_model_knights_share_one_gpu():
+    plans = plan_placement([{"name": n, "model": "llama3-8b"} for n in "ABC"], node(), PACK)
     assert len(plans) == 1 and plans[0].tp == 1 and plans[0].gpus == [0] and plans[0].knights == ["A", "B", "C"]
 
 
-def test_70b_tp_by_latency_target_and_by_memory():
-    p = plan_placement([{"name": n, "model": "llama3-70b"} for n in "AB"], node())
-    assert p[0].tp == 4 and p[0].gpus == [0, 1, 2, 3] and p[0].step_ms < 8      # config 5: TP=4
+def test_pack_policy_70b_tp_by_latency_target_and_by_memory():
+    p = plan_placement([{"name": n, "model": "llama3-70b"} for n in "AB"], node(), PACK)
+    assert p[0].tp == 4 and p[0].gpus == [0, 1, 2, 3] and p[0].step_ms < 8
+    assert plan_placement([{"name": "A", "model": "llama3-70b"}], node(1), PACK)[0].tp == 1   # fits alone
+    small = plan_placement([{"name": "A", "model": "llama3-70b"}], node(4, hbm=64), PACK)
+    assert small[0].tp == 4 and small[0].reason == "memory fit"
+
+
+def test_auto_lone_8b_table_gets_tensor_parallel_from_the_model():
+    """a lone 3 x Llama-3-8B table on an 8-GPU node must not idle 7 GPUs — the
+    cost model's fastest layout (one batched tp engine) is what the planner returns."""
+    plans = plan_placement([{"name": n, "model": "llama3-8b"} for n in "ABC"], node())
+    best_ms, best = split_plans("llama3-8b", 3, 8)[0]
+    assert [(len(p.knights), p.tp) for p in plans] == best and plans[0].tp > 1
+    assert abs(sum(p.round_ms for p in plans[:1]) - best_ms) < 1.0
+    assert sorted(g for p in plans for g in p.gpus) == list(range(sum(p.tp for p in plans)))
+
+
+def test_spread_config3_mistral_one_per_gpu_and_config5_70b_tp4_each():
+    """BASELINE config 3 (8 Mistral knights one-per-GPU) and config 5 (2 x Llama-3-70B, TP=4 each,
+    disjoint groups) under the ``spread`` policy."""
+    p3 = plan_placement([{"name": f"M{i}", "model": "mistral-7b"} for i in range(8)], node(), SPREAD)
+    assert [(p.tp, p.gpus, p.knights) for p in p3] == [(1, [i], [f"M{i}"]) for i in range(8)]
+    p5 = plan_placement([{"name": n, "model": "llama3-70b"} for n in "AB"], node(), SPREAD)
+    assert [(p.tp, p.gpus) for p in p5] == [(4, [0, 1, 2, 3]), (4, [4, 5, 6, 7])]
+
+
+def test_auto_memory_fit_and_sequential_mode():
     assert plan_placement([{"name": "A", "model": "llama3-70b"}], node(1))[0].tp == 1   # one GPU: fits alone
     small = plan_placement([{"name": "A", "model": "llama3-70b"}], node(4, hbm=64))
-    assert small[0].tp == 4 and small[0].reason == "memory fit"
+    assert small[0].tp == 4                                                               # memory forces tp 4
+    seq = plan_placement([{"name": n, "model": "llama3-8b"} for n in "ABC"], node(),
+                         PlacementPolicy(round_mode="sequential"))
+    assert sum(p.tp for p in seq) <= 8 and max(p.tp for p in seq) > 1
 
 
 def test_heterogeneous_models_get_disjoint_groups_then_share():
@@ -53,11 +85,13 @@ def test_init_writes_automatic_placement(project, monkeypatch):
     monkeypatch.setenv("ROUNDTABLE_FAKE_GPUS", json.dumps(node().to_json()))
     assert main(["--quiet", "init", "--yes", "--model", "llama3-70b", "--knights", "2"]) == 0
     cfg = json.load(open(project / ".roundtable" / "config.json"))
+    best = split_plans("llama3-70b", 2, 8)[0][1]          # the cost model's layout (auto policy)
+    assert best == [(2, 8)]
     for aid in ("claude-cli", "gemini-cli"):
         eng = cfg["adapter_config"][aid]["engine"]
-        assert eng["tp"] == 4 and eng["gpus"] == [0, 1, 2, 3]
+        assert eng["tp"] == 8 and eng["gpus"] == list(range(8))
     grp = cfg["engine"]["placement"]["groups"]
-    assert grp[0]["model"] == "llama3-70b" and grp[0]["tp"] == 4
+    assert grp[0]["model"] == "llama3-70b" and grp[0]["tp"] == 8 and grp[0]["round_ms"] > 0
     assert len(cfg["engine"]["placement"]["inventory"]["gpus"]) == 8
 
 

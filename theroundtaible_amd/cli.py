@@ -237,8 +237,10 @@ def cmd_init(args, ui: UI) -> int:
         # automatic placement: tp by memory fit + decode-step target, same-model knights together
         from .parallel.placement import plan_placement
         seats = [{"name": k["adapter"], **local_engine.get(k["adapter"], {"model": args.model})} for k in knights]
+        from .parallel.placement import PlacementPolicy
         plans = plan_placement([{"name": s_["name"], "model": s_["model"], "overrides": s_.get("model_overrides")}
-                                for s_ in seats], inv)
+                                for s_ in seats], inv,
+                               PlacementPolicy(mode=getattr(args, "placement", None) or "auto"))
         for pl in plans:
             for aid in pl.knights:
                 adapter_engine[aid] = dict(local_engine.get(aid, {"model": args.model}), tp=pl.tp, gpus=pl.gpus)
@@ -246,7 +248,7 @@ def cmd_init(args, ui: UI) -> int:
                   f"(tp={pl.tp}, {pl.weight_gib_per_gpu} GiB weights/GPU, ~{pl.step_ms} ms/step: {pl.reason})")
         placement = {"inventory": inv.to_json(),
                      "groups": [{"model": pl.model, "tp": pl.tp, "gpus": pl.gpus, "adapters": pl.knights,
-                                 "reason": pl.reason} for pl in plans]}
+                                 "reason": pl.reason, "round_ms": pl.round_ms} for pl in plans]}
     eng_top = {"default_model": args.model, "weights": args.weights, "dtype": "bf16",
                "max_new_tokens": args.max_new_tokens}
     if placement is not None:
@@ -670,6 +672,9 @@ def build_parser() -> argparse.ArgumentParser:
     i.add_argument("--knights", type=int, default=3)
     i.add_argument("--tp", type=int, default=None,
                    help="tensor-parallel degree for every knight (default: automatic placement from the GPU scout)")
+    i.add_argument("--placement", choices=["auto", "spread", "pack"], default="auto",
+                   help="automatic placement policy: auto = measured cost model (fastest predicted round), "
+                        "spread = one knight per GPU group, pack = same-model knights on one group")
     i.add_argument("--max-new-tokens", type=int, default=512)
     i.add_argument("--local-models", action="store_true",
                    help="seat every detected local checkpoint (ROUNDTABLE_MODELS_DIR, ./models, HF cache)")

@@ -6,16 +6,21 @@ local seats). The MI355X equivalent scouts GPUs instead of CLIs:
   so the CLI process itself never initializes HIP: per GPU the name / gfx arch, HBM total and
   free, CU count; plus the link matrix between GPUs from ``rocm-smi --showtopotype`` (XGMI on an
   MI355X node: every pair one hop, 7 links x ~153 GB/s per GPU).
-* :func:`plan_placement` chooses each model's tensor-parallel degree and GPU group:
-  - memory fit: weights/tp + a KV reserve (``kv_reserve_frac`` of HBM, at least room for every
-    knight of the model at ``ctx_tokens``) must fit ``usable_frac`` of HBM;
-  - decode latency: while GPUs are free, tp doubles until weights/tp streamed at ``hbm_tbps``
-    take <= ``step_ms_target`` per token (Llama-3-70B: 141 GB / 6 TB/s = 23.5 ms at tp=1 -> tp=4,
-    5.9 ms; Llama-3-8B: 2.7 ms -> tp=1); tp must divide the KV / query heads and the FFN;
-  - knights of the same model are placed TOGETHER on one GPU group (one engine: batched decode
-    + the ``shared`` prompt layout's single prefix KV copy);
-  - different models get disjoint GPU groups while GPUs last, then share (the engines split that
-    GPU's KV pool and run on their own HIP streams).
+* :func:`plan_placement` seats the knights on GPU groups. Policy ``mode``:
+  - ``auto`` (default): a measured wall-clock model (parallel/costmodel.py:
+    per-kernel floors + weight / KV streams calibrated on MI355X, K9 all-reduce latency per
+    layer, prefill FLOPs) predicts each candidate's round time — same-model knights batched on
+    one tp-N engine, or split into equal groups, for every tp the shapes and memory allow — and
+    the GPUs go where the slowest group gains most (several models: the bottleneck model gets
+    the next GPUs). A lone 3-knight Llama-3-8B table on 8 GPUs gets tp > 1;
+  - ``spread``: one knight per GPU group (BASELINE configs 2/3/5 wording: "one knight per
+    MI355X", "one-per-GPU", "TP=4 each"): tp = the largest allowed power of two with
+    knights x tp <= GPUs;
+  - ``pack``: round-1 policy — memory fit, then tp doubles while weights/tp streamed at
+    ``hbm_tbps`` exceed ``step_ms_target``; same-model knights together.
+  Memory fit everywhere: weights/tp + a KV reserve (``kv_reserve_frac`` of HBM, at least room
+  for every knight of the group at ``ctx_tokens``) must fit ``usable_frac`` of HBM; tp must
+  split the query heads and FFN, and split or replicate the KV heads.
 """
 from __future__ import annotations
 
@@ -148,7 +153,12 @@ class PlacementPolicy:
     kv_reserve_frac: float = 0.3    # KV headroom kept per GPU group beyond the weights
     ctx_tokens: int = 65536         # per-knight context the KV reserve must hold at least
     hbm_tbps: float = 6.0           # sustained weight-stream bandwidth (measured 5.8-6.8 TB/s)
-    step_ms_target: float = 8.0     # decode step (weights streamed once) target when GPUs allow
+    step_ms_target: float = 8.0     # pack mode: decode step (weights streamed once) target
+    mode: str = "auto"              # auto (cost model) | spread (one knight per group) | pack
+    round_mode: str = "parallel"    # the discussion's round mode (sequential = reference semantics)
+    new_tokens: int = 512           # cost model workload: decode tokens per knight turn
+    prefill_tokens: int = 2000      # new prompt tokens per knight turn
+    round_ctx: int = 20000          # resident transcript per knight
 
 
 @dataclass
@@ -160,6 +170,7 @@ class GroupPlan:
     weight_gib_per_gpu: float
     step_ms: float
     reason: str
+    round_ms: float = 0.0            # cost model prediction (auto / spread)
 
 
 def _tp_ok(model: str, overrides: Optional[dict], tp: int) -> bool:
@@ -168,10 +179,97 @@ def _tp_ok(model: str, overrides: Optional[dict], tp: int) -> bool:
     return ((c.n_kv_heads % tp == 0 or tp % c.n_kv_heads == 0) and c.n_heads % tp == 0 and c.ffn % tp == 0)
 
 
+def _fits(pol: PlacementPolicy, hbm: int, model: str, ov: Optional[dict], knights: int, tp: int) -> bool:
+    w, kvtok = model_bytes(model, ov), kv_bytes_per_token(model, ov)
+    return w / tp + max(pol.kv_reserve_frac * hbm, knights * pol.ctx_tokens * kvtok / tp) <= pol.usable_frac * hbm
+
+
 def plan_placement(knights: Sequence[dict], inv: Inventory, policy: Optional[PlacementPolicy] = None) -> List[GroupPlan]:
-    """``knights``: [{"name", "model", "overrides"?}] in seat order. Returns one GroupPlan per model
-    (its knights share one engine on one GPU group); every knight appears in exactly one plan."""
+    """``knights``: [{"name", "model", "overrides"?}] in seat order. Returns GroupPlans (one engine
+    each: its knights batch into one decode on its GPU group); every knight appears in exactly
+    one plan."""
     pol = policy or PlacementPolicy()
+    if pol.mode in ("auto", "spread") and inv.gpus:
+        plans = _plan_modelled(knights, inv, pol)
+        if plans is not None:
+            return plans
+    return _plan_pack(knights, inv, pol)
+
+
+def _plan_modelled(knights: Sequence[dict], inv: Inventory, pol: PlacementPolicy) -> Optional[List[GroupPlan]]:
+    """auto / spread placement from the cost model; None when the models cannot each get their
+    own GPUs (more models than GPUs: the pack policy shares GPUs between engines)."""
+    from .costmodel import round_estimate, tp_candidates
+    from ..models.config import get_config
+    n = len(inv.gpus)
+    hbm = min(g.hbm_bytes for g in inv.gpus) or 288 * GIB
+    by_model: Dict[str, List[dict]] = {}
+    for k in knights:
+        by_model.setdefault(k["model"], []).append(k)
+    kw = dict(new_tokens=pol.new_tokens, prefill_tokens=pol.prefill_tokens, ctx=pol.round_ctx,
+              round_mode=pol.round_mode)
+
+    def groups_ms(m: str, layout: List[tuple]) -> float:
+        ov = by_model[m][0].get("overrides")
+        per = [round_estimate(m, t, k, overrides=ov, **kw).round_ms for k, t in layout]
+        return sum(per) if pol.round_mode == "sequential" else max(per)
+
+    def options(m: str, budget: int) -> List[tuple]:
+        """(ms, layout) of every equal split of the model's knights into g groups x tp <= budget."""
+        ov = by_model[m][0].get("overrides")
+        cfg = get_config(m, **(ov or {}))
+        nk = len(by_model[m])
+        out = []
+        gs = [nk] if pol.mode == "spread" else range(1, nk + 1)
+        for g in gs:
+            sizes = [nk // g + (1 if i < nk % g else 0) for i in range(g)]
+            for t in tp_candidates(cfg, budget):
+                if g * t <= budget and all(_fits(pol, hbm, m, ov, s_, t) for s_ in sizes):
+                    layout = [(s_, t) for s_ in sizes]
+                    out.append((groups_ms(m, layout), layout))
+        if pol.mode == "spread" and out:       # one knight per group: the widest tp that fits
+            out = [max(out, key=lambda o: (o[1][0][1], -o[0]))]
+        out.sort(key=lambda o: (o[0], sum(t for _, t in o[1])))
+        return out
+
+    order = sorted(by_model, key=lambda m: -model_bytes(m, by_model[m][0].get("overrides")))
+    # 1. every model at its cheapest-in-GPUs feasible layout
+    state: Dict[str, tuple] = {}
+    for m in order:
+        opts = options(m, n)
+        if not opts:
+            return None
+        state[m] = min(opts, key=lambda o: (sum(t for _, t in o[1]), o[0]))
+    if sum(sum(t for _, t in state[m][1]) for m in order) > n:
+        return None
+    # 2. GPUs to the bottleneck model while its predicted round shrinks
+    while True:
+        used = sum(sum(t for _, t in state[m][1]) for m in order)
+        m = max(order, key=lambda x: state[x][0])
+        mine = sum(t for _, t in state[m][1])
+        better = [o for o in options(m, n - used + mine) if o[0] < state[m][0] * 0.98]
+        if not better:
+            break
+        state[m] = better[0]
+    plans: List[GroupPlan] = []
+    nxt = 0
+    for m in order:
+        ov = by_model[m][0].get("overrides")
+        names = [k["name"] for k in by_model[m]]
+        ms, layout = state[m]
+        w = model_bytes(m, ov)
+        for k, t in layout:
+            est = round_estimate(m, t, k, overrides=ov, **kw)
+            why = (f"cost model: {est.round_ms:.0f} ms/round predicted ({pol.round_mode})" if pol.mode == "auto"
+                   else f"one knight per group, widest tp ({est.round_ms:.0f} ms/round predicted)")
+            plans.append(GroupPlan(m, t, list(range(nxt, nxt + t)), names[:k], round(w / t / GIB, 1),
+                                   round(est.step_us / 1e3, 2), why, round(est.round_ms, 1)))
+            names = names[k:]
+            nxt += t
+    return plans
+
+
+def _plan_pack(knights: Sequence[dict], inv: Inventory, pol: PlacementPolicy) -> List[GroupPlan]:
     n = len(inv.gpus)
     by_model: Dict[str, List[dict]] = {}
     for k in knights:
