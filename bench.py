@@ -297,7 +297,8 @@ def main() -> int:
                    "simulated_tp": sim or None,
                    "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),
                    "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
-                   "exchange_ms_per_round": round(exch, 3), "engine_load_s": round(load_s, 2),
+                   "exchange_ms_per_round": round(exch, 3), "c1_skipped_batches": getattr(pool, "c1_skipped", 0),
+                   "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
                    "kv_blocks_used_rank0": engine.kv.num_blocks - engine.kv.alloc.num_free,
                    "kv_capacity_tokens": engine.kv_capacity_tokens,

@@ -93,6 +93,7 @@ struct AttnArgs {
   const int* groups = nullptr;
   int slot_stride = 0;         // partial slots per (sequence, head) >= n * num_splits; 0 = num_splits
   int probe = 0;               // latency probe (microbench only, RT_ATTN_PROBE): stop after phase k
+  int ext_combine = 0;         // 1: leave every partial for decode_combine_kernel (no in-launch combine)
 };
 
 // GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
@@ -341,6 +342,10 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
     __syncthreads();  // LDS is reused by the caller's next item
     return true;
   }
+  if (P.ext_combine) {  // many slots: a separate, CU-parallel combine launch reads the partials
+    __syncthreads();
+    return false;
+  }
 
   // ---- split-KV combine inside the launch (MI355X_MICROARCH "Valid forms", row 1): every
   // partial is stored sc1 and drained (vmcnt(0)) by each storing wave before the barrier;
@@ -367,15 +372,28 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
 
   // One thread per output element (member head row, 4 dims); the RL = D/4 threads of a row are
   // consecutive lanes. Per chunk of RL slots each lane loads ONE slot's (m, l) (shared with the
-  // row's other lanes by shuffles, not re-loaded by each) and its 4 dims of all RL partial O's:
-  // one round trip for up to RL slots (a group of 3 at 8 splits has 24), and the single
-  // combining CU moves half the bytes of a per-element (m, l) load.
+  // row's other lanes by shuffles, not re-loaded by each) and its 4 dims of all RL partial O's.
+  // The rows of the members being combined use nitems = nm * G * RL threads; the workgroup's
+  // other threads are not idle: Q = blockDim / nitems thread groups take interleaved slot chunks
+  // (chunk c -> group c % Q) and merge their (m, l, O) states through LDS, so a member with many
+  // slots (small KV-head shards of a tensor-parallel knight: 3 knights x 64 splits = 192 slots)
+  // needs ceil(nslots / (Q * RL)) dependent round trips instead of ceil(nslots / RL).
   constexpr int RL = D / 4;
+  constexpr int SCR = W * GM * (D + 4);   // floats of s_o, reused as the merge scratch
   const int per_m = G * RL;
   const int nm = __popc(mask);
+  const int nitems = nm * per_m;          // <= ncol * RL <= blockDim
+  int Q = (int)blockDim.x / nitems;
+  if (Q > 1 + SCR / (6 * nitems)) Q = 1 + SCR / (6 * nitems);
+  Q = Q < 1 ? 1 : (1 << (31 - __clz(Q)));
+  const int grp = threadIdx.x / nitems;
+  const int it = threadIdx.x - grp * nitems;
   const int lr = threadIdx.x & (RL - 1);
   const int lane0 = (threadIdx.x & 63) & ~(RL - 1);
-  for (int it = threadIdx.x; it < nm * per_m; it += blockDim.x) {   // rows are all-or-nothing
+  float4_ O = {0.f, 0.f, 0.f, 0.f};
+  float Mr = -INFINITY, Lr = 0.f;
+  int row = 0, d0 = 0;
+  if (grp < Q) {
     const int k = it / per_m;
     int mm = 0;
     for (int bits = mask, c = 0;; bits &= bits - 1) {   // k-th member set in the mask
@@ -383,11 +401,10 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       if (c++ == k) break;
     }
     const int w = it - k * per_m;
-    const int hj = w / RL, d0 = 4 * (w - hj * RL);
-    const int row = mm * Hq + hj;
-    float4_ O = {0.f, 0.f, 0.f, 0.f};
-    float Mr = -INFINITY, Lr = 0.f;
-    for (int s0 = 0; s0 < nslots; s0 += RL) {
+    const int hj = w / RL;
+    d0 = 4 * (w - hj * RL);
+    row = mm * Hq + hj;
+    for (int s0 = grp * RL; s0 < nslots; s0 += Q * RL) {
       const bool mine = s0 + lr < nslots;
       const float4_ mlq = mine ? rt::sc1_load4(pml_rsrc, (row * stride + s0 + lr) * 16)
                                : float4_{-INFINITY, 0.f, 0.f, 0.f};
@@ -415,6 +432,29 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       }
       Mr = Mc;
     }
+  }
+  if (Q > 1) {   // merge the Q groups' states in group order (deterministic), group 0 stores
+    float* scr = &S.s_o[0][0][0];
+    __syncthreads();
+    if (grp >= 1 && grp < Q) {
+      float* e = scr + ((grp - 1) * nitems + it) * 6;
+      e[0] = O[0]; e[1] = O[1]; e[2] = O[2]; e[3] = O[3]; e[4] = Mr; e[5] = Lr;
+    }
+    __syncthreads();
+    if (grp == 0) {
+      for (int q2 = 1; q2 < Q; ++q2) {
+        const float* e = scr + ((q2 - 1) * nitems + it) * 6;
+        const float Me = e[4];
+        if (Me == -INFINITY || e[5] <= 0.f) continue;
+        const float Mc = fmaxf(Mr, Me);
+        const float a = Mr == -INFINITY ? 0.f : exp2f(Mr - Mc), f = exp2f(Me - Mc);
+        O = O * a + f * float4_{e[0], e[1], e[2], e[3]};
+        Lr = Lr * a + f * e[5];
+        Mr = Mc;
+      }
+    }
+  }
+  if (grp == 0) {
     const float inv = Lr > 0.f ? 1.f / Lr : 0.f;
     store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
   }

@@ -79,8 +79,9 @@ def test_rope_and_cache(hq, hkv, d, rope):
     close(vc, vc2.to(DEV), 0.0)
 
 
-@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 2, 128)])
-@pytest.mark.parametrize("splits", [1, 3, 8])
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 2, 128), (4, 1, 128),
+                                      (8, 1, 128)])
+@pytest.mark.parametrize("splits", [1, 3, 8, 64])
 def test_paged_decode(hq, hkv, d, splits):
     lens = [1, 31, 32, 33, 257, 1500]
     B = len(lens)
@@ -108,8 +109,8 @@ def test_paged_decode(hq, hkv, d, splits):
     assert int(ws.counters.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64)])
-@pytest.mark.parametrize("splits", [1, 3, 10])
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64), (4, 1, 128)])
+@pytest.mark.parametrize("splits", [1, 3, 10, 64])
 @pytest.mark.parametrize("layout", ["table3", "mixed"])
 def test_paged_decode_shared_prefix_groups(hq, hkv, d, splits, layout):
     """Knights sharing a KV prefix (same leading block ids) decode it once per group: the

@@ -61,6 +61,14 @@ class DistributedPool:
             outs = first.execute_group([(self.local[pairs[i][0].knight_name], pairs[i][1]) for i in idxs], timeout_s)
             for i, o in zip(idxs, outs):
                 local_res[i] = o
+        if len(mine_idx) == len(pairs) and all(len(self.placement[k.knight_name]) == self.cluster.world
+                                               for k, _ in pairs):
+            # every knight of the batch spans EVERY rank (one tensor-parallel group: the strong-
+            # scaling layout): each rank already holds every result, identical across the group
+            # (same sampled ids from the same gathered logits) — no C1 round is needed
+            self.exchange_ms.append(0.0)
+            self.c1_skipped = getattr(self, "c1_skipped", 0) + 1
+            return [local_res[i] for i in range(len(pairs))]
         # contributions from the knights this rank leads
         led = [i for i in mine_idx if self.leader(pairs[i][0].knight_name) == rank]
         t0 = time.perf_counter()
