@@ -25,7 +25,12 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
                    int max_blocks, float scale, hipStream_t stream);
 int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
                   const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
-                  const int64_t* offsets, float* ws, hipStream_t stream);
+                  const int64_t* offsets, float* ws, hipStream_t stream, const void* advance);
+int launch_sample_advance(int64_t* tok, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
+                          const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
+                          int64_t* offsets, float* ws, int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens,
+                          int64_t* step, int max_steps, int64_t* slots, void* res, const int* block_tables,
+                          const void* embed, int max_blocks, int BS, int H, int64_t vocab, hipStream_t stream);
 int sample_workspace_floats(int B);
 
 int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int M, int N, int K, int ldo, float eps,
@@ -237,9 +242,55 @@ void sample(torch::Tensor out, torch::Tensor logits, torch::Tensor temperature, 
                   seeds.numel() >= B && offsets.numel() >= B,
               "sampling parameter vectors shorter than the batch");
   TORCH_CHECK(ws.numel() >= sample_workspace_floats((int)B), "sample workspace too small");
-  launch_sample(out.data_ptr<int64_t>(), logits.data_ptr(), bf, (int)B, (int)logits.size(1), logits.stride(0),
-                temperature.data_ptr<float>(), top_p.data_ptr<float>(), top_k.data_ptr<int>(),
-                seeds.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), ws.data_ptr<float>(), cur_stream());
+  const int rc = launch_sample(out.data_ptr<int64_t>(), logits.data_ptr(), bf, (int)B, (int)logits.size(1),
+                               logits.stride(0), temperature.data_ptr<float>(), top_p.data_ptr<float>(),
+                               top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(),
+                               ws.data_ptr<float>(), cur_stream(), nullptr);
+  TORCH_CHECK(rc == 0, "sample: rc=", rc);
+}
+
+// The captured decode step's sampler fused with decode_advance + next-step decode_prep (one launch).
+// `offsets` is read as the sampler's RNG offsets AND rewritten with the next step's.
+void sample_advance(torch::Tensor tok, torch::Tensor logits, torch::Tensor temperature, torch::Tensor top_p,
+                    torch::Tensor top_k, torch::Tensor seeds, torch::Tensor offsets, torch::Tensor ws,
+                    torch::Tensor out, torch::Tensor ids, torch::Tensor positions, torch::Tensor ctx_lens,
+                    torch::Tensor step, torch::Tensor slots, torch::Tensor res, torch::Tensor block_tables,
+                    torch::Tensor embed, int64_t block_size) {
+  check_type(tok, torch::kInt64, "tok");
+  check_type(ws, torch::kFloat32, "sample workspace");
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V] row-major");
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "logits must be bf16 or fp32");
+  const int64_t B = logits.size(0);
+  check_type(temperature, torch::kFloat32, "temperature");
+  check_type(top_p, torch::kFloat32, "top_p");
+  check_type(top_k, torch::kInt32, "top_k");
+  check_type(seeds, torch::kInt64, "seeds");
+  check_type(offsets, torch::kInt64, "offsets");
+  check_type(out, torch::kInt64, "out");
+  check_type(ids, torch::kInt64, "ids");
+  check_type(positions, torch::kInt64, "positions");
+  check_type(ctx_lens, torch::kInt32, "ctx_lens");
+  check_type(step, torch::kInt64, "step");
+  check_type(slots, torch::kInt64, "slots");
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_bf16(res, "res");
+  check_bf16(embed, "embed");
+  TORCH_CHECK(tok.numel() >= B && temperature.numel() >= B && top_p.numel() >= B && top_k.numel() >= B &&
+                  seeds.numel() >= B && offsets.numel() >= B && ids.numel() == B && positions.numel() == B &&
+                  ctx_lens.numel() == B && slots.numel() >= B && out.dim() == 2 && out.size(1) == B &&
+                  block_tables.size(0) >= B && res.dim() == 2 && res.size(0) == B && embed.dim() == 2 &&
+                  res.size(1) == embed.size(1) && block_size > 0,
+              "sample_advance: shapes");
+  TORCH_CHECK(ws.numel() >= sample_workspace_floats((int)B), "sample workspace too small");
+  const int rc = launch_sample_advance(
+      tok.data_ptr<int64_t>(), logits.data_ptr(), bf, (int)B, (int)logits.size(1), logits.stride(0),
+      temperature.data_ptr<float>(), top_p.data_ptr<float>(), top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(),
+      offsets.data_ptr<int64_t>(), ws.data_ptr<float>(), out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(),
+      positions.data_ptr<int64_t>(), ctx_lens.data_ptr<int>(), step.data_ptr<int64_t>(), (int)out.size(0),
+      slots.data_ptr<int64_t>(), res.data_ptr(), block_tables.data_ptr<int>(), embed.data_ptr(),
+      (int)block_tables.size(1), (int)block_size, (int)embed.size(1), embed.size(0), cur_stream());
+  TORCH_CHECK(rc == 0, "sample_advance: rc=", rc);
 }
 // Ws: fragment-shuffled weight [N_w, K] (N_w = 2N for SwiGLU); out [M, N] (unused for RESID).
 // PRO_NORM_ADD (pro=2): x2 [M,K] is added to x before the norm; xout (optional) receives x + x2.
@@ -553,6 +604,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_and_mul", &silu_and_mul);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("sample", &sample);
+  m.def("sample_advance", &sample_advance);
   m.def("sample_workspace_floats", &sample_workspace_floats);
   m.attr("arch") = "gfx950";
 }

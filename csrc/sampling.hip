@@ -1,55 +1,49 @@
-// K6: fused sampler — greedy / temperature / top-k / top-p, graph-safe RNG, multi-CU.
+// K6: fused sampler — greedy / temperature / top-k / top-p, graph-safe RNG — and, in the
+// captured decode step, the step's bookkeeping, in ONE launch (r02: six sampler launches +
+// decode_advance = 47 us per step, profiles/r03/prof8.md).
 //
 // Sampling is Gumbel-max: token = argmax(z_i + g_i) over the allowed set, z = (logit - max)/T,
 // g_i = -log(-log(u_i)), u_i a counter-based hash of (seed, offset, i): no RNG state, so a
 // captured hipGraph replays deterministically and a knight's stream depends only on
 // (seed, knight, position) (the engine passes each row's token position as `offset`).
 //
-// Each row is split into C chunks handled by C workgroups (a single workgroup per row is
-// LDS-atomic-bound: 2 x 128K histogram atomics on one CU), in six graph-capturable launches:
-//   1 stats  : per-chunk max/argmax, and the chunk's best Gumbel score over ALL tokens (B x C)
-//   2 accept : fast path. j* = argmax(z + g) over the whole vocabulary is the nucleus sample
-//              whenever j* lies in the nucleus, i.e. when the mass of the tokens strictly more
-//              likely than j* is below p * total (then the argmax over the nucleus is j*).
-//              j* is itself a softmax draw, so that holds with probability >= top_p (95 % at
-//              top_p 0.95). One pass sums both masses; the last-arriving chunk decides, writes
-//              the token and raises the row's `done` flag. Greedy and unfiltered rows finish
-//              here too; launches 3-6 return at once for a done row.  (grid B x C)
-//   3 hist   : coarse 2048-bin histogram of z over [-ZR, 0] (count + probability mass),
-//              chunk-local in LDS then merged with one global atomic per non-empty bin
-//   4 select : per row, block-scan the histogram -> the bin where top-k (count) or top-p
-//              (mass) crosses                                          (grid B)
-//   5 refine : 2048-bin sub-histogram of that one bin                 (grid B x C)
-//   6 final  : threshold from the sub-histogram, Gumbel-argmax over the chunk, then the
-//              last-arriving chunk of each row reduces the partials   (grid B x C)
-// Threshold resolution ZR/4M ~ 7e-6 in z; every pass uses 16-byte vector loads (G13).
+// Grid (B, C): C workgroups per row stream one chunk each (chunk max / argmax, and the chunk's
+// best Gumbel score over ALL its tokens), publish those 4 words write-through, and take a
+// ticket; the row's LAST-arriving workgroup (the "decider", MI355X_MICROARCH sc1 hand-off
+// table row 1) finishes the row alone:
+//   * greedy / unfiltered rows: reduce the C chunk records;
+//   * top-p rows, fast path: j* = argmax(z + g) over the whole vocabulary is the nucleus sample
+//     whenever the mass of the tokens strictly more likely than j* is below p * total (then the
+//     argmax over the nucleus is j*); j* is itself a softmax draw, so that holds with
+//     probability >= top_p. One pass of the decider over the row sums both masses;
+//   * otherwise (top-k, or a rejected j*): a 2048-bin histogram of z in LDS (count + mass) ->
+//     the crossing bin -> a 2048-bin sub-histogram of that bin -> threshold -> Gumbel argmax over
+//     the allowed set, all by the decider (coarse bins over the row's own z range, at most
+//     [-ZR, 0]; threshold resolution range / 4M <= 7e-6 in z).
+// The decider then writes the token and, with bookkeeping on (sample_advance), the decode_advance
+// + decode_prep work of its row (out[step, b], ids, positions, lengths, next K/V slot, sampler
+// offset, embedding row); the last decider of the launch bumps `step`. Every counter re-arms
+// itself, so the workspace is zeroed once (ops.sample_workspace) and replays need no memset.
 // Bit-for-bit RNG twin: theroundtaible_amd/ops/reference.py::uniform_tensor.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 constexpr int NB = 2048;
-constexpr int NT = 256;
+constexpr int NT = 512;     // threads per workgroup
+constexpr int NWV = NT / 64;
 constexpr int C = 32;       // chunks (workgroups) per row
 constexpr float ZR = 30.f;  // exp(-30) * 128K < 1e-8 of the mass: ignored
 
-// per-row workspace layout (floats / ints interchangeable, 4 bytes each)
+// per-row workspace (4-byte words, floats / ints interchangeable)
 constexpr int W_MAX = 0;                 // [C] chunk max
 constexpr int W_ARG = W_MAX + C;         // [C] chunk argmax (int)
 constexpr int W_GV = W_ARG + C;          // [C] chunk best Gumbel score v/T + g
 constexpr int W_GI = W_GV + C;           // [C] its token (int)
-// [W_HC, W_ROW) is zeroed by launch 1 (its chunks write only the words above)
-constexpr int W_HC = W_GI + C;           // [NB] coarse count
-constexpr int W_HM = W_HC + NB;          // [NB] coarse mass
-constexpr int W_SC = W_HM + NB;          // [NB] sub count
-constexpr int W_SM = W_SC + NB;          // [NB] sub mass
-constexpr int W_SEL = W_SM + NB;         // bsel(int), by_count(int), need(float), row max(float)
-constexpr int W_PV = W_SEL + 4;          // [C] partial score
-constexpr int W_PI = W_PV + C;           // [C] partial index (int)
-constexpr int W_CNT = W_PI + C;          // arrival counter (int)
-constexpr int W_DONE = W_CNT + 1;        // row sampled by the accept pass (int)
-constexpr int W_CNT2 = W_CNT + 2;        // accept-pass arrival counter (int)
-constexpr int W_SUM = W_CNT + 4;         // mass above j*, total mass (accept-pass accumulators)
-constexpr int W_ROW = W_SUM + 4;         // floats per row
+constexpr int W_MIN = W_GI + C;          // [C] chunk min
+constexpr int W_CNT = W_MIN + C;         // arrival ticket (int), re-armed by the decider
+constexpr int W_ROW = W_CNT + 4;         // words per row; after the B rows: the rows-done ticket
 
 RT_DEVICE uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -63,9 +57,9 @@ RT_DEVICE float gumbel(uint64_t key, uint32_t i) {
   return -__logf(-__logf(u));
 }
 
+// f(i, v) over [lo, hi) of a row, NT-strided, 16-byte loads when aligned (lo % 8 == 0)
 template <typename T, bool VEC, typename F>
-RT_DEVICE void for_chunk(const T* row, int lo, int hi, F&& f) {
-  // lo is a multiple of 8 (chunk boundaries are), so the vector path stays aligned
+RT_DEVICE void for_range(const T* row, int lo, int hi, F&& f) {
   if constexpr (VEC && sizeof(T) == 2) {
     const int nv = (hi - lo) >> 3;
     const rt::short8* p = reinterpret_cast<const rt::short8*>(row + lo);
@@ -91,6 +85,36 @@ RT_DEVICE void for_chunk(const T* row, int lo, int hi, F&& f) {
   }
 }
 
+// f(i, v) over a whole row [0, V): the decider's passes stream 256 KB on ONE CU, so every lane
+// keeps UNR 16-byte loads in flight before consuming them (a load-use loop would pay one
+// memory round trip per 16 bytes per lane).
+template <typename T, bool VEC, typename F>
+RT_DEVICE void for_row(const T* row, int V, F&& f) {
+  if constexpr (VEC && sizeof(T) == 2) {
+    constexpr int UNR = 8;
+    const int nv = V >> 3;
+    const rt::short8* p = reinterpret_cast<const rt::short8*>(row);
+    int c0 = threadIdx.x;
+    for (; c0 + (UNR - 1) * NT < nv; c0 += UNR * NT) {
+      rt::short8 v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) v[u] = p[c0 + u * NT];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f((c0 + u * NT) * 8 + j, rt::bf2f((uint16_t)v[u][j]));
+    }
+    for (int c = c0; c < nv; c += NT) {
+      const rt::short8 v = p[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f(c * 8 + j, rt::bf2f((uint16_t)v[j]));
+    }
+    for (int i = (nv << 3) + threadIdx.x; i < V; i += NT) f(i, rt::DT<T>::load(row + i));
+  } else {
+    for_range<T, VEC>(row, 0, V, f);
+  }
+}
+
 struct ArgMax {
   float v;
   int i;
@@ -111,7 +135,7 @@ RT_DEVICE ArgMax block_argmax(ArgMax a, float* sv, int* si) {
     si[wid] = a.i;
   }
   __syncthreads();
-  ArgMax b{lane < NT / 64 ? sv[lane] : -INFINITY, lane < NT / 64 ? si[lane] : 0x7fffffff};
+  ArgMax b{lane < NWV ? sv[lane] : -INFINITY, lane < NWV ? si[lane] : 0x7fffffff};
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) am_merge(b, __shfl_xor(b.v, o, 64), __shfl_xor(b.i, o, 64));
   return b;
@@ -123,179 +147,21 @@ RT_DEVICE void chunk_range(int V, int c, int& lo, int& hi) {
   hi = min(V, lo + per);
 }
 
-RT_DEVICE float row_max(const float* ws) {
-  float m = -INFINITY;
-  for (int c = 0; c < C; ++c) m = fmaxf(m, ws[W_MAX + c]);
-  return m;
-}
-
-// ---- 1: chunk max / argmax -----------------------------------------------------------------
-template <typename T, bool VEC>
-__global__ void __launch_bounds__(NT) smp_stats(float* __restrict__ ws, const T* __restrict__ logits, int V,
-                                                int64_t ld, const float* __restrict__ temperature,
-                                                const int64_t* __restrict__ seeds,
-                                                const int64_t* __restrict__ offsets) {
-  __shared__ float sv[4];
-  __shared__ int si[4];
-  const int b = blockIdx.x, c = blockIdx.y;
-  float* w = ws + (size_t)b * W_ROW;
-  // zero this chunk's share of the row's histogram / counter region (replaces a per-call
-  // memset launch; launches 2-5 are stream-ordered after this one)
-  {
-    const int z0 = W_HC, zn = W_ROW - W_HC, per = (zn + C - 1) / C;
-    const int lo_z = z0 + c * per, hi_z = min(z0 + zn, lo_z + per);
-    for (int i = lo_z + threadIdx.x; i < hi_z; i += NT) w[i] = 0.f;
-  }
-  int lo, hi;
-  chunk_range(V, c, lo, hi);
-  ArgMax a{-INFINITY, 0x7fffffff};
-  const float temp = temperature[b];
-  if (temp > 0.f) {   // also the chunk's best Gumbel score over every token (accept pass)
-    const float invT = 1.f / temp;
-    const uint64_t key = mix64((uint64_t)seeds[b] ^ mix64((uint64_t)offsets[b]));
-    ArgMax gb{-INFINITY, 0x7fffffff};
-    for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) {
-      am_merge(a, v, i);
-      am_merge(gb, v * invT + gumbel(key, (uint32_t)i), i);
-    });
-    gb = block_argmax(gb, sv, si);
-    if (threadIdx.x == 0) {
-      w[W_GV + c] = gb.v;
-      reinterpret_cast<int*>(w)[W_GI + c] = gb.i;
-    }
-  } else {
-    for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int i, float v) { am_merge(a, v, i); });
-  }
-  a = block_argmax(a, sv, si);
-  if (threadIdx.x == 0) {
-    w[W_MAX + c] = a.v;
-    reinterpret_cast<int*>(w)[W_ARG + c] = a.i;
-  }
-}
-
-// ---- 2: accept pass (fast path, see the header) -------------------------------------------------
-template <typename T, bool VEC>
-__global__ void __launch_bounds__(NT) smp_accept(int64_t* __restrict__ out, float* __restrict__ ws,
-                                                 const T* __restrict__ logits, int V, int64_t ld,
-                                                 const float* __restrict__ temperature,
-                                                 const float* __restrict__ top_p, const int* __restrict__ top_k) {
-  __shared__ float red[8];
-  const int b = blockIdx.x, c = blockIdx.y;
-  float* w = ws + (size_t)b * W_ROW;
-  int* wi = reinterpret_cast<int*>(w);
-  const float temp = temperature[b];
-  const int k = top_k[b];
-  const float p = top_p[b];
-  const bool use_k = k > 0 && k < V;
-  if (!(temp > 0.f) || (!use_k && !(p < 1.f))) {   // greedy, or nothing filtered: decided now
-    if (c == 0 && threadIdx.x == 0) {
-      ArgMax r{-INFINITY, 0x7fffffff};
-      for (int j = 0; j < C; ++j) {
-        if (temp > 0.f) am_merge(r, w[W_GV + j], wi[W_GI + j]);
-        else am_merge(r, w[W_MAX + j], wi[W_ARG + j]);
-      }
-      if (r.i < 0 || r.i >= V) {   // no finite score: the row argmax
-        r = ArgMax{-INFINITY, 0x7fffffff};
-        for (int j = 0; j < C; ++j) am_merge(r, w[W_MAX + j], wi[W_ARG + j]);
-      }
-      out[b] = r.i;
-      wi[W_DONE] = 1;
-    }
-    return;
-  }
-  if (use_k) return;   // top-k rows take the histogram path
-  ArgMax g{-INFINITY, 0x7fffffff};
-  for (int j = 0; j < C; ++j) am_merge(g, w[W_GV + j], wi[W_GI + j]);
-  if (g.i < 0 || g.i >= V) return;   // no finite score: the histogram path decides
-  const float mx = row_max(w), invT = 1.f / temp;
-  const T* row = logits + (size_t)b * ld;
-  const float vj = rt::DT<T>::load(row + g.i);
-  int lo, hi;
-  chunk_range(V, c, lo, hi);
-  float above = 0.f, total = 0.f;
-  for_chunk<T, VEC>(row, lo, hi, [&](int, float v) {
-    const float e = __expf((v - mx) * invT);
-    total += e;
-    above += v > vj ? e : 0.f;
-  });
-  above = rt::block_sum(above, red);
-  total = rt::block_sum(total, red);
-  if (threadIdx.x == 0) {
-    atomicAdd(&w[W_SUM], above);
-    atomicAdd(&w[W_SUM + 1], total);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(&wi[W_CNT2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == C - 1) {   // every chunk's sums are in: decide the row
-      const float A = __hip_atomic_load(&w[W_SUM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float Z = __hip_atomic_load(&w[W_SUM + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (A < p * Z) {
-        out[b] = g.i;
-        __hip_atomic_store(&wi[W_DONE], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-}
-
-// ---- 2 / 4: (sub-)histograms ---------------------------------------------------------------
-template <typename T, bool VEC, bool SUB>
-__global__ void __launch_bounds__(NT) smp_hist(float* __restrict__ ws, const T* __restrict__ logits, int V, int64_t ld,
-                                               const float* __restrict__ temperature, const float* __restrict__ top_p,
-                                               const int* __restrict__ top_k) {
-  __shared__ float hc[NB], hm[NB];
-  const int b = blockIdx.x, c = blockIdx.y;
-  float* w = ws + (size_t)b * W_ROW;
-  const float temp = temperature[b];
-  const int k = top_k[b];
-  if (!(temp > 0.f) || !((k > 0 && k < V) || top_p[b] < 1.f)) return;
-  if (reinterpret_cast<const int*>(w)[W_DONE]) return;   // sampled by the accept pass
-  int bsel = 0;
-  if constexpr (SUB) {
-    bsel = reinterpret_cast<const int*>(w)[W_SEL];
-    if (bsel >= NB) return;
-  }
-  for (int i = threadIdx.x; i < NB; i += NT) {
-    hc[i] = 0.f;
-    hm[i] = 0.f;
-  }
-  __syncthreads();
-  const float mx = row_max(w), invT = 1.f / temp, scale = NB / ZR;
-  const float top_edge = -(float)bsel / scale;
-  const float sub = scale * NB;
-  int lo, hi;
-  chunk_range(V, c, lo, hi);
-  for_chunk<T, VEC>(logits + (size_t)b * ld, lo, hi, [&](int, float v) {
-    const float z = (v - mx) * invT;
-    const float fb = -z * scale;
-    if constexpr (SUB) {
-      if (fb >= (float)bsel && fb < (float)(bsel + 1)) {
-        int sb = (int)((top_edge - z) * sub);
-        sb = sb < 0 ? 0 : (sb >= NB ? NB - 1 : sb);
-        atomicAdd(&hc[sb], 1.f);
-        atomicAdd(&hm[sb], __expf(z));
-      }
-    } else if (fb < (float)NB) {
-      const int bin = (int)fb;
-      atomicAdd(&hc[bin], 1.f);
-      atomicAdd(&hm[bin], __expf(z));
-    }
-  });
-  __syncthreads();
-  float* gc = w + (SUB ? W_SC : W_HC);
-  float* gm = w + (SUB ? W_SM : W_HM);
-  for (int i = threadIdx.x; i < NB; i += NT) {
-    if (hc[i] != 0.f) {
-      atomicAdd(gc + i, hc[i]);
-      atomicAdd(gm + i, hm[i]);
-    }
-  }
-}
-
-// First bin whose inclusive prefix of `a` reaches ta or of `bm` reaches tb (1024 threads, 2 bins each).
+// First bin whose inclusive prefix of `a` reaches ta or of `bm` reaches tb (NT threads, NB/NT
+// bins each); *pa / *pb = the exclusive prefixes before it. Returns NB when none crosses.
 RT_DEVICE int first_crossing(const float* a, const float* bm, float ta, float tb, float* scr, int* res, float* pa,
                              float* pb) {
+  constexpr int BPT = NB / NT;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const float a0 = a[2 * t], a1 = a[2 * t + 1], b0 = bm[2 * t], b1 = bm[2 * t + 1];
-  float sa = a0 + a1, sb = b0 + b1;
+  float la[BPT], lb[BPT], sa = 0.f, sb = 0.f;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    la[j] = a[BPT * t + j];
+    lb[j] = bm[BPT * t + j];
+    sa += la[j];
+    sb += lb[j];
+  }
+  const float ta_own = sa, tb_own = sb;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const float xa = __shfl_up(sa, o, 64), xb = __shfl_up(sb, o, 64);
@@ -307,185 +173,473 @@ RT_DEVICE int first_crossing(const float* a, const float* bm, float ta, float tb
   __syncthreads();
   if (lane == 63) {
     scr[wid] = sa;
-    scr[32 + wid] = sb;
+    scr[NWV + wid] = sb;
   }
   if (t == 0) *res = NB;
   __syncthreads();
-  float oa = 0.f, ob = 0.f;
+  float ca = 0.f, cb = 0.f;
   for (int w = 0; w < wid; ++w) {
-    oa += scr[w];
-    ob += scr[32 + w];
+    ca += scr[w];
+    cb += scr[NWV + w];
   }
-  const float ia = oa + sa, ib = ob + sb, ea = ia - a0 - a1, eb = ib - b0 - b1;
+  ca += sa - ta_own;     // exclusive prefix before this thread's first bin
+  cb += sb - tb_own;
   int cross = NB;
-  if (ea + a0 >= ta || eb + b0 >= tb) cross = 2 * t;
-  else if (ia >= ta || ib >= tb) cross = 2 * t + 1;
+  float ea = 0.f, eb = 0.f;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    if (cross == NB && (ca + la[j] >= ta || cb + lb[j] >= tb)) {
+      cross = BPT * t + j;
+      ea = ca;
+      eb = cb;
+    }
+    ca += la[j];
+    cb += lb[j];
+  }
   if (cross < NB) atomicMin(res, cross);
   __syncthreads();
-  const int cb = *res;
-  if (cb < NB && (cb >> 1) == t) {
-    *pa = (cb & 1) ? ea + a0 : ea;
-    *pb = (cb & 1) ? eb + b0 : eb;
+  const int cbin = *res;
+  if (cbin < NB && cross == cbin) {
+    *pa = ea;
+    *pb = eb;
   }
   __syncthreads();
-  return cb;
+  return cbin;
 }
 
-// ---- 3: select the threshold bin ---------------------------------------------------------------
-__global__ void __launch_bounds__(1024) smp_select(float* __restrict__ ws, int V, const float* __restrict__ temperature,
-                                                   const float* __restrict__ top_p, const int* __restrict__ top_k) {
-  __shared__ float scr[64];
-  __shared__ int sres;
-  __shared__ float spa, spb;
-  const int b = blockIdx.x;
-  float* w = ws + (size_t)b * W_ROW;
-  int* wi = reinterpret_cast<int*>(w);
-  const int k = top_k[b];
-  const float p = top_p[b];
-  if (!(temperature[b] > 0.f) || !((k > 0 && k < V) || p < 1.f) || wi[W_DONE]) {
-    if (threadIdx.x == 0) wi[W_SEL] = NB;
-    return;
-  }
-  const float* hc = w + W_HC;
-  const float* hm = w + W_HM;
-  float tm = 0.f;
-  for (int i = threadIdx.x; i < NB; i += 1024) tm += hm[i];
-  tm = rt::block_sum(tm, scr);
-  __syncthreads();
-  const bool use_k = k > 0 && k < V;
-  const float tk = use_k ? (float)k : 3.0e38f;
-  int bk = NB;
-  float pre_c = 0.f, zk_mass = tm;
-  if (use_k) {
-    bk = first_crossing(hc, hm, tk, 3.0e38f, scr, &sres, &spa, &spb);
-    if (bk < NB) {
-      zk_mass = spb + hm[bk];
-      pre_c = spa;
-    }
-  }
-  const float tp = p < 1.f ? p * zk_mass : 3.0e38f;
-  int bp = NB;
-  float pre_m = 0.f;
-  if (p < 1.f) {
-    bp = first_crossing(hc, hm, 3.0e38f, tp, scr, &sres, &spa, &spb);
-    pre_m = spb;
-  }
-  if (threadIdx.x == 0) {
-    if (bk <= bp) {
-      wi[W_SEL] = bk;
-      wi[W_SEL + 1] = 1;
-      w[W_SEL + 2] = tk - pre_c;
-    } else {
-      wi[W_SEL] = bp;
-      wi[W_SEL + 1] = 0;
-      w[W_SEL + 2] = tp - pre_m;
-    }
-  }
-}
-
-// ---- 5: threshold + Gumbel argmax + last-arriver reduction --------------------------------------
+// Top-p slow path without a histogram (the rejected-j* case, ~1 - top_p of the rows):
+// a token is inside the nucleus iff the mass of the tokens strictly more likely than it is below
+// p * total (the reference's sorted-cumsum cut, restated), the same test the accept pass made for
+// j*. Candidates = the chunks' best Gumbel tokens in score order; c1 = j* is out. ONE pass
+// measures the mass above the next NC candidates; the first one inside, c*, is the answer unless
+// a non-best token of a chunk ranked above c* (those chunks' bests are out) scores higher and is
+// inside: those chunks are rescanned, their tokens' nucleus test decided from the known
+// values (>= an inside candidate's value: in; <= an outside one's: out). Returns the token,
+// or -1 when some token stays undecided or no candidate is inside (the histogram path decides).
+constexpr int NC = 4;
 template <typename T, bool VEC>
-__global__ void __launch_bounds__(1024) smp_final(int64_t* __restrict__ out, float* __restrict__ ws,
-                                                  const T* __restrict__ logits, int V, int64_t ld,
-                                                  const float* __restrict__ temperature,
-                                                  const int64_t* __restrict__ seeds,
-                                                  const int64_t* __restrict__ offsets) {
-  __shared__ float scr[64];
-  __shared__ int sres;
-  __shared__ float spa, spb;
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  __shared__ int last;
-  const int b = blockIdx.x, c = blockIdx.y;
-  float* w = ws + (size_t)b * W_ROW;
-  int* wi = reinterpret_cast<int*>(w);
-  const float temp = temperature[b];
-  if (wi[W_DONE]) return;   // greedy / unfiltered / accepted: out[b] written by launch 2
-  const float mx = row_max(w), invT = 1.f / temp, scale = NB / ZR;
-  float zthr = -INFINITY;
-  const int bsel = wi[W_SEL];
-  if (bsel < NB) {
-    const bool by_count = wi[W_SEL + 1] != 0;
-    const float need = w[W_SEL + 2];
-    const int cb = by_count ? first_crossing(w + W_SC, w + W_SM, need, 3.0e38f, scr, &sres, &spa, &spb)
-                            : first_crossing(w + W_SC, w + W_SM, 3.0e38f, need, scr, &sres, &spa, &spb);
-    const int cc = cb < NB ? cb : NB - 1;
-    zthr = -(float)bsel / scale - (float)(cc + 1) / (scale * NB);
+RT_DEVICE int nucleus_by_candidates(const T* row, int V, float mx, float invT, float pz, float vj, uint64_t key,
+                                    const float* s_gv, const int* s_gi, float* sv, int* si, float* red) {
+  __shared__ int s_ord[C];
+  __shared__ float s_cv[NC];
+  __shared__ int s_flag;
+  if (threadIdx.x < C) {   // rank of chunk j's best by (score desc, index asc)
+    const int j = threadIdx.x;
+    int r = 0;
+    for (int q = 0; q < C; ++q)
+      r += (s_gv[q] > s_gv[j] || (s_gv[q] == s_gv[j] && s_gi[q] < s_gi[j])) ? 1 : 0;
+    s_ord[r] = j;
   }
-  const uint64_t key = mix64((uint64_t)seeds[b] ^ mix64((uint64_t)offsets[b]));
+  __syncthreads();
+  if (threadIdx.x < NC) {
+    const int gi = s_gi[s_ord[1 + threadIdx.x]];
+    s_cv[threadIdx.x] = (gi >= 0 && gi < V) ? rt::DT<T>::load(row + gi) : INFINITY;
+  }
+  if (threadIdx.x == 0) s_flag = 0;
+  __syncthreads();
+  float cv[NC], acc[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    cv[k] = s_cv[k];
+    acc[k] = 0.f;
+  }
+  for_row<T, VEC>(row, V, [&](int, float v) {
+    const float e = __expf((v - mx) * invT);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) acc[k] += v > cv[k] ? e : 0.f;
+  });
+  int kstar = -1;
+  float v_in = INFINITY, v_out = vj;   // known: values >= v_in are inside, <= v_out outside
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const float m = rt::block_sum(acc[k], red);
+    const bool ok = cv[k] != INFINITY && m < pz;
+    if (ok) {
+      if (kstar < 0) kstar = k;
+      v_in = fminf(v_in, cv[k]);
+    } else if (cv[k] != INFINITY) {
+      v_out = fmaxf(v_out, cv[k]);
+    }
+  }
+  if (kstar < 0) return -1;
+  const int cs = s_ord[1 + kstar];
+  ArgMax best{s_gv[cs], s_gi[cs]};
+  // chunks ranked above c* (their bests are outside): any token beating c* must be checked
+  for (int q = 0; q <= kstar; ++q) {
+    int lo, hi;
+    chunk_range(V, s_ord[q], lo, hi);
+    for_range<T, VEC>(row, lo, hi, [&](int i, float v) {
+      const float sc = v * invT + gumbel(key, (uint32_t)i);
+      if (sc > s_gv[cs] || (sc == s_gv[cs] && i < s_gi[cs])) {
+        if (v >= v_in) am_merge(best, sc, i);
+        else if (v > v_out) s_flag = 1;      // undecided from the known values
+      }
+    });
+  }
+  best = block_argmax(best, sv, si);
+  __syncthreads();
+  return s_flag ? -1 : best.i;
+}
+
+struct SampleArgs {
+  int64_t* tok;                 // [B] sampled ids
+  float* ws;                    // B * W_ROW + 4 words, zero before the first launch (self re-arming)
+  const void* logits;
+  int V;
+  int64_t ld;
+  const float* temperature;
+  const float* top_p;
+  const int* top_k;
+  const int64_t* seeds;
+  int64_t* offsets;             // read by every workgroup; rewritten by the deciders (adv)
+  int B;
+  // decode-step bookkeeping (adv = 1): decode_advance + next-step decode_prep of each row
+  int adv;
+  int64_t* out;                 // [max_steps, B]
+  int64_t* ids;
+  int64_t* positions;
+  int* ctx_lens;
+  int64_t* step;
+  int max_steps;
+  int64_t* slots;               // prep (res != nullptr)
+  uint16_t* res;
+  const int* block_tables;
+  const uint16_t* embed;
+  int max_blocks, BS, H;
+  int64_t vocab;
+  int probe;                    // microbench only (RT_SMP_PROBE): 1 = stop before the slow path,
+                                // 2 = after its coarse histogram, 3 = after the sub-histogram
+};
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
+  __shared__ float hc[NB], hm[NB];
+  // histogram accumulators: INTEGER LDS atomics (count, and mass in 32.32 fixed point) — LDS
+  // float atomic adds serialize per lane on gfx950 (r03 probe: a 128K-token coarse pass took
+  // 320 us on one workgroup), the integer ones do not
+  __shared__ unsigned hci[NB];
+  __shared__ unsigned long long hmi[NB];
+  __shared__ float sv[NWV], red[2 * NWV + 2];
+  __shared__ int si[NWV];
+  __shared__ float s_max[C], s_gv[C], s_min[C];
+  __shared__ int s_arg[C], s_gi[C];
+  __shared__ int s_last, s_res;
+  __shared__ float s_pa, s_pb;
+  const int b = blockIdx.x, c = blockIdx.y;
+  float* w = a.ws + (size_t)b * W_ROW;
+  int* wi = reinterpret_cast<int*>(w);
+  const T* row = static_cast<const T*>(a.logits) + (size_t)b * a.ld;
+  const int V = a.V;
+  const float temp = a.temperature[b];
+  const int64_t off = a.offsets[b];
+  const int64_t st = a.adv ? *a.step : 0;
+  // the deciders rewrite offsets / step: every read of them completes before this workgroup's
+  // ticket (below), and the deciders write only after every ticket of their row / launch
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint64_t key = mix64((uint64_t)a.seeds[b] ^ mix64((uint64_t)off));
+  const float invT = temp > 0.f ? 1.f / temp : 0.f;
+
+  // ---- 1: chunk records ----
   int lo, hi;
   chunk_range(V, c, lo, hi);
-  ArgMax a{-INFINITY, 0x7fffffff};
-  // 1024 threads walk the chunk (NT is 256 in for_chunk's stride: walk 4 sub-ranges)
-  const T* row = logits + (size_t)b * ld;
-  for (int i = lo + threadIdx.x; i < hi; i += 1024) {
-    const float z = (rt::DT<T>::load(row + i) - mx) * invT;
-    if (z >= zthr) am_merge(a, z + gumbel(key, (uint32_t)i), i);
+  ArgMax am{-INFINITY, 0x7fffffff}, gb{-INFINITY, 0x7fffffff};
+  float mn = INFINITY;
+  if (temp > 0.f) {
+    for_range<T, VEC>(row, lo, hi, [&](int i, float v) {
+      am_merge(am, v, i);
+      mn = fminf(mn, v);
+      am_merge(gb, v * invT + gumbel(key, (uint32_t)i), i);
+    });
+    gb = block_argmax(gb, sv, si);
+    mn = -rt::block_max(-mn, red);
+  } else {
+    for_range<T, VEC>(row, lo, hi, [&](int i, float v) { am_merge(am, v, i); });
   }
-  // block argmax over 16 waves
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) am_merge(a, __shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64));
-  if (lane == 0) {
-    sv[wid] = a.v;
-    si[wid] = a.i;
-  }
-  __syncthreads();
+  am = block_argmax(am, sv, si);
   if (threadIdx.x == 0) {
-    ArgMax bm{-INFINITY, 0x7fffffff};
-    for (int j = 0; j < 16; ++j) am_merge(bm, sv[j], si[j]);
-    // publish this chunk's partial with sc1 (write-through) stores, drain them, then count
-    // arrivals; the last arriver reads every partial with sc1 loads (MI355X_MICROARCH "Valid
-    // forms" row 1: no L2 writeback/invalidate fences needed)
-    __hip_atomic_store(&w[W_PV + c], bm.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&wi[W_PI + c], bm.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&w[W_MIN + c], mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&w[W_MAX + c], am.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&wi[W_ARG + c], am.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&w[W_GV + c], gb.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&wi[W_GI + c], gb.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int prev = __hip_atomic_fetch_add(&wi[W_CNT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev == C - 1);
-    if (last) {
-      ArgMax r{-INFINITY, 0x7fffffff};
-      for (int j = 0; j < C; ++j)
-        am_merge(r, __hip_atomic_load(&w[W_PV + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                 __hip_atomic_load(&wi[W_PI + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (r.i == 0x7fffffff) {  // empty allowed set (rounding): fall back to the row argmax
-        for (int j = 0; j < C; ++j) am_merge(r, w[W_MAX + j], wi[W_ARG + j]);
+    s_last = prev == C - 1;
+    if (s_last) __hip_atomic_store(&wi[W_CNT], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  // ---- 2: the decider ----
+  if (threadIdx.x < C) {
+    const int j = threadIdx.x;
+    s_max[j] = __hip_atomic_load(&w[W_MAX + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_arg[j] = __hip_atomic_load(&wi[W_ARG + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_gv[j] = __hip_atomic_load(&w[W_GV + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_gi[j] = __hip_atomic_load(&wi[W_GI + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_min[j] = __hip_atomic_load(&w[W_MIN + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  ArgMax ra{-INFINITY, 0x7fffffff}, g{-INFINITY, 0x7fffffff};
+  float rmin = INFINITY;
+  for (int j = 0; j < C; ++j) {
+    am_merge(ra, s_max[j], s_arg[j]);
+    am_merge(g, s_gv[j], s_gi[j]);
+    rmin = fminf(rmin, s_min[j]);
+  }
+  const float mx = ra.v;
+  const int k = a.top_k[b];
+  const float p = a.top_p[b];
+  const bool use_k = k > 0 && k < V;
+  int tok;
+  if (!(temp > 0.f)) {
+    tok = ra.i;
+  } else if (!use_k && !(p < 1.f)) {
+    tok = (g.i >= 0 && g.i < V) ? g.i : ra.i;     // no finite score: the row argmax
+  } else {
+    bool accepted = false;
+    int cand = -1;
+    if (!use_k && g.i >= 0 && g.i < V) {   // fast path: is j* inside the nucleus?
+      const float vj = rt::DT<T>::load(row + g.i);
+      float above = 0.f, total = 0.f;
+      for_row<T, VEC>(row, V, [&](int, float v) {
+        const float e = __expf((v - mx) * invT);
+        total += e;
+        above += v > vj ? e : 0.f;
+      });
+      above = rt::block_sum(above, red);
+      total = rt::block_sum(total, red);
+      accepted = above < p * total;
+      if (!accepted && a.probe == 0) cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, p * total, vj, key, s_gv,
+                                                                          s_gi, sv, si, red);
+    }
+    if (accepted || cand >= 0 || a.probe == 1) {
+      tok = accepted ? g.i : (cand >= 0 ? cand : ra.i);
+    } else {
+      // ---- slow path: histogram threshold, then the Gumbel argmax over the allowed set ----
+      // coarse bins span the row's actual z range [zlo, 0] (not a fixed [-ZR, 0]): the values
+      // spread over all NB bins, so the LDS atomics of one workgroup rarely collide
+      const float zlo = fmaxf(-ZR, fminf((rmin - mx) * invT, -1e-3f));
+      const float scale = NB / (-zlo * 1.0001f + 1e-6f);   // the row minimum lands inside the last bin
+      for (int i = threadIdx.x; i < NB; i += NT) {
+        hci[i] = 0u;
+        hmi[i] = 0ull;
       }
-      out[b] = r.i;
+      __syncthreads();
+      for_row<T, VEC>(row, V, [&](int, float v) {
+        const float z = (v - mx) * invT;
+        const float fb = -z * scale;
+        if (fb < (float)NB) {
+          const int bin = (int)fb;
+          atomicAdd(&hci[bin], 1u);
+          atomicAdd(&hmi[bin], (unsigned long long)(__expf(z) * 4294967296.f));
+        }
+      });
+      __syncthreads();
+      for (int i = threadIdx.x; i < NB; i += NT) {
+        hc[i] = (float)hci[i];
+        hm[i] = (float)(hmi[i] >> 8) * (1.f / 16777216.f);
+      }
+      __syncthreads();
+      if (a.probe == 2) {
+        if (threadIdx.x == 0) a.tok[b] = ra.i + (hc[0] == -1.f);
+        return;
+      }
+      float tm = 0.f;
+      for (int i = threadIdx.x; i < NB; i += NT) tm += hm[i];
+      tm = rt::block_sum(tm, red);
+      const float tk = use_k ? (float)k : 3.0e38f;
+      int bk = NB;
+      float pre_c = 0.f, zk_mass = tm;
+      if (use_k) {
+        bk = first_crossing(hc, hm, tk, 3.0e38f, red, &s_res, &s_pa, &s_pb);
+        if (bk < NB) {
+          zk_mass = s_pb + hm[bk];
+          pre_c = s_pa;
+        }
+      }
+      const float tp = p < 1.f ? p * zk_mass : 3.0e38f;
+      int bp = NB;
+      float pre_m = 0.f;
+      if (p < 1.f) {
+        bp = first_crossing(hc, hm, 3.0e38f, tp, red, &s_res, &s_pa, &s_pb);
+        pre_m = s_pb;
+      }
+      int bsel;
+      bool by_count;
+      float need;
+      if (bk <= bp) {
+        bsel = bk;
+        by_count = true;
+        need = tk - pre_c;
+      } else {
+        bsel = bp;
+        by_count = false;
+        need = tp - pre_m;
+      }
+      float zthr = -INFINITY;
+      if (bsel < NB) {   // sub-histogram of the selected bin
+        __syncthreads();
+        for (int i = threadIdx.x; i < NB; i += NT) {
+          hci[i] = 0u;
+          hmi[i] = 0ull;
+        }
+        __syncthreads();
+        const float top_edge = -(float)bsel / scale, sub = scale * NB;
+        for_row<T, VEC>(row, V, [&](int, float v) {
+          const float z = (v - mx) * invT;
+          const float fb = -z * scale;
+          if (fb >= (float)bsel && fb < (float)(bsel + 1)) {
+            int sb = (int)((top_edge - z) * sub);
+            sb = sb < 0 ? 0 : (sb >= NB ? NB - 1 : sb);
+            atomicAdd(&hci[sb], 1u);
+            atomicAdd(&hmi[sb], (unsigned long long)(__expf(z) * 4294967296.f));
+          }
+        });
+        __syncthreads();
+        for (int i = threadIdx.x; i < NB; i += NT) {
+          hc[i] = (float)hci[i];
+          hm[i] = (float)(hmi[i] >> 8) * (1.f / 16777216.f);
+        }
+        __syncthreads();
+        if (a.probe == 3) {
+          if (threadIdx.x == 0) a.tok[b] = ra.i + (hc[0] == -1.f);
+          return;
+        }
+        const int cb = by_count ? first_crossing(hc, hm, need, 3.0e38f, red, &s_res, &s_pa, &s_pb)
+                                : first_crossing(hc, hm, 3.0e38f, need, red, &s_res, &s_pa, &s_pb);
+        const int cc = cb < NB ? cb : NB - 1;
+        zthr = -(float)bsel / scale - (float)(cc + 1) / (scale * NB);
+      }
+      // Gumbel argmax over the allowed set {z >= zthr}. A chunk's best score over ALL its tokens
+      // (s_gv / s_gi, from the stats phase) is also its best allowed one whenever that token is
+      // allowed; only the chunks whose best is not (the rejected j*'s, ~1 - top_p of the others)
+      // are scanned again. Scores s_gv = v/T + g differ from z + g by the row constant mx/T.
+      ArgMax r{-INFINITY, 0x7fffffff};
+      __shared__ int s_rescan[C];
+      __shared__ int s_nres;
+      if (threadIdx.x == 0) s_nres = 0;
+      __syncthreads();
+      if (threadIdx.x < C) {
+        const int j = threadIdx.x, gi = s_gi[j];
+        const bool ok = gi >= 0 && gi < V && (rt::DT<T>::load(row + gi) - mx) * invT >= zthr;
+        if (!ok) s_rescan[atomicAdd(&s_nres, 1)] = j;
+      }
+      __syncthreads();
+      for (int j = 0; j < C; ++j) {
+        const int gi = s_gi[j];
+        bool listed = false;
+        for (int q = 0; q < s_nres; ++q) listed |= s_rescan[q] == j;
+        if (!listed) am_merge(r, s_gv[j] - mx * invT, gi);     // every thread: same merge order
+      }
+      for (int q = 0; q < s_nres; ++q) {
+        int clo, chi;
+        chunk_range(V, s_rescan[q], clo, chi);
+        for_range<T, VEC>(row, clo, chi, [&](int i, float v) {
+          const float z = (v - mx) * invT;
+          if (z >= zthr) am_merge(r, z + gumbel(key, (uint32_t)i), i);
+        });
+      }
+      r = block_argmax(r, sv, si);
+      tok = r.i == 0x7fffffff ? ra.i : r.i;     // empty allowed set (rounding): the row argmax
+    }
+  }
+
+  // ---- 3: the token and this row's step bookkeeping ----
+  if (threadIdx.x == 0) {
+    a.tok[b] = tok;
+    if (a.adv) {
+      if (st < a.max_steps) a.out[st * a.B + b] = tok;
+      a.ids[b] = tok;
+      const int64_t pn = a.positions[b] + 1;
+      a.positions[b] = pn;
+      a.ctx_lens[b] += 1;
+      if (a.slots != nullptr) {   // past the table (a turn's last step) the slot is never used
+        const int64_t bi = pn / a.BS;
+        const int64_t blk = bi < a.max_blocks ? a.block_tables[(size_t)b * a.max_blocks + bi] : 0;
+        a.slots[b] = blk * a.BS + pn % a.BS;
+        a.offsets[b] = pn + 1;
+      }
+    }
+  }
+  if (a.adv && a.res != nullptr) {   // next step's embedding row, 16 B per lane
+    int64_t t = tok < 0 ? 0 : (tok >= a.vocab ? a.vocab - 1 : tok);
+    const int row8 = a.H / 8;
+    const uint4* src = reinterpret_cast<const uint4*>(a.embed) + (size_t)t * row8;
+    uint4* dst = reinterpret_cast<uint4*>(a.res) + (size_t)b * row8;
+    for (int i = threadIdx.x; i < row8; i += NT) dst[i] = src[i];
+  }
+  if (a.adv && threadIdx.x == 0) {   // the last decider of the launch advances the step counter
+    int* done = reinterpret_cast<int*>(a.ws) + (size_t)a.B * W_ROW;
+    const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == a.B - 1) {
+      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *a.step = st + 1;
     }
   }
 }
 }  // namespace
 
-int sample_workspace_floats(int B) { return B * W_ROW; }
+int sample_workspace_floats(int B) { return B * W_ROW + 4; }
 
 int launch_sample(int64_t* out, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
                   const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
-                  const int64_t* offsets, float* ws, hipStream_t stream) {
+                  const int64_t* offsets, float* ws, hipStream_t stream, const void* advance) {
   if (B == 0) return 0;
+  if (V < 1) return -1;
   const size_t esz = is_bf16 ? 2 : 4;
   const bool vec = ((uintptr_t)logits % 16 == 0) && ((ld_row * esz) % 16 == 0);
-  const dim3 g2(B, C);
-#define RT_SMP(TT, VV)                                                                                              \
-  do {                                                                                                              \
-    hipLaunchKernelGGL((smp_stats<TT, VV>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,             \
-                       temperature, seeds, offsets);                                                                \
-    hipLaunchKernelGGL((smp_accept<TT, VV>), g2, dim3(NT), 0, stream, out, ws, (const TT*)logits, V, ld_row,        \
-                       temperature, top_p, top_k);                                                                  \
-    hipLaunchKernelGGL((smp_hist<TT, VV, false>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,        \
-                       temperature, top_p, top_k);                                                                  \
-    hipLaunchKernelGGL(smp_select, dim3(B), dim3(1024), 0, stream, ws, V, temperature, top_p, top_k);              \
-    hipLaunchKernelGGL((smp_hist<TT, VV, true>), g2, dim3(NT), 0, stream, ws, (const TT*)logits, V, ld_row,         \
-                       temperature, top_p, top_k);                                                                  \
-    hipLaunchKernelGGL((smp_final<TT, VV>), g2, dim3(1024), 0, stream, out, ws, (const TT*)logits, V, ld_row,       \
-                       temperature, seeds, offsets);                                                                \
-  } while (0)
+  SampleArgs a{};
+  if (advance != nullptr) a = *static_cast<const SampleArgs*>(advance);
+  a.tok = out;
+  a.ws = ws;
+  a.logits = logits;
+  a.V = V;
+  a.ld = ld_row;
+  a.temperature = temperature;
+  a.top_p = top_p;
+  a.top_k = top_k;
+  a.seeds = seeds;
+  a.offsets = const_cast<int64_t*>(offsets);
+  a.B = B;
+  static const int probe = getenv("RT_SMP_PROBE") ? atoi(getenv("RT_SMP_PROBE")) : 0;
+  a.probe = probe;
+  const dim3 g(B, C);
   if (is_bf16) {
-    if (vec) RT_SMP(uint16_t, true);
-    else RT_SMP(uint16_t, false);
+    if (vec) hipLaunchKernelGGL((smp_kernel<uint16_t, true>), g, dim3(NT), 0, stream, a);
+    else hipLaunchKernelGGL((smp_kernel<uint16_t, false>), g, dim3(NT), 0, stream, a);
   } else {
-    if (vec) RT_SMP(float, true);
-    else RT_SMP(float, false);
+    if (vec) hipLaunchKernelGGL((smp_kernel<float, true>), g, dim3(NT), 0, stream, a);
+    else hipLaunchKernelGGL((smp_kernel<float, false>), g, dim3(NT), 0, stream, a);
   }
-#undef RT_SMP
-  return 0;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The captured decode step's sampler + bookkeeping (decode_advance + decode_prep semantics).
+int launch_sample_advance(int64_t* tok, const void* logits, bool is_bf16, int B, int V, int64_t ld_row,
+                          const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
+                          int64_t* offsets, float* ws, int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens,
+                          int64_t* step, int max_steps, int64_t* slots, void* res, const int* block_tables,
+                          const void* embed, int max_blocks, int BS, int H, int64_t vocab, hipStream_t stream) {
+  const bool prep = res != nullptr;
+  if (prep && (slots == nullptr || block_tables == nullptr || embed == nullptr || H % 8 || BS <= 0 ||
+               max_blocks <= 0 || vocab <= 0))
+    return -3;
+  SampleArgs a{};
+  a.adv = 1;
+  a.out = out;
+  a.ids = ids;
+  a.positions = positions;
+  a.ctx_lens = ctx_lens;
+  a.step = step;
+  a.max_steps = max_steps;
+  a.slots = prep ? slots : nullptr;
+  a.res = (uint16_t*)res;
+  a.block_tables = block_tables;
+  a.embed = (const uint16_t*)embed;
+  a.max_blocks = max_blocks;
+  a.BS = BS;
+  a.H = H;
+  a.vocab = vocab;
+  return launch_sample(tok, logits, is_bf16, B, V, ld_row, temperature, top_p, top_k, seeds, offsets, ws, stream, &a);
 }

@@ -322,6 +322,46 @@ def test_sample_top_p_nucleus():
 
 
 
+@pytest.mark.parametrize("mode", ["greedy", "top_p", "top_k"])
+def test_sample_advance_equals_sample_then_advance(mode):
+    """The captured step's fused K6 + bookkeeping launch (csrc/sampling.hip sample_advance) equals
+    sample -> decode_advance(prep) run separately, bit for bit, over several chained steps on ONE
+    persistent workspace (its tickets re-arm: no memset between replays)."""
+    B, V, H, bs, maxb = 5, 128256, 256, 32, 8
+    g = torch.Generator(device=DEV).manual_seed(3)
+    embed = (torch.randn(V, H, generator=g, device=DEV)).to(torch.bfloat16)
+    bt = torch.randperm(64, device=DEV)[:B * maxb].to(torch.int32).reshape(B, maxb)
+    temp = torch.full((B,), 0.0 if mode == "greedy" else 0.8, device=DEV)
+    top_p = torch.full((B,), 0.9 if mode == "top_p" else 1.0, device=DEV)
+    top_k = torch.full((B,), 40 if mode == "top_k" else 0, dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 5
+
+    def state():
+        pos = torch.tensor([3, 40, 77, 100, 31], dtype=torch.int64, device=DEV)
+        return dict(out=torch.zeros(16, B, dtype=torch.int64, device=DEV), ids=torch.zeros(B, dtype=torch.int64, device=DEV),
+                    pos=pos, ctx=(pos + 1).to(torch.int32), step=torch.zeros(1, dtype=torch.int64, device=DEV),
+                    slots=torch.zeros(B, dtype=torch.int64, device=DEV), offs=pos + 1,
+                    res=torch.zeros(B, H, dtype=torch.bfloat16, device=DEV))
+    a, r = state(), state()
+    ws = ops.sample_workspace(B, DEV)
+    nxt = torch.zeros(B, dtype=torch.int64, device=DEV)
+    for step in range(4):
+        logits = bf(B, V, scale=3.0, seed=100 + step)
+        ops.sample_advance(logits, temp, top_p, top_k, seeds, a["offs"], ws, nxt, a["out"], a["ids"], a["pos"],
+                           a["ctx"], a["step"], a["slots"], a["res"], bt, embed, bs)
+        t = ops.sample(logits, temp, top_p, top_k, seeds, r["offs"])
+        ops.decode_advance(r["out"], r["ids"], r["pos"], r["ctx"], r["step"], t,
+                           prep=(r["slots"], r["offs"], r["res"], bt, embed, bs))
+        assert torch.equal(nxt, t), (step, nxt, t)
+    for k in a:
+        assert torch.equal(a[k], r[k]), k
+    assert int(a["step"]) == 4
+    wsi = ws.view(torch.int32)
+    assert int(wsi[-4]) == 0                                       # rows-done ticket re-armed
+    row = (ws.numel() - 4) // B
+    assert all(int(wsi[b * row + row - 4]) == 0 for b in range(B))   # row tickets re-armed
+
+
 def test_paging_guard_matches_reference():
     g = torch.Generator().manual_seed(3)
     for trial in range(40):

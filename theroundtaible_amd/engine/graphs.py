@@ -62,6 +62,8 @@ class DecodeGraph:
             self.groups = torch.zeros(B, 3, dtype=torch.int32, device=dev)
             self._reset_groups()
         self.guard_err = torch.zeros(1, dtype=torch.int32, device=dev)   # debug paging guard (captured)
+        self.nxt = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.sample_ws = ops.sample_workspace(B, dev)      # self-re-arming K6 tickets
         self.graph = None
         self._host_out: List[torch.Tensor] = []
         self._capture()
@@ -96,10 +98,17 @@ class DecodeGraph:
             logits = e.model.forward(self.input_ids, self.positions, e.kv, meta, hidden=hidden)
         else:
             logits = e.model.forward(self.input_ids, self.positions, e.kv, meta)
+        if fused and not self.dist_greedy:
+            # ONE launch: K6 sampling + record / advance + the next step's slots, offsets, embeddings
+            ops.sample_advance(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets,
+                               self.sample_ws, self.nxt, self.out, self.input_ids, self.positions, self.ctx_lens,
+                               self.step, self.slots, self.hidden, self.block_tables, e.model.w["embed"], self.bs)
+            return
         if self.dist_greedy:
             nxt = e.tp.greedy_gather(logits, e.cfg.vocab)
         else:
-            nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets)
+            nxt = ops.sample(logits.contiguous(), self.temp, self.top_p, self.top_k, self.seeds, offsets,
+                             ws=self.sample_ws)
         # one epilogue launch: record ids, advance positions / lengths / step (+ next step's prep)
         if fused:
             ops.decode_advance(self.out, self.input_ids, self.positions, self.ctx_lens, self.step, nxt,

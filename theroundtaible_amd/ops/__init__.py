@@ -377,14 +377,42 @@ def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
     return ref.gelu_tanh(x)
 
 
+def sample_workspace(batch: int, device) -> torch.Tensor:
+    """Zeroed K6 workspace for ``batch`` rows: its arrival tickets re-arm themselves after every
+    launch, so one persistent workspace serves every replay of a captured step (no memset)."""
+    return torch.zeros(native().sample_workspace_floats(batch), dtype=torch.float32, device=device)
+
+
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
-           seeds: torch.Tensor, offsets: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Per-row ``offsets`` (int64, device-resident: the knight's position) keep hipGraph replays deterministic."""
+           seeds: torch.Tensor, offsets: torch.Tensor, out: Optional[torch.Tensor] = None,
+           ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-row ``offsets`` (int64, device-resident: the knight's position) keep hipGraph replays
+    deterministic. ``ws``: a :func:`sample_workspace` (one is zero-allocated per call otherwise)."""
     if _use_native(logits):
         if out is None:
             out = torch.empty(logits.shape[0], dtype=torch.int64, device=logits.device)
         nat = native()
-        ws = torch.empty(nat.sample_workspace_floats(logits.shape[0]), dtype=torch.float32, device=logits.device)
+        if ws is None:
+            ws = sample_workspace(logits.shape[0], logits.device)
         nat.sample(out, logits, temperature, top_p, top_k, seeds, offsets, ws)
         return out
     return ref.sample(logits, temperature, top_p, top_k, seeds, offsets)
+
+
+def sample_advance(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor, top_k: torch.Tensor,
+                   seeds: torch.Tensor, offsets: torch.Tensor, ws: torch.Tensor, nxt: torch.Tensor,
+                   out: torch.Tensor, ids: torch.Tensor, positions: torch.Tensor, ctx_lens: torch.Tensor,
+                   step: torch.Tensor, slots: torch.Tensor, res: torch.Tensor, block_tables: torch.Tensor,
+                   embed: torch.Tensor, block_size: int) -> torch.Tensor:
+    """The captured decode step's K6 sampler fused with :func:`decode_advance` + the next step's
+    :func:`decode_prep` (one launch): samples ``nxt`` from ``logits`` with the RNG ``offsets``, then
+    records it in ``out[step]``, advances ids / positions / lengths / step and writes the next
+    step's K/V slots, ``offsets`` and embedding rows."""
+    if _use_native(logits):
+        native().sample_advance(nxt, logits, temperature, top_p, top_k, seeds, offsets, ws, out, ids, positions,
+                                ctx_lens, step, slots, res, block_tables, embed, int(block_size))
+        return nxt
+    nxt.copy_(ref.sample(logits, temperature, top_p, top_k, seeds, offsets))
+    ref.decode_advance(out, ids, positions, ctx_lens, step, nxt, (slots, offsets, res, block_tables, embed,
+                                                                  block_size))
+    return nxt

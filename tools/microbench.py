@@ -223,7 +223,13 @@ def bench_sample(B):
     seeds = torch.arange(B, device=DEV, dtype=torch.int64)
     offs = torch.zeros(B, device=DEV, dtype=torch.int64)
     out = torch.empty(B, dtype=torch.int64, device=DEV)
-    row(f"sample top-p B={B} V={V}", timed(lambda i: ops.sample(lg, t, tp, tk, seeds, offs, out)), B * V * 2)
+    ws = ops.sample_workspace(B, DEV)
+    row(f"sample top-p B={B} V={V}", timed(lambda i: ops.sample(lg, t, tp, tk, seeds, offs, out, ws=ws)), B * V * 2)
+    tg = torch.zeros(B, device=DEV)
+    row(f"sample greedy B={B} V={V}", timed(lambda i: ops.sample(lg, tg, tp, tk, seeds, offs, out, ws=ws)), B * V * 2)
+    tk40 = torch.full((B,), 40, dtype=torch.int32, device=DEV)
+    row(f"sample top-k 40 (slow path) B={B} V={V}", timed(lambda i: ops.sample(lg, t, tp, tk40, seeds, offs, out, ws=ws)),
+        B * V * 2)
 
 
 def bench_prefill(T):

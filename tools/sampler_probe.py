@@ -1,0 +1,20 @@
+import sys, torch, time
+sys.path.insert(0, '/root/repo')
+from theroundtaible_amd import ops
+DEV='cuda'
+def t(fn, n=20):
+    fn(); torch.cuda.synchronize()
+    a=torch.cuda.Event(enable_timing=True); b=torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n): fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b)*1000/n
+for V in (32000, 128256):
+  for B in (1, 3):
+    lg=(torch.randn(B,V,device=DEV)).to(torch.bfloat16)
+    ws=ops.sample_workspace(B, DEV); out=torch.empty(B,dtype=torch.int64,device=DEV)
+    s=torch.arange(B,device=DEV); o=torch.zeros(B,dtype=torch.int64,device=DEV)
+    T=torch.full((B,),0.8,device=DEV); one=torch.ones(B,device=DEV); k0=torch.zeros(B,dtype=torch.int32,device=DEV)
+    for name,(temp,p,k) in {'greedy':(T*0,one,k0),'unfilt':(T,one,k0),'topp.9':(T,one*0.9,k0),'topp.3':(T,one*0.3,k0),
+                            'topk40':(T,one,k0+40),'topk4000':(T,one,k0+4000)}.items():
+        print(V,B,name, round(t(lambda: ops.sample(lg,temp,p,k,s,o,out,ws=ws)),1))
