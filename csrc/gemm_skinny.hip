@@ -187,8 +187,9 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
 int split_workspace_ints(int max_split_tiles) { return SPLIT_CTRS + max_split_tiles * 2 * SPLIT_STRIDE; }
 
 // Split-K part count for a T-tile, ks-k-step GEMM on `cus` CUs (0 = no split-K): enough parts
-// that T x S reaches `target` workgroups (default 2 per CU), each part >= 8 k-steps, T x S capped
-// by the workspace. RT_SPLITK=<S> pins S (1 = off), RT_SPLITK_TARGET=<wgs> moves the target
+// that T x S reaches `target` workgroups (default one per CU: r03 microbench, Llama-3-8B tp8
+// NORM_ADD shards, qkv 48 tiles 8.70 us unsplit / 8.25 at 1 WG per CU / 11.26 at 2 per CU;
+// profiles/r03/gemm_tp_shards_*.md), each part >= 8 k-steps, T x S capped by the workspace. RT_SPLITK=<S> pins S (1 = off), RT_SPLITK_TARGET=<wgs> moves the target
 // (microbenchmark sweeps; read once per process).
 int splitk_parts(int T, int ks, int cus, int64_t ws_ints) {
   static const int pinned = [] {
@@ -204,7 +205,7 @@ int splitk_parts(int T, int ks, int cus, int64_t ws_ints) {
   if (pinned > 1) {
     S = pinned;
   } else {
-    const int target = target_env > 0 ? target_env : 2 * cus;
+    const int target = target_env > 0 ? target_env : cus;
     S = (target + T - 1) / T;
   }
   S = S < ks / 8 ? S : ks / 8;

@@ -264,6 +264,8 @@ RT_DEVICE int nucleus_by_candidates(const T* row, int V, float mx, float invT, f
   if (kstar < 0) return -1;
   const int cs = s_ord[1 + kstar];
   ArgMax best{s_gv[cs], s_gi[cs]};
+  __shared__ float s_uv[NC], s_us[NC];
+  __shared__ int s_ui[NC];
   // chunks ranked above c* (their bests are outside): any token beating c* must be checked
   for (int q = 0; q <= kstar; ++q) {
     int lo, hi;
@@ -271,14 +273,41 @@ RT_DEVICE int nucleus_by_candidates(const T* row, int V, float mx, float invT, f
     for_range<T, VEC>(row, lo, hi, [&](int i, float v) {
       const float sc = v * invT + gumbel(key, (uint32_t)i);
       if (sc > s_gv[cs] || (sc == s_gv[cs] && i < s_gi[cs])) {
-        if (v >= v_in) am_merge(best, sc, i);
-        else if (v > v_out) s_flag = 1;      // undecided from the known values
+        if (v >= v_in) {
+          am_merge(best, sc, i);
+        } else if (v > v_out) {             // undecided from the known values: test it exactly
+          const int u = atomicAdd(&s_flag, 1);
+          if (u < NC) {
+            s_uv[u] = v;
+            s_us[u] = sc;
+            s_ui[u] = i;
+          }
+        }
       }
     });
   }
   best = block_argmax(best, sv, si);
   __syncthreads();
-  return s_flag ? -1 : best.i;
+  const int nu = s_flag;
+  if (nu > NC) return -1;
+  if (nu > 0) {   // one more pass: the mass above each undecided token
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      cv[k] = k < nu ? s_uv[k] : INFINITY;
+      acc[k] = 0.f;
+    }
+    for_row<T, VEC>(row, V, [&](int, float v) {
+      const float e = __expf((v - mx) * invT);
+#pragma unroll
+      for (int k = 0; k < NC; ++k) acc[k] += v > cv[k] ? e : 0.f;
+    });
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const float m = rt::block_sum(acc[k], red);
+      if (k < nu && m < pz) am_merge(best, s_us[k], s_ui[k]);
+    }
+  }
+  return best.i;
 }
 
 struct SampleArgs {
