@@ -43,7 +43,11 @@ constexpr int W_GV = W_ARG + C;          // [C] chunk best Gumbel score v/T + g
 constexpr int W_GI = W_GV + C;           // [C] its token (int)
 constexpr int W_MIN = W_GI + C;          // [C] chunk min
 constexpr int W_CNT = W_MIN + C;         // arrival ticket (int), re-armed by the decider
-constexpr int W_ROW = W_CNT + 4;         // words per row; after the B rows: the rows-done ticket
+constexpr int W_KB = W_CNT + 4;          // [C] chunk's top histogram bin floor(max / T * BW) (int)
+constexpr int HB = 128;                  // histogram bins per chunk (the last one: everything lower)
+constexpr float BW = 16.f;               // bins per unit of z = logit / T
+constexpr int W_HIST = W_KB + C;         // [C][HB] chunk mass per bin, relative to the chunk max
+constexpr int W_ROW = W_HIST + C * HB;   // words per row; after the B rows: the rows-done ticket
 
 RT_DEVICE uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -352,7 +356,8 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   __shared__ int si[NWV];
   __shared__ float s_max[C], s_gv[C], s_min[C];
   __shared__ int s_arg[C], s_gi[C];
-  __shared__ int s_last, s_res;
+  __shared__ int s_last, s_res, s_kb[C];
+  __shared__ float s_sc[C];
   __shared__ float s_pa, s_pb;
   const int b = blockIdx.x, c = blockIdx.y;
   float* w = a.ws + (size_t)b * W_ROW;
@@ -367,6 +372,14 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const uint64_t key = mix64((uint64_t)a.seeds[b] ^ mix64((uint64_t)off));
   const float invT = temp > 0.f ? 1.f / temp : 0.f;
+  const int k = a.top_k[b];
+  const float p = a.top_p[b];
+  const bool use_k = k > 0 && k < V;
+  // top-p rows (no top-k): every chunk also publishes a histogram of its tokens' mass on a grid
+  // aligned across chunks (bin = floor(logit / T * BW)), which decides the accept test below
+  // without another pass over the row for all but the rows whose j* shares a bin with the cut
+  const bool hist = temp > 0.f && p < 1.f && !use_k;
+  const float sbin = invT * BW;
 
   // ---- 1: chunk records ----
   int lo, hi;
@@ -385,6 +398,32 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     for_range<T, VEC>(row, lo, hi, [&](int i, float v) { am_merge(am, v, i); });
   }
   am = block_argmax(am, sv, si);
+  if (hist) {
+    // second sweep of the (L2-resident) chunk: mass exp((v - chunk max) / T) per bin, integer
+    // LDS atomics in 32.32 fixed point (float LDS atomics serialize on gfx950)
+    const float cmax = am.v;
+    const float ktop = floorf(cmax * sbin);
+    for (int i = threadIdx.x; i < HB; i += NT) hmi[i] = 0ull;
+    __syncthreads();
+    if (cmax > -INFINITY) {
+      for_range<T, VEC>(row, lo, hi, [&](int, float v) {
+        const float e = __expf((v - cmax) * invT);
+        if (e > 0.f) {
+          const float kr = fminf(fmaxf(ktop - floorf(v * sbin), 0.f), (float)(HB - 1));
+          atomicAdd(&hmi[(int)kr], (unsigned long long)(e * 4294967296.f));
+        }
+      });
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < HB; i += NT)
+      __hip_atomic_store(&w[W_HIST + c * HB + i], (float)(hmi[i] >> 8) * (1.f / 16777216.f), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&wi[W_KB + c], cmax > -INFINITY ? (int)ktop : -(1 << 30), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every thread's histogram stores complete before thread 0's ticket
+  }
   if (threadIdx.x == 0) {
     __hip_atomic_store(&w[W_MIN + c], mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&w[W_MAX + c], am.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,9 +456,6 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     rmin = fminf(rmin, s_min[j]);
   }
   const float mx = ra.v;
-  const int k = a.top_k[b];
-  const float p = a.top_p[b];
-  const bool use_k = k > 0 && k < V;
   int tok;
   if (!(temp > 0.f)) {
     tok = ra.i;
@@ -430,16 +466,52 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     int cand = -1;
     if (!use_k && g.i >= 0 && g.i < V) {   // fast path: is j* inside the nucleus?
       const float vj = rt::DT<T>::load(row + g.i);
-      float above = 0.f, total = 0.f;
-      for_row<T, VEC>(row, V, [&](int, float v) {
-        const float e = __expf((v - mx) * invT);
-        total += e;
-        above += v > vj ? e : 0.f;
-      });
-      above = rt::block_sum(above, red);
-      total = rt::block_sum(total, red);
-      accepted = above < p * total;
-      if (!accepted && a.probe == 0) cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, p * total, vj, key, s_gv,
+      // bounds on the mass strictly above j* from the chunk histograms: bins above j*'s bin are
+      // above it, its own bin (and a chunk's open-ended last bin reaching it) may or may not be
+      const float kj = floorf(vj * sbin);
+      float lo_m = 0.f, mid_m = 0.f, tot_m = 0.f;
+      if (threadIdx.x < C) {
+        const int j = threadIdx.x;
+        s_kb[j] = __hip_atomic_load(&wi[W_KB + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_sc[j] = __expf((s_max[j] - mx) * invT);
+      }
+      __syncthreads();
+      float hv[C * HB / NT];
+#pragma unroll
+      for (int q = 0; q < C * HB / NT; ++q)
+        hv[q] = __hip_atomic_load(&w[W_HIST + threadIdx.x + q * NT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int q = 0; q < C * HB / NT; ++q) {
+        const int e = threadIdx.x + q * NT, cc = e / HB, kk = e - cc * HB;
+        const float m = hv[q] * s_sc[cc];
+        const float kb = (float)(s_kb[cc] - kk);   // this bin's grid index (the last bin: its top)
+        tot_m += m;
+        if (kk < HB - 1) {
+          lo_m += kb > kj ? m : 0.f;
+          mid_m += kb == kj ? m : 0.f;
+        } else {
+          mid_m += kb >= kj ? m : 0.f;
+        }
+      }
+      lo_m = rt::block_sum(lo_m, red);
+      mid_m = rt::block_sum(mid_m, red);
+      tot_m = rt::block_sum(tot_m, red);
+      float pz = p * tot_m;
+      bool decided = lo_m + mid_m < pz || lo_m >= pz;
+      accepted = lo_m + mid_m < pz;
+      if (!decided) {   // j* shares its bin with the cut: the exact test, one pass
+        float above = 0.f, total = 0.f;
+        for_row<T, VEC>(row, V, [&](int, float v) {
+          const float e = __expf((v - mx) * invT);
+          total += e;
+          above += v > vj ? e : 0.f;
+        });
+        above = rt::block_sum(above, red);
+        total = rt::block_sum(total, red);
+        pz = p * total;
+        accepted = above < pz;
+      }
+      if (!accepted && a.probe == 0) cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, pz, vj, key, s_gv,
                                                                           s_gi, sv, si, red);
     }
     if (accepted || cand >= 0 || a.probe == 1) {

@@ -359,7 +359,7 @@ def test_sample_advance_equals_sample_then_advance(mode):
     wsi = ws.view(torch.int32)
     assert int(wsi[-4]) == 0                                       # rows-done ticket re-armed
     row = (ws.numel() - 4) // B
-    assert all(int(wsi[b * row + row - 4]) == 0 for b in range(B))   # row tickets re-armed
+    assert all(int(wsi[b * row + 5 * 32]) == 0 for b in range(B))   # row tickets (W_CNT) re-armed
 
 
 def test_paging_guard_matches_reference():
