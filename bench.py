@@ -75,6 +75,8 @@ def parse():
     p.add_argument("--layout", default="shared", choices=["shared", "append", "reference"],
                    help="prompt layout; 'shared' (default) keeps ONE copy of a table's common prefix KV per GPU, "
                         "read once per decode step for all of the table's knights there (grouped K3)")
+    p.add_argument("--c1-events", default="",
+                   help="write each rank's C1 event log (name, CLOCK_MONOTONIC ns) to <path>.r<rank>.json")
     p.add_argument("--placement", default="packed", choices=["packed", "striped"],
                    help="packed (default): a table's knights share one GPU group (batched decode + shared prefix "
                         "KV); striped: knight j of table t on group (kpt*t + j) mod groups (every response "
@@ -110,6 +112,20 @@ def _self_launch(args) -> int:
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.run(cmd, env=env).returncode
+
+
+def _overlap_order_ok(events) -> bool:
+    """Every speculative prefill ran while a C1 all-gather was in flight (after its start,
+    before its wait)."""
+    open_ = False
+    for e in events:
+        if e == "c1_start":
+            open_ = True
+        elif e == "c1_wait":
+            open_ = False
+        elif e == "speculate" and not open_:
+            return False
+    return True
 
 
 def main() -> int:
@@ -298,6 +314,10 @@ def main() -> int:
                    "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),
                    "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "c1_skipped_batches": getattr(pool, "c1_skipped", 0),
+                   "c1_device_assembled": pool.exchange.device_path if pool.exchange is not None else 0,
+                   "speculative_prefill_tokens_rank0": engine.stats.get("speculative_tokens", 0),
+                   "c1_speculations_rank0": pool.events.count("speculate"),
+                   "c1_overlap_order_ok": _overlap_order_ok(pool.events),
                    "engine_load_s": round(load_s, 2),
                    "resident_tokens_rank0": sum(s.length for s in engine.kv.seqs.values()),
                    "kv_blocks_used_rank0": engine.kv.num_blocks - engine.kv.alloc.num_free,
@@ -310,6 +330,9 @@ def main() -> int:
                    "engine_decode_ms_per_round": round(sum(dec_ms.values()) / n_timed, 2),
                    "host_ms_per_round": round(ms_round - sum(eng_ms.values()) / n_timed, 2)},
     }
+    if args.c1_events:
+        with open(f"{args.c1_events}.r{cl.rank}.json", "w") as f:
+            json.dump({"rank": cl.rank, "events": pool.events, "ns": pool.event_ns}, f)
     if cl.rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

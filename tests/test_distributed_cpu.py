@@ -384,3 +384,31 @@ def test_ranks_needed_from_placement(tmp_path):
     _tp_project(tmp_path, {"A": {"tp": 4}, "B": {"gpus": [5]}, "C": {}})
     n, why, cpu = ranks_needed(load_config(str(tmp_path)))
     assert n == 6 and "A tp=4" in why and cpu
+
+
+def test_c1_overlaps_speculative_prefill_striped():
+    """in a striped table (knights on different ranks) each rank prefills what it
+    already knows of the next round's shared prompt (its own finished entries at the head of the
+    speaking order) WHILE the C1 all-gather of the other ranks' replies is in flight; the next
+    round keeps that KV by LCP. Pinned: the order c1_start < speculate < c1_wait, speculative
+    tokens were prefilled, and the transcripts equal a run without speculation."""
+    on = _bench(2, ("--scaling", "weak", "--placement", "striped", "--temperature", "0.8"))
+    env_off = dict(os.environ, ROUNDTABLE_C1_SPECULATE="0")
+    old = os.environ.get("ROUNDTABLE_C1_SPECULATE")
+    os.environ["ROUNDTABLE_C1_SPECULATE"] = "0"
+    try:
+        off = _bench(2, ("--scaling", "weak", "--placement", "striped", "--temperature", "0.8"))
+    finally:
+        if old is None:
+            os.environ.pop("ROUNDTABLE_C1_SPECULATE", None)
+        else:
+            os.environ["ROUNDTABLE_C1_SPECULATE"] = old
+    del env_off
+    d_on, d_off = on["detail"], off["detail"]
+    assert d_on["failed_turns"] == 0 and d_off["failed_turns"] == 0
+    assert d_on["c1_overlap_order_ok"] is True
+    assert d_on["c1_speculations_rank0"] > 0 and d_on["speculative_prefill_tokens_rank0"] > 0
+    assert d_off["c1_speculations_rank0"] == 0 and d_off["speculative_prefill_tokens_rank0"] == 0
+    assert d_on["transcript_sha"] == d_off["transcript_sha"]
+    # the speculated KV was reused: the turns themselves prefilled fewer tokens
+    assert d_on["prefill_tokens"] < d_off["prefill_tokens"]

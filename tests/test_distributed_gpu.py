@@ -125,3 +125,24 @@ def test_rccl_data_plane_single_rank():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["ok"] and rec["backend"] == "nccl" and rec["checks"] >= 9 and rec["ranks_ok"] == 1, rec
+
+
+def test_c1_speculative_prefill_striped_on_shared_gpu():
+    """VERDICT r2 #6 on the GPU: a 2-rank striped table; the C1 token buffer is assembled from
+    the decode graph's device buffer (no host staging) and each rank prefills the next round's
+    known prefix while the exchange is in flight. Same transcript as without speculation."""
+    on = _bench(("--scaling", "weak", "--placement", "striped"))
+    d = on["detail"]
+    assert d["failed_turns"] == 0 and d["c1_overlap_order_ok"] is True, on["_log"]
+    assert d["c1_speculations_rank0"] > 0 and d["speculative_prefill_tokens_rank0"] > 0, on["_log"]
+    old = os.environ.get("ROUNDTABLE_C1_SPECULATE")
+    os.environ["ROUNDTABLE_C1_SPECULATE"] = "0"
+    try:
+        off = _bench(("--scaling", "weak", "--placement", "striped"))
+    finally:
+        if old is None:
+            os.environ.pop("ROUNDTABLE_C1_SPECULATE", None)
+        else:
+            os.environ["ROUNDTABLE_C1_SPECULATE"] = old
+    assert off["detail"]["speculative_prefill_tokens_rank0"] == 0
+    assert d["transcript_sha"] == off["detail"]["transcript_sha"]

@@ -91,6 +91,7 @@ class TurnOutput:
     ids: List[int]
     metrics: Dict[str, float]
     error: Optional[BaseException] = None
+    dev_ids: Optional[torch.Tensor] = None    # ``ids`` on the engine's device (None: host only)
 
 
 def _dtype(s: str) -> torch.dtype:
@@ -144,7 +145,8 @@ class Engine:
         self.max_recoveries = 3
         self._recoveries = 0
         self._dead = False
-        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0}
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0,
+                      "speculative_tokens": 0}
         self._calls = 0
         self.faults = dict(ecfg.faults)
         for item in filter(None, os.environ.get("ROUNDTABLE_ENGINE_FAULTS", "").split(",")):
@@ -316,6 +318,33 @@ class Engine:
             s.blocks.append(shared.blocks[i])
         s.tokens[:] = shared.tokens[:nblocks * bs]     # a referenced shared block is always full
         return nblocks * bs
+
+    @torch.no_grad()
+    def warm_shared(self, prompt: PromptLike) -> int:
+        """Prefill the shared part of a PREDICTED next prompt into its table's shared sequence
+        ahead of the turn (the C1 overlap, knights/distributed.py): the real turn's
+        ``sync_shared`` keeps it by LCP, a wrong guess is rolled back the same way. KV only, no
+        logits are used. Tensor-parallel engines never speculate (their ranks would have to
+        agree on it). Returns the tokens prefilled."""
+        key = getattr(prompt, "shared_key", None)
+        if key is None or not self.healthy or self.tp.size > 1:
+            return 0
+        ids, n = self.encode_prompt_split(prompt)
+        if n <= 0:
+            return 0
+        with self._on_stream():
+            sq, delta = self.sync_shared(key, ids[:n])
+            if not delta:
+                return 0
+            try:
+                with trace.range(f"speculative shared prefill {len(delta)}"):
+                    self.prefill_reserved([self.reserve(sq, delta)])
+            except KVCacheOOM:
+                self.kv.truncate(sq, len(ids[:n]) - len(delta))
+                return 0
+        self.stats["speculative_tokens"] += len(delta)
+        self.stats["prefill_tokens"] += len(delta)
+        return len(delta)
 
     def release(self, key: str) -> None:
         self.kv.free_seq(key)
@@ -590,7 +619,8 @@ class Engine:
         self.check_device_flags()
         outs = []
         seen = set()
-        for t, s, g, n, d, key, nf in zip(turns, seqs, gen, reused, deltas, keys, forced):
+        dev_gen = getattr(self, "_dev_gen", None) or [None] * len(turns)
+        for t, s, g, n, d, key, nf, dg in zip(turns, seqs, gen, reused, deltas, keys, forced, dev_gen):
             text = self.tokenizer.decode(g)
             spre = 0
             if key is not None and key not in seen:     # the group's shared prefill, counted once
@@ -601,7 +631,8 @@ class Engine:
                 "shared_tokens": sh_blocks.get(key, 0) * self.kv.block_size if key is not None else 0,
                 "decode_tokens": len(g) - nf, "forced_tokens": nf, "prefill_ms": (t1 - t0) * 1e3,
                 "decode_ms": (t2 - t1) * 1e3, "decode_tok_s": (len(g) - nf) / max(t2 - t1, 1e-9), "batch": len(turns),
-                "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3, "tp": self.tp.size}))
+                "resident_tokens": s.length, "turn_ms": (t2 - t_start) * 1e3, "tp": self.tp.size},
+                dev_ids=dg if nf == 0 else None))   # forced tails exist only on the host
         self.stats["prefill_tokens"] += sum(len(d) for d in deltas) + sum(shared_pre.values())
         self.stats["decode_tokens"] += sum(len(g) for g in gen) - sum(forced)
         self.stats["prefill_s"] += t1 - t0
@@ -784,9 +815,12 @@ class Engine:
         with trace.range(f"decode B={B} steps={steps}"):
             if runner is not None:
                 toks = runner.run(self, seqs, turns, first, steps, deadline, eos, groups)
+                dev_toks = runner.last_dev
             else:
                 toks = self._decode_eager(seqs, turns, first, steps, deadline, eos, groups)
+                dev_toks = None
         gen: List[List[int]] = []
+        self._dev_gen: List[Optional[torch.Tensor]] = []
         for b, (s, t) in enumerate(zip(seqs, turns)):
             g = toks[b][:max_new[b]]
             if not t.params.ignore_eos:
@@ -794,6 +828,9 @@ class Engine:
             if t.params.stop_on_consensus:
                 g = _cut_at_consensus(self.tokenizer, g)
             gen.append(g)
+            # the kept ids are a prefix of the sampled ones: their device copy is a slice
+            self._dev_gen.append(dev_toks[b, :len(g)] if dev_toks is not None and len(g) <= dev_toks.shape[1]
+                                 else torch.tensor(g, dtype=torch.int64).to(self.device, non_blocking=True))
             # resident KV = prompt + the tokens actually kept (the last one's K/V is not computed yet)
             # resident = prompt + kept tokens except the last (its K/V was never computed)
             s.tokens.extend(g)

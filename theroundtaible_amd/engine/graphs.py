@@ -224,5 +224,8 @@ class DecodeGraph:
         if engine.debug_checks:
             self.check_guard()
         n = done_at - 1
+        # the same ids kept on the device, [B, n + 1] (C1 all-gathers them without host staging);
+        # a copy: the next turn's replays overwrite ``out``
+        self.last_dev = torch.cat([first[:B].view(1, B), self.out[:n, :B]], 0).t().contiguous()
         got = self.out[:n, :B].t().tolist() if n > 0 else [[] for _ in range(B)]
         return [[f] + g for f, g in zip(first_host, got)]

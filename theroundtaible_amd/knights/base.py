@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import threading
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Union
 
 from ..consensus import parse_consensus
 from ..prompt import PromptLike
@@ -27,6 +27,10 @@ class TurnRequest:
     prompt: PromptLike
     round: int = 0
     max_new_tokens: Optional[int] = None
+    # optional: seq_key -> TurnResult of the turns already finished HERE  ->  the table's next
+    # prompt as far as those results determine it (or None). A distributed pool calls it while
+    # the C1 exchange of the remote results is in flight and prefetches that prefix.
+    speculate: Optional[Callable[[Dict[str, "TurnResult"]], Optional[PromptLike]]] = None
 
 
 @dataclass
@@ -35,6 +39,8 @@ class TurnResult:
     ids: Optional[List[int]] = None
     tokenizer: Optional[str] = None
     metrics: Dict[str, Any] = field(default_factory=dict)
+    # the same ids as a tensor on the engine's device (C1 all-gathers it without host staging)
+    dev_ids: Optional[Any] = None
 
 
 class KnightBackend:

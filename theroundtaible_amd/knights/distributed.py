@@ -15,6 +15,7 @@ speaker's group computes while the others wait in the collective.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple, Union  # noqa: F401
 
@@ -36,6 +37,9 @@ class DistributedPool:
         self.tokenizer = tokenizer
         self.exchange_ms: List[float] = []
         self.exchange: Optional[TokenExchange] = None
+        self.events: List[str] = []     # C1 ordering record (c1_start / speculate / c1_wait)
+        self.event_ns: List[int] = []   # CLOCK_MONOTONIC ns of each event (the kernel-trace clock)
+        self.speculate = os.environ.get("ROUNDTABLE_C1_SPECULATE", "1") != "0"
         if cluster.distributed:
             led = [sum(1 for r in placement.values() if r[0] == k) for k in range(cluster.world)]
             self.exchange = TokenExchange(cluster, max(led), max_reply_tokens, cluster.device)
@@ -45,6 +49,46 @@ class DistributedPool:
 
     def leader(self, name: str) -> int:
         return self.placement[name][0]
+
+    def _speculate(self, pairs, local_res, mine_idx) -> None:
+        """C1 overlap: while the remote replies are in flight, ask each table's predictor
+        (``TurnRequest.speculate``, set by the orchestrator) for its next prompt as far as THIS
+        rank's finished turns determine it, and prefill that prefix on every local engine hosting
+        one of the table's knights (``KnightBackend.prefetch`` -> ``Engine.warm_shared``). The
+        next turn keeps the prefilled KV by LCP; a wrong guess costs only the prefill.
+        ROUNDTABLE_C1_SPECULATE=0 disables it."""
+        if not self.speculate:
+            return
+        local_ok = {pairs[i][1].seq_key: local_res[i] for i in mine_idx
+                    if i in local_res and not isinstance(local_res[i], BaseException)}
+        preds: Dict[int, tuple] = {}
+        for i in mine_idx:
+            f = getattr(pairs[i][1], "speculate", None)
+            if f is not None:
+                preds.setdefault(id(f), (f, []))[1].append(i)
+        for f, idxs in preds.values():
+            try:
+                prompt = f(local_ok)
+            except Exception:  # noqa: BLE001 - a failed guess only loses the overlap
+                prompt = None
+            if prompt is None:
+                continue
+            self._event("speculate")
+            done = set()
+            for i in idxs:
+                b = self.local[pairs[i][0].knight_name]
+                if b.group_key() in done:
+                    continue
+                done.add(b.group_key())
+                with trace.range("C1 overlap: speculative prefill"):
+                    b.prefetch(pairs[i][1].seq_key, prompt)
+            self._event("speculate_end")
+
+    def _event(self, name: str) -> None:
+        self.events.append(name)
+        self.event_ns.append(time.monotonic_ns())
+        if len(self.events) > 4096:
+            del self.events[:1024], self.event_ns[:1024]
 
     def execute_round(self, pairs: Sequence[Tuple["RemoteKnight", TurnRequest]],
                       timeout_s: float) -> List[Union[TurnResult, BaseException]]:
@@ -82,23 +126,29 @@ class DistributedPool:
                 has_ids = o.ids is not None
                 meta[i] = ("ok", None if has_ids else o.text, o.tokenizer, o.metrics)
                 if has_ids:
-                    ids_contrib.append((i, list(o.ids)))
+                    ids_contrib.append((i, list(o.ids), getattr(o, "dev_ids", None)))
         with trace.range("C1 exchange"):
             ex = self.exchange
             if ex is None:
+                self._speculate(pairs, local_res, mine_idx)
                 all_meta = self.cluster.all_gather_object(meta)
-                all_ids = exchange_token_ids(self.cluster, ids_contrib, self.cluster.device)
+                all_ids = exchange_token_ids(self.cluster, [c[:2] for c in ids_contrib], self.cluster.device)
             else:
-                # the static-shape token all-gather (RCCL) is in flight while the gloo metadata
-                # round runs; a rank whose replies overflow the static buffers says so in its
-                # metadata and every rank then joins the shape-agreeing fallback (collective)
+                # the static-shape token all-gather (RCCL, from the device token buffers) is in
+                # flight while this rank prefills what it already knows of the next prompt and
+                # the gloo metadata round runs; a rank whose replies overflow the static buffers
+                # says so in its metadata and every rank then joins the shape-agreeing fallback
                 fits = ex.fits(ids_contrib)
                 ex.start(ids_contrib if fits else [])
+                self._event("c1_start")
+                self._speculate(pairs, local_res, mine_idx)
                 meta[-1] = not fits
                 all_meta = self.cluster.all_gather_object(meta)
                 all_ids = ex.wait()
+                self._event("c1_wait")
                 if any(m.get(-1) for m in all_meta):
-                    all_ids.update(exchange_token_ids(self.cluster, [] if fits else ids_contrib, self.cluster.device))
+                    all_ids.update(exchange_token_ids(self.cluster, [] if fits else [c[:2] for c in ids_contrib],
+                                                      self.cluster.device))
         self.exchange_ms.append((time.perf_counter() - t0) * 1e3)
         merged: Dict[int, tuple] = {}
         for m in all_meta:

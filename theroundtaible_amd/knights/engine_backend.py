@@ -63,11 +63,16 @@ class EngineBackend(KnightBackend):
             if o.error is not None:
                 res.append(o.error)
             else:
-                res.append(TurnResult(o.text, o.ids, self.engine.tokenizer.family, dict(o.metrics)))
+                res.append(TurnResult(o.text, o.ids, self.engine.tokenizer.family, dict(o.metrics), o.dev_ids))
         return res
 
     def execute_many(self, reqs: Sequence[TurnRequest], timeout_s: float):
         return self.execute_group([(self, r) for r in reqs], timeout_s)
+
+    def prefetch(self, seq_key: str, prompt_prefix) -> None:
+        """Prefill the shared (table) part of a predicted next prompt now (Engine.warm_shared)."""
+        with self.lock:
+            self.engine.warm_shared(prompt_prefix)
 
     def release(self, seq_key: str) -> None:
         with self.lock:

@@ -310,15 +310,49 @@ class Orchestrator:
         visible = list(self.all_rounds)
         files, cmds = self.tool_state["files"], self.tool_state["commands"]
         plan = []
+        predict = self._next_prompt_predictor(rnd, order)
         for knight in order:
             backend = self.backends.get(knight.adapter)
             if backend is None:
                 self.ui.warn(f"  {knight.name} didn't show up today. Typical.")
                 continue
             prompt = self._prompt(knight, self.ctx, visible, rnd, self.cont is not None, files, cmds)
-            plan.append((knight, backend, TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens)))
+            plan.append((knight, backend, TurnRequest(self.table_id + knight.name, prompt, rnd, self.opt.max_new_tokens,
+                                                      speculate=predict)))
         self.store.update_status(self.session_path, phase="discussing", current_knight=None, round=rnd)
         return plan
+
+    def _next_prompt_predictor(self, rnd: int, order: Sequence[KnightConfig]):
+        """``shared`` layout: a function from the turns of this round finished so far (on one
+        rank) to the table's round-``rnd + 1`` prompt as far as they determine it — the
+        transcript plus this round's entries up to the first one not known yet, rendered exactly
+        as :meth:`_record` will append them (entry header, reply ids, consensus annotation; an
+        entry that triggers tool results ends the known part). A distributed pool prefills that
+        shared prefix while the other ranks' replies are in flight (C1 overlap)."""
+        if self.layout != "shared":
+            return None
+        transcript = list(self.transcript)
+
+        def predict(done: Dict[str, TurnResult]) -> Optional[Prompt]:
+            segs = list(transcript)
+            n = 0
+            for knight in order:
+                res = done.get(self.table_id + knight.name)
+                backend = self.backends.get(knight.adapter)
+                if res is None or backend is None or isinstance(res, BaseException):
+                    break
+                consensus = backend.parse_consensus(res.text, rnd)
+                entry = RoundEntry(knight=knight.name, round=rnd, response=res.text, consensus=consensus,
+                                   timestamp="", metrics={})
+                segs.extend(transcript_entry_segments(entry, res.ids, res.tokenizer))
+                n += 1
+                if consensus is not None and (consensus.file_requests or consensus.verify_commands):
+                    break
+            if n == 0:
+                return None
+            return build_turn_prompt_shared(order[0], self.config.knights, self.ctx, segs, rnd + 1,
+                                            shared_key=self.table_id + "@table")
+        return predict
 
     def record_parallel(self, rnd: int, order: Sequence[KnightConfig],
                         results: Dict[str, Union[TurnResult, BaseException]]) -> None:
