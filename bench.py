@@ -316,6 +316,7 @@ def main() -> int:
                    "exchange_ms_per_round": round(exch, 3), "c1_skipped_batches": getattr(pool, "c1_skipped", 0),
                    "c1_device_assembled": pool.exchange.device_path if pool.exchange is not None else 0,
                    "speculative_prefill_tokens_rank0": engine.stats.get("speculative_tokens", 0),
+                   "speculative_kept_tokens_rank0": engine.stats.get("speculative_kept", 0),
                    "c1_speculations_rank0": pool.events.count("speculate"),
                    "c1_overlap_order_ok": _overlap_order_ok(pool.events),
                    "engine_load_s": round(load_s, 2),

@@ -408,6 +408,9 @@ def test_c1_overlaps_speculative_prefill_striped():
     assert d_on["failed_turns"] == 0 and d_off["failed_turns"] == 0
     assert d_on["c1_overlap_order_ok"] is True
     assert d_on["c1_speculations_rank0"] > 0 and d_on["speculative_prefill_tokens_rank0"] > 0
+    # every speculated token was the real next prompt's (kept by LCP; none rolled back) — except
+    # in the last round, whose speculation no later turn consumes
+    assert 0 < d_on["speculative_kept_tokens_rank0"] <= d_on["speculative_prefill_tokens_rank0"]
     assert d_off["c1_speculations_rank0"] == 0 and d_off["speculative_prefill_tokens_rank0"] == 0
     assert d_on["transcript_sha"] == d_off["transcript_sha"]
     # the speculated KV was reused: the turns themselves prefilled fewer tokens

@@ -146,7 +146,7 @@ class Engine:
         self._recoveries = 0
         self._dead = False
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0,
-                      "speculative_tokens": 0}
+                      "speculative_tokens": 0, "speculative_kept": 0}
         self._calls = 0
         self.faults = dict(ecfg.faults)
         for item in filter(None, os.environ.get("ROUNDTABLE_ENGINE_FAULTS", "").split(",")):
@@ -295,6 +295,10 @@ class Engine:
             self.kv.free_seq(old)
         s = self.kv.seq(sk)
         n = lcp(s.tokens, shared)
+        spec = self.__dict__.setdefault("_spec_pred", {}).pop(sk, None)
+        if spec is not None:   # how much of a speculative prefill the real prompt kept
+            base, pred = spec
+            self.stats["speculative_kept"] += max(0, min(n, len(pred)) - base)
         self.kv.truncate(s, n)
         return s, shared[n:]
 
@@ -336,6 +340,7 @@ class Engine:
             sq, delta = self.sync_shared(key, ids[:n])
             if not delta:
                 return 0
+            self._spec_pred[self.shared_seq_key(key)] = (n - len(delta), ids[:n])
             try:
                 with trace.range(f"speculative shared prefill {len(delta)}"):
                     self.prefill_reserved([self.reserve(sq, delta)])

@@ -49,8 +49,10 @@ def windows(ev):
 
 
 def short(name):
-    name = name.split("(")[0]
-    return name[:48]
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    for sep in ("<", "("):
+        name = name.split(sep)[0]
+    return name[:40]
 
 
 def main(argv):
