@@ -100,9 +100,9 @@ class TPInfo:
         if self.size == 1:
             return pair[:, 1].long()
         src = pair.cpu() if self._host_staged(local) else pair
-        parts = [torch.empty_like(src) for _ in range(self.size)]
-        dist.all_gather(parts, src, group=self.group)
-        g = torch.stack(parts).to(local.device)            # [tp, B, 2]
+        flat = src.new_empty((self.size * B, 2))
+        dist.all_gather_into_tensor(flat, src, group=self.group)   # one collective, no per-rank copies
+        g = flat.view(self.size, B, 2).to(local.device)    # [tp, B, 2]
         best = g[..., 0].argmax(dim=0)                     # first max = lowest rank = lowest id
         return g[best, torch.arange(B, device=local.device), 1].long()
 
@@ -120,9 +120,12 @@ class TPInfo:
         if self.size == 1:
             return x
         src = x.contiguous().cpu() if self._host_staged(x) else x.contiguous()
-        parts: List[torch.Tensor] = [torch.empty_like(src) for _ in range(self.size)]
-        dist.all_gather(parts, src, group=self.group)
-        return torch.cat(parts, dim=-1).to(x.device)
+        # ONE all-gather into a [tp, rows, shard] buffer and ONE permuting copy (a list-output
+        # all_gather + cat costs a copy kernel per rank on top, inside every decode step)
+        flat = src.new_empty((self.size * src.shape[0],) + tuple(src.shape[1:]))
+        dist.all_gather_into_tensor(flat, src, group=self.group)
+        out = flat.view(self.size, *src.shape).movedim(0, -2).reshape(*src.shape[:-1], self.size * src.shape[-1])
+        return out.to(x.device)
 
 
 class SimulatedTP(TPInfo):
