@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   __shared__ int si[NWV];
   __shared__ float s_max[C], s_gv[C], s_min[C];
   __shared__ int s_arg[C], s_gi[C];
-  __shared__ int s_last, s_res, s_kb[C];
+  __shared__ int s_last, s_res, s_kb[C], s_lump, s_rescan_c[C];
   __shared__ float s_sc[C];
   __shared__ float s_pa, s_pb;
   const int b = blockIdx.x, c = blockIdx.y;
@@ -511,8 +511,75 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
         pz = p * total;
         accepted = above < pz;
       }
-      if (!accepted && a.probe == 0) cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, pz, vj, key, s_gv,
-                                                                          s_gi, sv, si, red);
+      if (!accepted && a.probe == 0) {
+        // rejected j*: the nucleus cut from the SAME histograms, merged on the common z grid
+        // (bin g = kmax - floor(v / T * BW), 0 = top). With the crossing bin g*, tokens in bins
+        // above it are inside the nucleus, below it outside, in it undecided. A chunk's best
+        // Gumbel token inside the nucleus is its best allowed one; chunks whose best is not are
+        // rescanned (tokens above g* only). Exact unless an undecided token (bin g*, or an
+        // open-ended last bin reaching g*) could win: then the candidate / histogram paths.
+        int kmx = -(1 << 30);
+        for (int j = 0; j < C; ++j) kmx = max(kmx, s_kb[j]);
+        for (int i = threadIdx.x; i < NB; i += NT) hmi[i] = 0ull;
+        if (threadIdx.x == 0) s_lump = NB;
+        __syncthreads();
+        for (int q = 0; q < C * HB / NT; ++q) {   // re-read (L2): hv is not kept live across the passes
+          const int e = threadIdx.x + q * NT, cc = e / HB, kk = e - cc * HB;
+          const float m = __hip_atomic_load(&w[W_HIST + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * s_sc[cc];
+          const int gb = kmx - (s_kb[cc] - kk);
+          if (m > 0.f) {
+            if (kk == HB - 1 || gb >= NB) atomicMin(&s_lump, min(gb, NB - 1));   // open-ended: its top
+            else atomicAdd(&hmi[gb], (unsigned long long)(m * 4294967296.f));
+          }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < NB; i += NT) {
+          hc[i] = 0.f;
+          hm[i] = (float)(hmi[i] >> 8) * (1.f / 16777216.f);
+        }
+        __syncthreads();
+        const int gst = first_crossing(hc, hm, 3.0e38f, pz, red, &s_res, &s_pa, &s_pb);
+        if (gst < NB && s_lump > gst) {
+          if (threadIdx.x < C) {
+            const int j = threadIdx.x, gi = s_gi[j];
+            const int gb = (gi >= 0 && gi < V) ? kmx - (int)floorf(rt::DT<T>::load(row + gi) * sbin) : NB;
+            s_rescan_c[j] = gb < gst ? 0 : 1;
+          }
+          __syncthreads();
+          ArgMax win{-INFINITY, 0x7fffffff}, amb{-INFINITY, 0x7fffffff};
+          for (int j = 0; j < C; ++j)
+            if (!s_rescan_c[j]) am_merge(win, s_gv[j], s_gi[j]);   // every thread: same merge order
+          for (int j = 0; j < C; ++j) {
+            if (!s_rescan_c[j]) continue;
+            int clo, chi;
+            chunk_range(V, j, clo, chi);
+            // two accumulators updated by selects (a branch choosing one of two structs makes the
+            // compiler address them through scratch)
+            float wv = win.v, av = amb.v;
+            int wi = win.i, ai = amb.i;
+            for_range<T, VEC>(row, clo, chi, [&](int i, float v) {
+              const int gb = kmx - (int)floorf(v * sbin);
+              if (gb <= gst) {
+                const float sc = v * invT + gumbel(key, (uint32_t)i);
+                const bool in = gb < gst;
+                const bool bw = in && (sc > wv || (sc == wv && i < wi));
+                const bool ba = !in && (sc > av || (sc == av && i < ai));
+                wv = bw ? sc : wv;
+                wi = bw ? i : wi;
+                av = ba ? sc : av;
+                ai = ba ? i : ai;
+              }
+            });
+            win = ArgMax{wv, wi};
+            amb = ArgMax{av, ai};
+          }
+          win = block_argmax(win, sv, si);
+          amb = block_argmax(amb, sv, si);
+          if (win.i != 0x7fffffff && (amb.v < win.v || (amb.v == win.v && amb.i > win.i))) cand = win.i;
+        }
+        if (cand < 0)
+          cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, pz, vj, key, s_gv, s_gi, sv, si, red);
+      }
     }
     if (accepted || cand >= 0 || a.probe == 1) {
       tok = accepted ? g.i : (cand >= 0 ? cand : ra.i);

@@ -18,3 +18,13 @@ for V in (32000, 128256):
     for name,(temp,p,k) in {'greedy':(T*0,one,k0),'unfilt':(T,one,k0),'topp.9':(T,one*0.9,k0),'topp.3':(T,one*0.3,k0),
                             'topk40':(T,one,k0+40),'topk4000':(T,one,k0+4000)}.items():
         print(V,B,name, round(t(lambda: ops.sample(lg,temp,p,k,s,o,out,ws=ws)),1))
+# per-row view of the B=3 top-p launches (fixed seeds: each row takes the same path every call)
+V = 128256
+lg = torch.randn(3, V, device=DEV).to(torch.bfloat16)
+for p_ in (0.9, 0.3):
+    for b in range(3):
+        ws = ops.sample_workspace(1, DEV); out = torch.empty(1, dtype=torch.int64, device=DEV)
+        s = torch.tensor([b], device=DEV); o = torch.zeros(1, dtype=torch.int64, device=DEV)
+        T = torch.full((1,), 0.8, device=DEV); P = torch.full((1,), p_, device=DEV)
+        k0 = torch.zeros(1, dtype=torch.int32, device=DEV)
+        print("row", b, "topp", p_, round(t(lambda: ops.sample(lg[b:b + 1], T, P, k0, s, o, out, ws=ws)), 1))
