@@ -43,7 +43,8 @@ constexpr int W_GV = W_ARG + C;          // [C] chunk best Gumbel score v/T + g
 constexpr int W_GI = W_GV + C;           // [C] its token (int)
 constexpr int W_MIN = W_GI + C;          // [C] chunk min
 constexpr int W_CNT = W_MIN + C;         // arrival ticket (int), re-armed by the decider
-constexpr int W_KB = W_CNT + 4;          // [C] chunk's top histogram bin floor(max / T * BW) (int)
+constexpr int W_SC = W_CNT + 1;          // histogram grid scale for the next launch (float, 0 = default)
+constexpr int W_KB = W_CNT + 4;          // [C] chunk's top histogram bin floor(max * scale) (int)
 constexpr int HB = 128;                  // histogram bins per chunk (the last one: everything lower)
 constexpr float BW = 16.f;               // bins per unit of z = logit / T
 constexpr int W_HIST = W_KB + C;         // [C][HB] chunk mass per bin, relative to the chunk max
@@ -370,16 +371,20 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   // the deciders rewrite offsets / step: every read of them completes before this workgroup's
   // ticket (below), and the deciders write only after every ticket of their row / launch
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const uint64_t key = mix64((uint64_t)a.seeds[b] ^ mix64((uint64_t)off));
-  const float invT = temp > 0.f ? 1.f / temp : 0.f;
+  // grid scale of this row's histograms (bins per logit unit): chosen by the previous launch's
+  // decider from the row's value span (0 before the first launch: the default)
+  const float sgrid = __hip_atomic_load(&w[W_SC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int k = a.top_k[b];
   const float p = a.top_p[b];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read before the ticket: the decider rewrites it
+  const uint64_t key = mix64((uint64_t)a.seeds[b] ^ mix64((uint64_t)off));
+  const float invT = temp > 0.f ? 1.f / temp : 0.f;
   const bool use_k = k > 0 && k < V;
   // top-p rows (no top-k): every chunk also publishes a histogram of its tokens' mass on a grid
-  // aligned across chunks (bin = floor(logit / T * BW)), which decides the accept test below
+  // aligned across chunks (bin = floor(logit * scale)), which decides the accept test below
   // without another pass over the row for all but the rows whose j* shares a bin with the cut
   const bool hist = temp > 0.f && p < 1.f && !use_k;
-  const float sbin = invT * BW;
+  const float sbin = sgrid > 0.f ? sgrid : invT * BW;
 
   // ---- 1: chunk records ----
   int lo, hi;
@@ -714,6 +719,15 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   }
 
   // ---- 3: the token and this row's step bookkeeping ----
+  if (hist && threadIdx.x == 0) {
+    // next launch's grid: HB - 2 bins over the row's span (at most 8 / invT, where the mass
+    // below is < e^-8 of the top token's), so a near-flat distribution (random-init weights)
+    // still spreads over the bins instead of landing in one or two; never so fine that
+    // floor(v * scale) leaves the int range
+    const float span = fmaxf(fminf(mx - rmin, 8.f / invT), 1e-4f);
+    const float sn = fminf((float)(HB - 2) / span, 1e6f / (fabsf(mx) + fabsf(rmin) + 1.f));
+    __hip_atomic_store(&w[W_SC], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (threadIdx.x == 0) {
     a.tok[b] = tok;
     if (a.adv) {
