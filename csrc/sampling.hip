@@ -365,18 +365,49 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   int* wi = reinterpret_cast<int*>(w);
   const T* row = static_cast<const T*>(a.logits) + (size_t)b * a.ld;
   const int V = a.V;
+  int lo, hi;
+  chunk_range(V, c, lo, hi);
+  // this thread's first 16 B of the chunk, requested before the parameter loads (the chunk
+  // pass cannot start until `temperature` arrives; its first round trip overlaps that one)
+  rt::short8 pv{};
+  bool has_pv = false;
+  if constexpr (VEC && sizeof(T) == 2) {
+    if ((int)threadIdx.x < ((hi - lo) >> 3)) {
+      pv = *reinterpret_cast<const rt::short8*>(row + lo + 8 * threadIdx.x);
+      has_pv = true;
+    }
+  }
+  // f(i, v) over the chunk [lo, hi), the preloaded vector first (used by both chunk sweeps)
+  auto for_chunk = [&](auto&& f) {
+    if constexpr (VEC && sizeof(T) == 2) {
+      const int nv = (hi - lo) >> 3;
+      if (has_pv) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f(lo + 8 * (int)threadIdx.x + j, rt::bf2f((uint16_t)pv[j]));
+      }
+      const rt::short8* pp = reinterpret_cast<const rt::short8*>(row + lo);
+      for (int cc = threadIdx.x + NT; cc < nv; cc += NT) {
+        const rt::short8 v = pp[cc];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f(lo + cc * 8 + j, rt::bf2f((uint16_t)v[j]));
+      }
+      for (int i = lo + (nv << 3) + threadIdx.x; i < hi; i += NT) f(i, rt::DT<T>::load(row + i));
+    } else {
+      for_range<T, VEC>(row, lo, hi, f);
+    }
+  };
   const float temp = a.temperature[b];
   const int64_t off = a.offsets[b];
   const int64_t st = a.adv ? *a.step : 0;
-  // the deciders rewrite offsets / step: every read of them completes before this workgroup's
-  // ticket (below), and the deciders write only after every ticket of their row / launch
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // grid scale of this row's histograms (bins per logit unit): chosen by the previous launch's
   // decider from the row's value span (0 before the first launch: the default)
   const float sgrid = __hip_atomic_load(&w[W_SC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int k = a.top_k[b];
   const float p = a.top_p[b];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // read before the ticket: the decider rewrites it
+  // the deciders rewrite offsets / step / the grid scale: every read of them completes before
+  // this workgroup's ticket (below), and the deciders write only after every ticket of their
+  // row / launch (one wait for all the parameter loads)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const uint64_t key = mix64((uint64_t)a.seeds[b] ^ mix64((uint64_t)off));
   const float invT = temp > 0.f ? 1.f / temp : 0.f;
   const bool use_k = k > 0 && k < V;
@@ -387,12 +418,10 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   const float sbin = sgrid > 0.f ? sgrid : invT * BW;
 
   // ---- 1: chunk records ----
-  int lo, hi;
-  chunk_range(V, c, lo, hi);
   ArgMax am{-INFINITY, 0x7fffffff}, gb{-INFINITY, 0x7fffffff};
   float mn = INFINITY;
   if (temp > 0.f) {
-    for_range<T, VEC>(row, lo, hi, [&](int i, float v) {
+    for_chunk([&](int i, float v) {
       am_merge(am, v, i);
       mn = fminf(mn, v);
       am_merge(gb, v * invT + gumbel(key, (uint32_t)i), i);
@@ -400,7 +429,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     gb = block_argmax(gb, sv, si);
     mn = -rt::block_max(-mn, red);
   } else {
-    for_range<T, VEC>(row, lo, hi, [&](int i, float v) { am_merge(am, v, i); });
+    for_chunk([&](int i, float v) { am_merge(am, v, i); });
   }
   am = block_argmax(am, sv, si);
   if (hist) {
@@ -411,7 +440,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     for (int i = threadIdx.x; i < HB; i += NT) hmi[i] = 0ull;
     __syncthreads();
     if (cmax > -INFINITY) {
-      for_range<T, VEC>(row, lo, hi, [&](int, float v) {
+      for_chunk([&](int, float v) {
         const float e = __expf((v - cmax) * invT);
         if (e > 0.f) {
           const float kr = fminf(fmaxf(ktop - floorf(v * sbin), 0.f), (float)(HB - 1));
@@ -444,6 +473,9 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   if (!s_last) return;
 
   // ---- 2: the decider ----
+  // ONE round trip for everything the chunks published: records, grid tops and (top-p rows)
+  // the 4096 histogram words, 8 per thread
+  float hv[C * HB / NT];
   if (threadIdx.x < C) {
     const int j = threadIdx.x;
     s_max[j] = __hip_atomic_load(&w[W_MAX + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -451,6 +483,12 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     s_gv[j] = __hip_atomic_load(&w[W_GV + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_gi[j] = __hip_atomic_load(&wi[W_GI + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_min[j] = __hip_atomic_load(&w[W_MIN + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (hist) s_kb[j] = __hip_atomic_load(&wi[W_KB + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (hist) {
+#pragma unroll
+    for (int q = 0; q < C * HB / NT; ++q)
+      hv[q] = __hip_atomic_load(&w[W_HIST + threadIdx.x + q * NT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   ArgMax ra{-INFINITY, 0x7fffffff}, g{-INFINITY, 0x7fffffff};
@@ -475,16 +513,8 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
       // above it, its own bin (and a chunk's open-ended last bin reaching it) may or may not be
       const float kj = floorf(vj * sbin);
       float lo_m = 0.f, mid_m = 0.f, tot_m = 0.f;
-      if (threadIdx.x < C) {
-        const int j = threadIdx.x;
-        s_kb[j] = __hip_atomic_load(&wi[W_KB + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_sc[j] = __expf((s_max[j] - mx) * invT);
-      }
+      if (threadIdx.x < C) s_sc[threadIdx.x] = __expf((s_max[threadIdx.x] - mx) * invT);
       __syncthreads();
-      float hv[C * HB / NT];
-#pragma unroll
-      for (int q = 0; q < C * HB / NT; ++q)
-        hv[q] = __hip_atomic_load(&w[W_HIST + threadIdx.x + q * NT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int q = 0; q < C * HB / NT; ++q) {
         const int e = threadIdx.x + q * NT, cc = e / HB, kk = e - cc * HB;
