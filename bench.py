@@ -160,6 +160,11 @@ def main() -> int:
         args.knights_per_gpu = kpt
     if N % T:
         raise SystemExit(f"--tp {T} must divide the {N} launched GPUs")
+    from theroundtaible_amd.models.config import get_config
+    mc = get_config(args.model, **({"n_layers": args.layers} if args.layers else {}))
+    if T > 1 and (mc.n_heads % T or mc.ffn % T or (mc.n_kv_heads % T and T % mc.n_kv_heads)):
+        raise SystemExit(f"{args.model} ({mc.n_heads} heads, {mc.n_kv_heads} KV heads, FFN {mc.ffn}) "
+                         f"does not split over tp={T}")
     n_groups = N // T                      # GPU groups; a knight lives on one group (T ranks)
     total_knights = args.knights_per_gpu * n_groups
     n_tables = max(1, total_knights // kpt)

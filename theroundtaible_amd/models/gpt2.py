@@ -26,6 +26,8 @@ class GPT2Model:
         self.tp = tp or TPInfo()
         self.device = device
         self.dtype = dtype
+        if cfg.n_heads % self.tp.size or cfg.ffn % self.tp.size:
+            raise ValueError(f"{cfg.name}: {cfg.n_heads} heads / FFN {cfg.ffn} do not split over tp={self.tp.size}")
         self.n_heads = cfg.n_heads // self.tp.size
         self.n_kv_heads = self.n_heads
         self.head_dim = cfg.head_dim
