@@ -186,11 +186,10 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
 
 int split_workspace_ints(int max_split_tiles) { return SPLIT_CTRS + max_split_tiles * 2 * SPLIT_STRIDE; }
 
-// Split-K part count for a T-tile, ks-k-step GEMM on `cus` CUs (0 = no split-K): enough parts
-// that T x S reaches `target` workgroups (default one per CU: r03 microbench, Llama-3-8B tp8
-// NORM_ADD shards, qkv 48 tiles 8.70 us unsplit / 8.25 at 1 WG per CU / 11.26 at 2 per CU;
-// profiles/r03/gemm_tp_shards_*.md), each part >= 8 k-steps, T x S capped by the workspace. RT_SPLITK=<S> pins S (1 = off), RT_SPLITK_TARGET=<wgs> moves the target
-// (microbenchmark sweeps; read once per process).
+// Split-K part count for a T-tile, ks-k-step GEMM on `cus` CUs (0 = no split-K): the most parts
+// that keep every CU at one workgroup (profiles/r03/gemm_tp_shards_*), each part >= 8 k-steps,
+// T x S capped by the workspace. RT_SPLITK=<S> pins S (1 = off),
+// RT_SPLITK_TARGET=<wgs> = the r03-first rule S = ceil(wgs / T) (microbenchmark sweeps; read once).
 int splitk_parts(int T, int ks, int cus, int64_t ws_ints) {
   static const int pinned = [] {
     const char* e = getenv("RT_SPLITK");
@@ -201,15 +200,21 @@ int splitk_parts(int T, int ks, int cus, int64_t ws_ints) {
     return e ? atoi(e) : 0;
   }();
   if (cus <= 0 || T >= cus || T > SPLIT_CTRS || pinned == 1) return 0;
+  const int smax = ks / 8 < 16 ? ks / 8 : 16;
   int S;
   if (pinned > 1) {
     S = pinned;
+  } else if (target_env > 0) {
+    S = (target_env + T - 1) / T;
   } else {
-    const int target = target_env > 0 ? target_env : cus;
-    S = (target + T - 1) / T;
+    // at most ONE part per CU: T x S just above the CU count doubles some CUs, which costs more
+    // than the split gains (r03 microbench, Llama-3-8B shards, us unsplit -> split: tp 8 qkv 48
+    // tiles 8.70 -> 8.34 at S = 6 (288 WGs) / 11.26 at S = 11; tp 2 qkv 192 tiles 9.44 -> 10.85 at
+    // S = 2; tp 4 gate_up 224 tiles 13.64 -> 14.18 at S = 2): S = floor(cus / T), so only shapes
+    // with <= cus / 2 tiles split
+    S = cus / T;
   }
-  S = S < ks / 8 ? S : ks / 8;
-  if (S > 16) S = 16;
+  S = S < smax ? S : smax;
   while (S >= 2 && SPLIT_CTRS + (int64_t)T * S * SPLIT_STRIDE > ws_ints) --S;
   return S >= 2 ? S : 0;
 }
@@ -234,8 +239,25 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
                     eps, re, (const uint16_t*)x2, (uint16_t*)xo};
       args.kmajor = forced_order();
       const dim3 grid(T * S);
-#define RT_SK(P, E) \
-  hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 4, 2>), grid, dim3(256), 0, stream, args, split_ws, S)
+      // (NW, U) of the split-K parts: 8 waves x 2 steps — one part per CU streams with twice
+      // the bytes in flight of 4 waves (r03 microbench, Llama-3-8B tp 4 qkv 8.79 -> 7.98 us; tp 2/8
+      // shards within noise; 4x4 no better: profiles/r03/gemm_tp_splitk_cfg_sweep.md).
+      // RT_SPLITK_CFG=<NW>x<U> (8x2, 4x2, 4x4) pins it
+      static const int skcfg = [] {
+        const char* e = getenv("RT_SPLITK_CFG");
+        int nw = 0, u = 0;
+        if (!e || sscanf(e, "%dx%d", &nw, &u) != 2) return 802;
+        return nw * 100 + u;
+      }();
+#define RT_SK(P, E)                                                                                                 \
+  do {                                                                                                              \
+    if (skcfg == 402)                                                                                               \
+      hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 4, 2>), grid, dim3(256), 0, stream, args, split_ws, S);  \
+    else if (skcfg == 404)                                                                                          \
+      hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 4, 4>), grid, dim3(256), 0, stream, args, split_ws, S);  \
+    else                                                                                                            \
+      hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 8, 2>), grid, dim3(512), 0, stream, args, split_ws, S);  \
+  } while (0)
       if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SK(PRO_PLAIN, EPI_STORE);
       else if (pro == PRO_NORM && epi == EPI_STORE) RT_SK(PRO_NORM, EPI_STORE);
       else if (pro == PRO_NORM_ADD && epi == EPI_STORE) RT_SK(PRO_NORM_ADD, EPI_STORE);
