@@ -42,8 +42,8 @@ class Calibration:
     ar_us: float = 8.0
     # vocab-parallel logits gather (RCCL all-gather inside the graph) per step: estimate
     gather_us: float = 10.0
-    sampler_us: float = 40.0        # K6, 6 launches (profiles/r03 prof: 8.4+8.3+6.2+6.0+5.3+4.8 us)
-    step_overhead_us: float = 8.0   # decode_advance + graph-replay gaps per step
+    sampler_us: float = 26.0        # K6 + step bookkeeping, ONE launch (profiles/r03/bench_final_kernels_25rounds.md)
+    step_overhead_us: float = 5.0   # graph-replay gaps per step (the bookkeeping is inside K6)
     # prefill: effective GEMM + attention throughput of the chunked varlen prefill (r02: 52.6 ms
     # per round for ~1.9K new tokens x 3 knights on Llama-3-8B -> ~0.6 PFLOP/s incl. attention)
     prefill_tflops: float = 600.0
