@@ -308,6 +308,29 @@ def test_sample_fast_path_matches_reference():
     assert hits >= total - 2, (hits, total)
 
 
+def test_sample_rejection_paths_match_reference():
+    """Low top-p (most whole-vocabulary draws rejected: the histogram-resolved nucleus, the
+    candidate test and the threshold search all run) and near-flat rows (random-init models: the
+    histogram grid scale adapts after the first call on a persistent workspace) agree with the
+    fp64 reference draw for draw."""
+    B, V = 8, 128256
+    logits = bf(B, V, scale=2.0, seed=91).float()
+    logits[1::2] *= 0.05
+    temp = torch.full((B,), 0.8, device=DEV)
+    top_p = torch.tensor([0.3, 0.3, 0.5, 0.5, 0.95, 0.95, 0.99, 0.7], device=DEV)
+    top_k = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ws = ops.sample_workspace(B, DEV)
+    hits = total = 0
+    for rep in range(6):
+        seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 104729 + rep
+        offs = torch.arange(B, dtype=torch.int64, device=DEV) + 777 * rep
+        got = ops.sample(logits, temp, top_p, top_k, seeds, offs, ws=ws).cpu()
+        exp = ref.sample(logits.cpu(), temp.cpu(), top_p.cpu(), top_k.cpu(), seeds.cpu(), offs.cpu())
+        hits += int((got == exp).sum())
+        total += B
+    assert hits >= total - 2, (hits, total)
+
+
 def test_sample_top_p_nucleus():
     V = 1000
     logits = torch.full((1, V), -10.0, device=DEV)
