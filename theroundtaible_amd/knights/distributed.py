@@ -81,7 +81,10 @@ class DistributedPool:
                     continue
                 done.add(b.group_key())
                 with trace.range("C1 overlap: speculative prefill"):
-                    b.prefetch(pairs[i][1].seq_key, prompt)
+                    try:
+                        b.prefetch(pairs[i][1].seq_key, prompt)
+                    except Exception:  # noqa: BLE001 - a failed speculation only loses the overlap;
+                        pass           # a real device fault surfaces in the next turn
             self._event("speculate_end")
 
     def _event(self, name: str) -> None:
