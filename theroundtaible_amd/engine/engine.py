@@ -347,6 +347,17 @@ class Engine:
             except KVCacheOOM:
                 self.kv.truncate(sq, len(ids[:n]) - len(delta))
                 return 0
+            except RuntimeError as e:
+                # the reserved span's KV may be incomplete: drop the whole shared sequence (the
+                # next turn prefills it again) and let run_turns' recovery probe the device
+                sk = self.shared_seq_key(key)
+                self.__dict__.get("_shared_lru", {}).pop(sk, None)
+                self._spec_pred.pop(sk, None)
+                self.kv.free_seq(sk)
+                msg = str(e)
+                if "HIP" in msg or "hip" in msg or "device" in msg:
+                    self.healthy = False
+                return 0
         self.stats["speculative_tokens"] += len(delta)
         self.stats["prefill_tokens"] += len(delta)
         return len(delta)
