@@ -145,3 +145,31 @@ def test_lru_never_evicts_a_shared_key_of_the_current_batch():
     for t in range(4):          # every member still references live (allocated) blocks
         for blk in e.kv.seqs[f"k{t}"].blocks:
             assert e.kv.alloc.ref[blk] > 0
+
+
+def test_warm_shared_reused_by_next_turn_and_fault_drops_it():
+    """Engine.warm_shared (the C1-overlap speculative prefill): a predicted shared prefix is
+    prefilled ahead of the turn and the turn keeps it by LCP (same tokens as without the warm-up,
+    fewer turn-time prefill tokens); a device fault during the warm-up drops the shared sequence
+    and flags the engine for recovery instead of leaving half-written KV for the LCP to reuse."""
+    from theroundtaible_amd.prompt import Segment
+    a, b = _engine(), _engine()
+    tr = [Segment("\n\n### Claude (Ronde 1):\n"), Segment("Een eerste antwoord over gedeelde KV " * 4)]
+    turns_a, turns_b = _turns(tr, 2, "t0"), _turns(tr, 2, "t0")
+    n = a.warm_shared(turns_a[0].prompt)
+    assert n > 0 and a.stats["speculative_tokens"] == n
+    out_a = a.run_turns(turns_a)
+    out_b = b.run_turns(turns_b)
+    assert [o.ids for o in out_a] == [o.ids for o in out_b]
+    assert a.stats["speculative_kept"] == n
+    pre_a = sum(o.metrics["prefill_tokens"] for o in out_a)
+    pre_b = sum(o.metrics["prefill_tokens"] for o in out_b)
+    assert pre_a == pre_b - n
+    # fault during a warm-up
+    c = _engine()
+
+    def boom(*args, **kw):
+        raise RuntimeError("HIP error: injected fault in the speculative prefill")
+    c.prefill_reserved = boom
+    assert c.warm_shared(_turns(tr, 2, "t0")[0].prompt) == 0
+    assert c.shared_seq_key("t0@table") not in c.kv.seqs and not c.healthy
