@@ -415,3 +415,12 @@ def test_c1_overlaps_speculative_prefill_striped():
     assert d_on["transcript_sha"] == d_off["transcript_sha"]
     # the speculated KV was reused: the turns themselves prefilled fewer tokens
     assert d_on["prefill_tokens"] < d_off["prefill_tokens"]
+
+
+def test_strong_scaling_sampled_decode_tp2():
+    """Sampled (temperature 0.7, top-p 0.95) tensor-parallel decode, the driver bench's setting:
+    logit shards all-gathered in ONE all_gather_into_tensor and sampled on the full row, every
+    rank drawing the same token."""
+    out = _bench(2, ("--temperature", "0.7"))
+    assert out["config"]["parallelism"] == "tp2" and out["detail"]["failed_turns"] == 0
+    assert out["detail"]["decode_tokens"] == 3 * 8 * 2

@@ -80,6 +80,15 @@ def test_strong_scaling_bench_on_shared_gpu(nproc):
     assert out["detail"]["k9_oneshot"], out["_log"]
 
 
+def test_strong_scaling_sampled_decode_on_shared_gpu():
+    """The driver's strong-scaling bench samples (temperature 0.7, top-p 0.95): the sampled TP
+    decode — vocab-parallel lm_head, ONE all_gather_into_tensor of the logit shards, the fused K6
+    sampler on the gathered row — rehearsed at tp 2 (the other rehearsals decode greedily)."""
+    out = _bench(("--temperature", "0.7"), nproc=2)
+    assert out["config"]["parallelism"] == "tp2" and out["detail"]["failed_turns"] == 0, out["_log"]
+    assert out["detail"]["decode_tokens"] == 3 * 16 * 2, out["_log"]
+
+
 def _tp_check(nproc, model, layers, tokens=12):
     gc.collect()
     torch.cuda.empty_cache()
