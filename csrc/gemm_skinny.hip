@@ -42,14 +42,23 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(GemmArgs p) {
 // above the line through its neighbours).
 constexpr int SPLIT_CTRS = 256;   // counter words at the head of the split workspace
 template <int PRO, int EPI, int NW, int U>
-__global__ void __launch_bounds__(NW * 64) skinny_gemm_bal_kernel(GemmArgs p, int* __restrict__ ws, int R) {
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_bal_kernel(GemmArgs p, int* __restrict__ ws, int R, int xpair) {
   __shared__ GemmSmem<nacc<EPI>(), NW> sm;
   Stage<PRO, EPI, U> st0;
   const int T = p.N / 16;
   const int b = blockIdx.x;
   if (b < 2 * R) {
-    const int r = b >> 1;
-    const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)r * 2 * SPLIT_STRIDE, ws + r, b & 1, 2};
+    // the two halves of a tile on ONE XCD when R % 8 == 0 (blocks b and b + 8 of each group of 16:
+    // round-robin dispatch puts both on XCD b % 8), so the combine reads same-XCD partials
+    int r, idx;
+    if (xpair && (R & 7) == 0) {
+      r = (b >> 4) * 8 + (b & 7);
+      idx = (b >> 3) & 1;
+    } else {
+      r = b >> 1;
+      idx = b & 1;
+    }
+    const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)r * 2 * SPLIT_STRIDE, ws + r, idx, 2};
     gemm_tile<PRO, EPI, NW, U, false>(p, T - R + r, sm, st0, false, false, &sx);
   } else {
     gemm_tile<PRO, EPI, NW, U, false>(p, b - 2 * R, sm, st0, false, false);
@@ -287,27 +296,29 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
                     eps, re, nullptr, nullptr};
       args.kmajor = forced_order();
       const dim3 grid(T + R);
+      // the two halves of a remainder tile on one XCD (RT_BAL_XCD=0: adjacent block ids, r02)
+      static const int bal_xpair = !(getenv("RT_BAL_XCD") && getenv("RT_BAL_XCD")[0] == '0');
       if (pro == PRO_NORM && epi == EPI_ROPE)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_ROPE, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else if (pro == PRO_PLAIN && epi == EPI_ROPE)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_ROPE, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else if (pro == PRO_NORM && epi == EPI_SWIGLU)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_SWIGLU, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else if (pro == PRO_PLAIN && epi == EPI_SWIGLU)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_SWIGLU, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else if (pro == PRO_NORM && epi == EPI_STORE)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_NORM, EPI_STORE, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else if (pro == PRO_PLAIN && epi == EPI_STORE)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_STORE, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else if (pro == PRO_PLAIN && epi == EPI_RESID)
         hipLaunchKernelGGL((skinny_gemm_bal_kernel<PRO_PLAIN, EPI_RESID, 4, 2>), grid, dim3(256), 0, stream, args,
-                           split_ws, R);
+                           split_ws, R, bal_xpair);
       else
         return -2;
       return 0;
