@@ -317,6 +317,9 @@ def main() -> int:
         "detail": {"world": cl.world, "backend": cl.backend, "c1_ranks": cl.world if cl.distributed else 1,
                    "simulated_tp": sim or None,
                    "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),
+                   "k9_us": getattr(getattr(engine.tp, "oneshot", None), "latency_us", None),
+                   "k9_fused_gemm_ar": bool(getattr(getattr(engine.tp, "oneshot", None), "fused", False)),
+                   "k9_fused_saving_us": getattr(getattr(engine.tp, "oneshot", None), "fused_saving_us", None),
                    "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "c1_skipped_batches": getattr(pool, "c1_skipped", 0),
                    "c1_device_assembled": pool.exchange.device_path if pool.exchange is not None else 0,

@@ -55,6 +55,7 @@ int oneshot_create(int world, int rank, int cap_elems, char* handles);
 int oneshot_open(int id, const char* all_handles);
 int oneshot_capacity(int id);
 int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream);
+int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, hipStream_t stream);
 int oneshot_error(int id);
 int oneshot_clear_error(int id);
 int oneshot_set_poll_limit(int id, long long limit);
@@ -392,14 +393,14 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
 
 // K9 one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot_ar.hip).
 py::tuple py_oneshot_create(int64_t world, int64_t rank, int64_t cap_elems) {
-  char h[128] = {0};
+  char h[192] = {0};
   const int id = oneshot_create((int)world, (int)rank, (int)cap_elems, h);
   TORCH_CHECK(id >= 0, "oneshot_create failed (rc=", id, ")");
-  return py::make_tuple(id, py::bytes(h, 128));
+  return py::make_tuple(id, py::bytes(h, 192));
 }
 void py_oneshot_open(int64_t id, py::bytes all_handles, int64_t world) {
   const std::string hs = all_handles;
-  TORCH_CHECK((int64_t)hs.size() == world * 128, "oneshot_open: need world x 128 handle bytes");
+  TORCH_CHECK((int64_t)hs.size() == world * 192, "oneshot_open: need world x 192 handle bytes");
   const int rc = oneshot_open((int)id, hs.data());
   TORCH_CHECK(rc == 0, "oneshot_open: hipIpcOpenMemHandle failed (rc=", rc, ")");
 }
@@ -408,6 +409,17 @@ void py_oneshot_allreduce(int64_t id, torch::Tensor x) {
   TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= oneshot_capacity((int)id), "oneshot_allreduce: size");
   const int rc = oneshot_allreduce((int)id, x.data_ptr(), (int)x.numel(), cur_stream());
   TORCH_CHECK(rc == 0, "oneshot_allreduce failed (rc=", rc, ")");
+}
+// Row-parallel decode GEMM with the K9 exchange fused into its epilogue (EPI_AR).
+void py_oneshot_gemm_ar(int64_t id, torch::Tensor out, torch::Tensor x, torch::Tensor Ws) {
+  check_bf16(out, "oneshot_gemm_ar out");
+  check_bf16(x, "oneshot_gemm_ar x");
+  check_bf16(Ws, "oneshot_gemm_ar Ws");
+  TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "oneshot_gemm_ar: x [M,K], Ws [N,K]");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) == Ws.size(0), "oneshot_gemm_ar: out [M,N]");
+  const int rc = oneshot_gemm_ar((int)id, out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)x.size(0),
+                                 (int)Ws.size(0), (int)x.size(1), cur_stream());
+  TORCH_CHECK(rc == 0, "oneshot_gemm_ar: unsupported configuration (rc=", rc, ")");
 }
 
 // Decode-step bookkeeping (csrc/decode_step.hip).
@@ -573,6 +585,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("oneshot_create", &py_oneshot_create, py::arg("world"), py::arg("rank"), py::arg("cap_elems"));
   m.def("oneshot_open", &py_oneshot_open, py::arg("id"), py::arg("all_handles"), py::arg("world"));
   m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
+  m.def("oneshot_gemm_ar", &py_oneshot_gemm_ar, py::arg("id"), py::arg("out"), py::arg("x"), py::arg("Ws"));
   m.def("oneshot_capacity", [](int64_t id) { return oneshot_capacity((int)id); });
   m.def("oneshot_error", [](int64_t id) { return oneshot_error((int)id); });
   m.def("oneshot_clear_error", [](int64_t id) { return oneshot_clear_error((int)id); });

@@ -16,7 +16,14 @@
 // The call counter (`epoch`) lives on the device and is advanced by the last workgroup out, so
 // the launch is hipGraph-capturable and replays with no host involvement.
 // Every flag wait is bounded: on expiry *err is set and the kernel proceeds (never a hang).
-#include "common.h"
+//
+// The same comm also serves the FUSED form (skinny_gemm_ar_kernel below, epilogue EPI_AR of
+// skinny_core.h): a row-parallel decode GEMM (o / down projection) exchanges each finished
+// 16-column tile itself — push, per-(peer, tile) flag, wait, rank-order sum — so the decode step
+// has no separate all-reduce launch at all, and a tile's xGMI round trip overlaps the other
+// tiles' weight streams. Both forms share the receive buffers and the call counter (a call of
+// either kind is one epoch), so they interleave freely within a captured graph.
+#include "skinny_core.h"
 
 #include <cstdio>
 #include <cstring>
@@ -27,6 +34,8 @@ namespace {
 constexpr int MAXW = 8;    // ranks per all-reduce group (one xGMI hop to every peer)
 constexpr int MAXB = 64;   // workgroups per call (flags per (slot, source rank))
 constexpr long long FLAG_POLL_LIMIT = 1ll << 26;   // default bound (~seconds); tests lower it per comm
+constexpr int MAXT = 1024; // 16-column tiles per fused call (N <= 16384)
+static_assert(MAXW == skinny::AR_MAXW, "rank limit shared with the fused epilogue");
 
 struct Peers {
   uint16_t* data[MAXW];    // rank p's receive buffer: [2 slots][world][cap] bf16
@@ -107,6 +116,8 @@ struct Comm {
   int device = 0;
   uint16_t* data = nullptr;               // own receive buffer
   uint32_t* flags = nullptr;              // own flags
+  uint32_t* tflags = nullptr;             // own per-tile flags of the fused GEMM form
+  uint32_t* peer_tflags[MAXW] = {};
   uint32_t* ctr = nullptr;                // [epoch, done] (plain device memory, local only)
   int* err = nullptr;
   long long poll_limit = FLAG_POLL_LIMIT;
@@ -122,10 +133,18 @@ Comm* get(int id) {
 }
 size_t data_bytes(const Comm& c) { return (size_t)2 * c.world * c.cap * sizeof(uint16_t); }
 size_t flag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXB * sizeof(uint32_t); }
+size_t tflag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXT * sizeof(uint32_t); }
+
+template <int NW, int U>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_ar_kernel(skinny::GemmArgs p) {
+  __shared__ skinny::GemmSmem<1, NW> sm;
+  skinny::Stage<skinny::PRO_PLAIN, skinny::EPI_AR, U> st0;
+  skinny::gemm_tile<skinny::PRO_PLAIN, skinny::EPI_AR, NW, U, false>(p, blockIdx.x, sm, st0, false, false);
+}
 }  // namespace
 
-// Allocates this rank's IPC buffers. Returns a comm id (>= 0) or a negative error; the two
-// 64-byte IPC handles (data, flags) are written to `handles` (128 bytes).
+// Allocates this rank's IPC buffers. Returns a comm id (>= 0) or a negative error; the three
+// 64-byte IPC handles (data, flags, tile flags) are written to `handles` (192 bytes).
 int oneshot_create(int world, int rank, int cap_elems, char* handles) {
   if (world < 2 || world > MAXW || rank < 0 || rank >= world || cap_elems < 8 || cap_elems % 8) return -1;
   Comm* c = new Comm;
@@ -135,29 +154,33 @@ int oneshot_create(int world, int rank, int cap_elems, char* handles) {
   if (hipGetDevice(&c->device) != hipSuccess) { delete c; return -2; }
   if (hipExtMallocWithFlags((void**)&c->data, data_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void**)&c->flags, flag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags((void**)&c->tflags, tflag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipMalloc((void**)&c->ctr, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc((void**)&c->err, sizeof(int)) != hipSuccess) {
     delete c;
     return -3;
   }
-  if (hipMemset(c->flags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->ctr, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
+  if (hipMemset(c->flags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->tflags, 0, tflag_bytes(*c)) != hipSuccess ||
+      hipMemset(c->ctr, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(c->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     delete c;
     return -4;
   }
-  hipIpcMemHandle_t hd, hf;
-  if (hipIpcGetMemHandle(&hd, c->data) != hipSuccess || hipIpcGetMemHandle(&hf, c->flags) != hipSuccess) {
+  hipIpcMemHandle_t hd, hf, ht;
+  if (hipIpcGetMemHandle(&hd, c->data) != hipSuccess || hipIpcGetMemHandle(&hf, c->flags) != hipSuccess ||
+      hipIpcGetMemHandle(&ht, c->tflags) != hipSuccess) {
     delete c;
     return -5;
   }
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
   memcpy(handles, &hd, 64);
   memcpy(handles + 64, &hf, 64);
+  memcpy(handles + 128, &ht, 64);
   std::lock_guard<std::mutex> lk(g_mu);
   g_comms.push_back(c);
   return (int)g_comms.size() - 1;
 }
 
-// Maps every peer's buffers: `all_handles` = world x 128 bytes, in rank order.
+// Maps every peer's buffers: `all_handles` = world x 192 bytes, in rank order.
 int oneshot_open(int id, const char* all_handles) {
   Comm* c = get(id);
   if (c == nullptr) return -1;
@@ -165,19 +188,25 @@ int oneshot_open(int id, const char* all_handles) {
     if (p == c->rank) {
       c->peers.data[p] = c->data;
       c->peers.flags[p] = c->flags;
+      c->peer_tflags[p] = c->tflags;
       continue;
     }
-    hipIpcMemHandle_t hd, hf;
-    memcpy(&hd, all_handles + (size_t)p * 128, 64);
-    memcpy(&hf, all_handles + (size_t)p * 128 + 64, 64);
+    hipIpcMemHandle_t hd, hf, ht;
+    memcpy(&hd, all_handles + (size_t)p * 192, 64);
+    memcpy(&hf, all_handles + (size_t)p * 192 + 64, 64);
+    memcpy(&ht, all_handles + (size_t)p * 192 + 128, 64);
     void* pd = nullptr;
     void* pf = nullptr;
+    void* pt = nullptr;
     if (hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -2;
     c->opened.push_back(pd);
     if (hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -3;
     c->opened.push_back(pf);
+    if (hipIpcOpenMemHandle(&pt, ht, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -3;
+    c->opened.push_back(pt);
     c->peers.data[p] = (uint16_t*)pd;
     c->peers.flags[p] = (uint32_t*)pf;
+    c->peer_tflags[p] = (uint32_t*)pt;
   }
   return 0;
 }
@@ -198,6 +227,37 @@ int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream) {
   nb = nb < 1 ? 1 : (nb > MAXB ? MAXB : nb);
   hipLaunchKernelGGL(oneshot_ar_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
                      c->cap, c->peers, c->ctr, c->ctr + 1, c->err, c->poll_limit);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// Fused row-parallel decode GEMM + all-reduce: out[M, N] = sum over ranks of x_r[M, K] . W_r[N, K]^T,
+// every rank calling with its own shard (Ws shuffled by shuffle_weight, plain layout rule).
+// Same (NW, U) rule as the standalone plain launch (gemm_skinny.hip): 4 x 4 below 384 tiles.
+int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, hipStream_t stream) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  if (M < 1 || M > 16 || K % 32 || N % 16 || N / 16 > MAXT || (int64_t)M * N > c->cap) return -2;
+  if (((uintptr_t)out & 15) || ((uintptr_t)x & 15) || ((uintptr_t)Ws & 15)) return -2;
+  for (int p = 0; p < c->world; ++p)
+    if (c->peers.data[p] == nullptr || c->peer_tflags[p] == nullptr) return -3;
+  skinny::GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const rt::short8*)Ws, nullptr, M, N, K, N, 0.f,
+                        skinny::RopeEpi{}, nullptr, nullptr};
+  for (int p = 0; p < c->world; ++p) {
+    args.ar.data[p] = c->peers.data[p];
+    args.ar.tflags[p] = c->peer_tflags[p];
+  }
+  args.ar.ctr = c->ctr;
+  args.ar.err = c->err;
+  args.ar.poll_limit = c->poll_limit;
+  args.ar.rank = c->rank;
+  args.ar.world = c->world;
+  args.ar.cap = c->cap;
+  args.ar.maxt = MAXT;
+  const dim3 grid(N / 16);
+  if (N / 16 >= 384)
+    hipLaunchKernelGGL((skinny_gemm_ar_kernel<4, 2>), grid, dim3(256), 0, stream, args);
+  else
+    hipLaunchKernelGGL((skinny_gemm_ar_kernel<4, 4>), grid, dim3(256), 0, stream, args);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
@@ -238,6 +298,7 @@ void oneshot_destroy(int id) {
   for (void* p : c->opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(c->data);
   (void)hipFree(c->flags);
+  (void)hipFree(c->tflags);
   (void)hipFree(c->ctr);
   (void)hipFree(c->err);
   delete c;

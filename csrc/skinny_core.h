@@ -18,7 +18,10 @@
 //             applied after the MFMAs) | NORM_ADD (A = bf16(x + x2): tensor-parallel residual
 //             plus the all-reduced partial; workgroup 0 publishes the sum to `xo`).
 // Epilogues:  STORE | RESID (res += y, in place) | SWIGLU (silu(gate) * up) |
-//             ROPE (qkv: rotate q/k pairs, write q, scatter k/v into the paged caches).
+//             ROPE (qkv: rotate q/k pairs, write q, scatter k/v into the paged caches) |
+//             AR (tensor-parallel row-parallel output: the K9 one-shot all-reduce per tile —
+//             push the bf16 tile to every rank's receive buffer, wait for the peers' copies of
+//             the SAME tile, sum in rank order; csrc/oneshot_ar.hip).
 // SC1 = true (persistent kernel): activations produced inside the same launch are read with
 // sc1 loads and every output is stored sc1 (write-through), MI355X_MICROARCH "Valid forms".
 #pragma once
@@ -30,7 +33,7 @@ using rt::float4_;
 using rt::short8;
 
 enum : int { PRO_PLAIN = 0, PRO_NORM = 1, PRO_NORM_ADD = 2 };
-enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_ROPE = 3 };
+enum : int { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_ROPE = 3, EPI_AR = 4 };
 
 struct RopeEpi {
   const int64_t* positions;  // [M]
@@ -39,6 +42,18 @@ struct RopeEpi {
   uint16_t* v_cache;
   const int64_t* slots;      // [M]
   int Hq, Hkv, D, BS;
+};
+
+// EPI_AR: the K9 comm of csrc/oneshot_ar.hip (receive buffers [2 slots][world][cap] bf16 and
+// per-tile flags [2][world][maxt] of every rank, the comm's call counter [epoch, done])
+constexpr int AR_MAXW = 8;
+struct ArEpi {
+  uint16_t* data[AR_MAXW];
+  uint32_t* tflags[AR_MAXW];
+  uint32_t* ctr;
+  int* err;
+  long long poll_limit;
+  int rank, world, cap, maxt;
 };
 
 struct GemmArgs {
@@ -54,6 +69,7 @@ struct GemmArgs {
   // weight record order (see weight_order): -1 = the shape's rule, as shuffle_weight wrote it;
   // 0 / c > 0 pinned (layout experiments, tools/exp_balance.hip)
   int kmajor = -1;
+  ArEpi ar{};           // EPI_AR only
 };
 
 template <int NACC, int NW>   // NACC = accumulators per lane (2 for SwiGLU gate + up)
@@ -258,6 +274,74 @@ RT_DEVICE void gemm_prefetch(const GemmArgs& p, int tile, Stage<PRO, EPI, U>& st
   issue_w<PRO, EPI, NW, U>(st0, wt, wt2, wid, nsteps, lane, sstride);
 }
 
+// EPI_AR: one tile's share of the K9 one-shot all-reduce, run by the workgroup that computed it
+// (a row-parallel decode GEMM needs no separate all-reduce launch). The value every rank
+// contributes is the bf16-rounded tile, exactly what the standalone K9 kernel would have been
+// given, and the copies are summed in fp32 in rank order, so the result is bit-identical to
+// GEMM (STORE) + K9 on every rank. Protocol as oneshot_ar.hip: remote 16-B pushes -> system
+// fence -> one flag per (peer, tile) -> bounded wait on the peers' flags of this tile in our own
+// memory -> sum. The last workgroup out advances the comm's call counter (graph-replayable).
+// Slot reuse: before this call writes slot (epoch & 1) again, every workgroup of the previous
+// call saw each peer's flag of that call, which the peer raised after its call before it (the
+// slot's last reader) had completed.
+template <int NW>
+RT_DEVICE void ar_exchange(const GemmArgs& p, int tile, float v, int m, int n, bool live,
+                           GemmSmem<1, NW>& sm) {
+  const ArEpi& ar = p.ar;
+  const int M = p.M, N = p.N;
+  const uint32_t epoch = __hip_atomic_load(ar.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int slot = (int)(epoch & 1u);
+  uint16_t* stage = reinterpret_cast<uint16_t*>(&sm.red[0][0][0][0]);   // [16 rows][16 cols] bf16
+  __syncthreads();                         // every wave is done reading the reduction buffers
+  const uint16_t mine = rt::f2bf(v);
+  if (live) stage[m * 16 + n] = mine;
+  __syncthreads();
+  // 1. push: row m of the tile = 32 B = two 16-B stores per destination rank
+  const int t = threadIdx.x;
+  if (t < 2 * M * ar.world) {
+    const int dst = t / (2 * M), rem = t - dst * 2 * M, row = rem >> 1, half = rem & 1;
+    const uint4 val = *reinterpret_cast<const uint4*>(stage + row * 16 + half * 8);
+    uint16_t* d = ar.data[dst] + ((size_t)slot * ar.world + ar.rank) * ar.cap + (size_t)row * N + tile * 16 + half * 8;
+    *reinterpret_cast<uint4*>(d) = val;
+  }
+  // 2. release: all pushes complete before any flag of this tile is raised
+  __threadfence_system();
+  __syncthreads();
+  if (t < ar.world)
+    __hip_atomic_store(ar.tflags[t] + ((size_t)slot * ar.world + ar.rank) * ar.maxt + tile, epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  // 3. wait for every rank's copy of this tile (bounded: on expiry flag the error, proceed)
+  if (t < ar.world) {
+    const uint32_t* f = ar.tflags[ar.rank] + ((size_t)slot * ar.world + t) * ar.maxt + tile;
+    long long it = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > ar.poll_limit) {
+        __hip_atomic_store(ar.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();
+  // 4. sum the world copies in rank order (fp32), store the bf16 result
+  if (live) {
+    const uint16_t* own = ar.data[ar.rank] + (size_t)slot * ar.world * ar.cap + (size_t)m * N + tile * 16 + n;
+    float acc = 0.f;
+    for (int r = 0; r < ar.world; ++r) acc += rt::bf2f(r == ar.rank ? mine : own[(size_t)r * ar.cap]);
+    p.out[(size_t)m * p.ldo + tile * 16 + n] = rt::f2bf(acc);
+  }
+  // 5. the last workgroup out advances the call counter (every workgroup has read it)
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(ar.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(ar.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ar.ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // One 16-column tile. `st0` may hold this tile's prefetched stage-0 weights (prefetched=true).
 // `publish_xo`: this workgroup writes the NORM_ADD sum to p.xo.
 template <int PRO, int EPI, int NW, int U, bool SC1>
@@ -416,10 +500,13 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
         const int hv = h - re.Hq - re.Hkv;
         st16<SC1>(re.v_cache + (((size_t)blk * re.Hkv + hv) * D + pp) * re.BS + off, v);
       }
+    } else if constexpr (EPI == EPI_AR) {
+      // stored after the exchange below
     } else {
       st16<SC1>(p.out + (size_t)m * p.ldo + col, v);
     }
   }
+  if constexpr (EPI == EPI_AR) ar_exchange<NW>(p, tile, v, m, n, live, sm);
   __syncthreads();  // LDS reduction buffers are reused by the next tile
 }
 }  // namespace skinny

@@ -111,10 +111,13 @@ def test_tp_fused_decode_matches_tp1_on_shared_gpu(model, layers, tp):
     qkv / gate_up, ping-pong residual, K9 one-shot all-reduces between the ranks, vocab-parallel
     lm_head — against a tp=1 engine with the same ``random-dev`` weights on the same GPU:
     prefill and decode logits cosine > 0.999, greedy tokens identical, no failed turn, no
-    expired K9 wait. Llama-3-8B shapes (the strong-scaling bench) and Llama-3-70B (config 5)."""
+    expired K9 wait; o / down on the fused GEMM + all-reduce launch. Llama-3-8B shapes (the strong-scaling bench) and Llama-3-70B (config 5)."""
     ref = _tp_check(1, model, layers)
     got = _tp_check(tp, model, layers)
     assert got["world"] == tp and got["fused"] and got["k9"], got
+    # o / down ran as ONE launch each with the exchange in the epilogue (EPI_AR), after the
+    # comm's self-test matched it bit for bit against GEMM + K9 on every rank
+    assert got["fused_ar"] and got["fused_ar_calls"] > 0, got
     assert ref["fused"] and ref["world"] == 1
     assert all(e is None for e in got["errors"]) and not got["flag_errors"], got["errors"]
     cos = torch.nn.functional.cosine_similarity

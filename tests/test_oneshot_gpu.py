@@ -23,4 +23,7 @@ def test_oneshot_allreduce_ranks_on_one_gpu(world):
     ranks = recs[0]["ranks"]
     assert sorted(o["rank"] for o in ranks) == list(range(world))
     assert all(o["checks"] == 6 + 15 for o in ranks)
+    # creation ran the exact self-tests: K9 values over both slots, then the fused GEMM + exchange
+    # (EPI_AR) bit-identical to GEMM + K9 at three shard shapes
+    assert all(o["fused_gemm_ar"] is True and o["self_test_latency_us"] > 0 for o in ranks), ranks
     assert next(o for o in ranks if o["rank"] == 0).get("expiry_flagged") is True

@@ -192,7 +192,9 @@ class LlamaModel:
         so their outputs are partial sums — stored plainly, all-reduced over RCCL (C2, inside the
         hipGraph), and added to the residual by the NEXT GEMM's NORM_ADD prologue, whose
         workgroup 0 also writes the new residual (ping-pong buffers, never in place). The lm_head
-        is vocab-parallel + all-gather (C3). Still 5 kernels + 2 all-reduces per layer."""
+        is vocab-parallel + all-gather (C3). 5 kernels per layer: when the K9 comm passed its fused
+        self-test, o / down carry the all-reduce in their epilogue (``tp.row_parallel``), else
+        5 kernels + 2 all-reduce launches."""
         cfg, tp = self.cfg, self.tp
         eps = cfg.norm_eps
         dec = self.decode_weights()
@@ -214,11 +216,11 @@ class LlamaModel:
                                          x2=h, xout=bufs[1 - cur], **sk)
                 cur = 1 - cur
             a = self.attention(q, kc, vc, meta)
-            h = tp.all_reduce(ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_STORE, **sk))
+            h = tp.row_parallel(a.reshape(B, -1), lw["wo"], **sk)
             g = ops.skinny_gemm(bufs[cur], lw["w_gate_up"], ops.PRO_NORM_ADD, ops.EPI_SWIGLU, eps=eps, x2=h,
                                 xout=bufs[1 - cur], **sk)
             cur = 1 - cur
-            h = tp.all_reduce(ops.skinny_gemm(g, lw["w_down"], ops.PRO_PLAIN, ops.EPI_STORE, **sk))
+            h = tp.row_parallel(g, lw["w_down"], **sk)
         logits = ops.skinny_gemm(bufs[cur], dec["lm_head"], ops.PRO_NORM_ADD, ops.EPI_STORE, eps=eps, x2=h, **sk)
         if meta.local_logits:
             return logits

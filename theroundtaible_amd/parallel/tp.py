@@ -76,6 +76,17 @@ class TPInfo:
                 dist.all_reduce(x, group=self.group)
         return x
 
+    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
+        """Decode row-parallel linear (o / down on shuffled weights) + C2: ONE launch with the
+        K9 exchange fused into the GEMM epilogue when the one-shot comm passed its fused self-test,
+        else the skinny GEMM followed by :meth:`all_reduce`."""
+        from .. import ops
+        os_ = self.oneshot
+        if self.size > 1 and os_ is not None and os_.accepts_gemm(x, Ws):
+            self.fused_ar_calls = getattr(self, "fused_ar_calls", 0) + 1
+            return os_.gemm_ar(x, Ws)
+        return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
+
     def any_rank(self, flag: bool) -> bool:
         """True if ``flag`` is set on any rank of the group (host-side agreement, e.g. to fail a
         turn on every rank of a TP knight when one rank's K9 flag wait expired)."""
@@ -148,6 +159,21 @@ class SimulatedTP(TPInfo):
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         self.sim_all_reduces = getattr(self, "sim_all_reduces", 0) + 1
         return x
+
+    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
+        from .. import ops
+        return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
+
+    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
+        """Decode row-parallel linear (o / down on shuffled weights) + C2: ONE launch with the
+        K9 exchange fused into the GEMM epilogue when the one-shot comm passed its fused self-test,
+        else the skinny GEMM followed by :meth:`all_reduce`."""
+        from .. import ops
+        os_ = self.oneshot
+        if self.size > 1 and os_ is not None and os_.accepts_gemm(x, Ws):
+            self.fused_ar_calls = getattr(self, "fused_ar_calls", 0) + 1
+            return os_.gemm_ar(x, Ws)
+        return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
 
     def any_rank(self, flag: bool) -> bool:
         return flag

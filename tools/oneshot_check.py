@@ -47,7 +47,8 @@ def main() -> int:
     from theroundtaible_amd.parallel.oneshot import try_create
     ar = try_create(dist.group.WORLD, rank, world)
     assert ar is not None, "one-shot all-reduce could not be set up"
-    out = {"rank": rank, "world": world, "backend": backend, "checks": 0}
+    out = {"rank": rank, "world": world, "backend": backend, "checks": 0, "self_test_latency_us": ar.latency_us,
+           "fused_gemm_ar": ar.fused, "fused_saving_us": ar.fused_saving_us}
     for tag, n in enumerate([8, 1024, 4096, 8192, 3 * 8192, 16 * 8192]):
         x = data(rank, n, tag, dev)
         ar(x)

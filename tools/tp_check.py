@@ -68,12 +68,14 @@ def main() -> int:
     outs = e.run_turns([Turn("K1", prompt, sp), Turn("K2", prompt + " Tweede ridder.", sp)])
     flag_errors = e.device_flag_errors()
     rec = {"world": cl.world, "backend": cl.backend, "fused": bool(fused),
-           "k9": bool(getattr(e.tp, "oneshot", None)), "prefill_logits": pre[0].cpu(), "decode_logits": dec[0].cpu(),
+           "k9": bool(getattr(e.tp, "oneshot", None)),
+           "fused_ar": bool(getattr(getattr(e.tp, "oneshot", None), "fused", False)),
+           "fused_ar_calls": int(getattr(e.tp, "fused_ar_calls", 0)), "prefill_logits": pre[0].cpu(), "decode_logits": dec[0].cpu(),
            "ids": [o.ids for o in outs], "errors": [str(o.error) if o.error else None for o in outs],
            "flag_errors": flag_errors}
     if cl.rank == 0:
         torch.save(rec, a.out)
-        print(f"tp_check world={cl.world} fused={fused} k9={rec['k9']} ids={rec['ids']}", flush=True)
+        print(f"tp_check world={cl.world} fused={fused} k9={rec['k9']} fused_ar={rec['fused_ar_calls']} ids={rec['ids']}", flush=True)
     cl.barrier()
     shutdown_cluster()
     return 0
