@@ -320,6 +320,8 @@ def main() -> int:
                    "k9_us": getattr(getattr(engine.tp, "oneshot", None), "latency_us", None),
                    "k9_fused_gemm_ar": bool(getattr(getattr(engine.tp, "oneshot", None), "fused", False)),
                    "k9_fused_saving_us": getattr(getattr(engine.tp, "oneshot", None), "fused_saving_us", None),
+                   "k9_gather": bool(getattr(getattr(engine.tp, "oneshot", None), "gather_ok", False)),
+                   "k9_gather_saving_us": getattr(getattr(engine.tp, "oneshot", None), "gather_saving_us", None),
                    "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "c1_skipped_batches": getattr(pool, "c1_skipped", 0),
                    "c1_device_assembled": pool.exchange.device_path if pool.exchange is not None else 0,

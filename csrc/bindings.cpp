@@ -56,6 +56,9 @@ int oneshot_open(int id, const char* all_handles);
 int oneshot_capacity(int id);
 int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream);
 int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, hipStream_t stream);
+int oneshot_allgather(int id, const void* in, void* out, int rows, int shard, hipStream_t stream);
+int oneshot_gather_capacity();
+int oneshot_handle_bytes();
 int oneshot_error(int id);
 int oneshot_clear_error(int id);
 int oneshot_set_poll_limit(int id, long long limit);
@@ -393,14 +396,15 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
 
 // K9 one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot_ar.hip).
 py::tuple py_oneshot_create(int64_t world, int64_t rank, int64_t cap_elems) {
-  char h[192] = {0};
-  const int id = oneshot_create((int)world, (int)rank, (int)cap_elems, h);
+  std::vector<char> h((size_t)oneshot_handle_bytes(), 0);
+  const int id = oneshot_create((int)world, (int)rank, (int)cap_elems, h.data());
   TORCH_CHECK(id >= 0, "oneshot_create failed (rc=", id, ")");
-  return py::make_tuple(id, py::bytes(h, 192));
+  return py::make_tuple(id, py::bytes(h.data(), h.size()));
 }
 void py_oneshot_open(int64_t id, py::bytes all_handles, int64_t world) {
   const std::string hs = all_handles;
-  TORCH_CHECK((int64_t)hs.size() == world * 192, "oneshot_open: need world x 192 handle bytes");
+  TORCH_CHECK((int64_t)hs.size() == world * oneshot_handle_bytes(), "oneshot_open: need world x ",
+              oneshot_handle_bytes(), " handle bytes");
   const int rc = oneshot_open((int)id, hs.data());
   TORCH_CHECK(rc == 0, "oneshot_open: hipIpcOpenMemHandle failed (rc=", rc, ")");
 }
@@ -409,6 +413,16 @@ void py_oneshot_allreduce(int64_t id, torch::Tensor x) {
   TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= oneshot_capacity((int)id), "oneshot_allreduce: size");
   const int rc = oneshot_allreduce((int)id, x.data_ptr(), (int)x.numel(), cur_stream());
   TORCH_CHECK(rc == 0, "oneshot_allreduce failed (rc=", rc, ")");
+}
+// One-shot all-gather along the last dim (C3 logits): out [rows, world * shard] from in [rows, shard].
+void py_oneshot_allgather(int64_t id, torch::Tensor in, torch::Tensor out, int64_t world) {
+  check_bf16(in, "oneshot_allgather in");
+  check_bf16(out, "oneshot_allgather out");
+  TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && out.size(0) == in.size(0) && out.size(1) == in.size(1) * world,
+              "oneshot_allgather: in [rows, shard], out [rows, world * shard]");
+  const int rc = oneshot_allgather((int)id, in.data_ptr(), out.data_ptr(), (int)in.size(0), (int)in.size(1),
+                                   cur_stream());
+  TORCH_CHECK(rc == 0, "oneshot_allgather: unsupported configuration (rc=", rc, ")");
 }
 // Row-parallel decode GEMM with the K9 exchange fused into its epilogue (EPI_AR).
 void py_oneshot_gemm_ar(int64_t id, torch::Tensor out, torch::Tensor x, torch::Tensor Ws) {
@@ -586,6 +600,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("oneshot_open", &py_oneshot_open, py::arg("id"), py::arg("all_handles"), py::arg("world"));
   m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
   m.def("oneshot_gemm_ar", &py_oneshot_gemm_ar, py::arg("id"), py::arg("out"), py::arg("x"), py::arg("Ws"));
+  m.def("oneshot_allgather", &py_oneshot_allgather, py::arg("id"), py::arg("in"), py::arg("out"), py::arg("world"));
+  m.def("oneshot_gather_capacity", []() { return oneshot_gather_capacity(); });
   m.def("oneshot_capacity", [](int64_t id) { return oneshot_capacity((int)id); });
   m.def("oneshot_error", [](int64_t id) { return oneshot_error((int)id); });
   m.def("oneshot_clear_error", [](int64_t id) { return oneshot_clear_error((int)id); });

@@ -35,6 +35,8 @@ constexpr int MAXW = 8;    // ranks per all-reduce group (one xGMI hop to every 
 constexpr int MAXB = 64;   // workgroups per call (flags per (slot, source rank))
 constexpr long long FLAG_POLL_LIMIT = 1ll << 26;   // default bound (~seconds); tests lower it per comm
 constexpr int MAXT = 1024; // 16-column tiles per fused call (N <= 16384)
+constexpr int GCAP = 16 * 131072;   // all-gather output elements per slot (16 rows x a 128K vocab)
+constexpr int NHANDLES = 5;         // IPC handles per rank: data, flags, tile flags, gather data, gather flags
 static_assert(MAXW == skinny::AR_MAXW, "rank limit shared with the fused epilogue");
 
 struct Peers {
@@ -111,6 +113,74 @@ __global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ 
   }
 }
 
+// One-shot ALL-GATHER (C3: the vocab-parallel logits of a tensor-parallel decode step): every
+// rank pushes its [rows, shard] slice straight into its column block of every rank's
+// [rows, world * shard] receive buffer, raises one flag per (peer, workgroup), waits for the
+// peers' flags of the same workgroup range and copies the gathered rows out — one launch and
+// one xGMI hop, replacing RCCL's ring all-gather plus the permute into [rows, world * shard].
+// Same epoch / slot discipline as the all-reduce (shared call counter).
+struct GPeers {
+  uint16_t* data[MAXW];    // rank p's gather buffer: [2 slots][GCAP]
+  uint32_t* flags[MAXW];   // rank p's gather flags: [2 slots][world][MAXB]
+};
+
+__global__ void __launch_bounds__(256) oneshot_ag_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                         int rows, int shard, int rank, int world, GPeers P,
+                                                         uint32_t* epoch_ctr, uint32_t* done_ctr, int* err,
+                                                         long long poll_limit) {
+  const uint32_t epoch = __hip_atomic_load(epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int slot = (int)(epoch & 1u);
+  const int nb = gridDim.x, blk = blockIdx.x;
+  const int vrow = shard >> 3;                          // 16-byte vectors per row of a slice
+  const int nvec = rows * vrow;
+  const int per = (nvec + nb - 1) / nb;
+  const int v0 = blk * per, v1 = min(nvec, v0 + per);
+  const size_t ld = (size_t)world * shard;              // gathered row length
+  using vec = uint4;
+  // 1. push this workgroup's vectors of our slice into every rank's buffer (own included)
+  for (int v = v0 + (int)threadIdx.x; v < v1; v += blockDim.x) {
+    const int row = v / vrow, c8 = v - row * vrow;
+    const vec x = reinterpret_cast<const vec*>(in)[v];
+    const size_t dst = (size_t)slot * GCAP + row * ld + (size_t)rank * shard + (size_t)c8 * 8;
+    for (int p = 0; p < world; ++p) *reinterpret_cast<vec*>(P.data[p] + dst) = x;
+  }
+  __threadfence_system();
+  __syncthreads();
+  if ((int)threadIdx.x < world)
+    __hip_atomic_store(P.flags[threadIdx.x] + ((size_t)slot * world + rank) * MAXB + blk, epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  // 2. wait for every rank's vectors of the same range (every rank's slice has the same shape)
+  if ((int)threadIdx.x < world) {
+    const uint32_t* f = P.flags[rank] + ((size_t)slot * world + threadIdx.x) * MAXB + blk;
+    long long it = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > poll_limit) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();
+  // 3. copy the gathered range of every rank's block out of the (uncached) receive buffer
+  const uint16_t* mine = P.data[rank] + (size_t)slot * GCAP;
+  for (int r = 0; r < world; ++r)
+    for (int v = v0 + (int)threadIdx.x; v < v1; v += blockDim.x) {
+      const int row = v / vrow, c8 = v - row * vrow;
+      const size_t o = row * ld + (size_t)r * shard + (size_t)c8 * 8;
+      reinterpret_cast<vec*>(out + o)[0] = *reinterpret_cast<const vec*>(mine + o);
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (uint32_t)nb - 1u) {
+      __hip_atomic_store(done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(epoch_ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 struct Comm {
   int world = 0, rank = 0, cap = 0;       // cap: max elements per call
   int device = 0;
@@ -118,6 +188,9 @@ struct Comm {
   uint32_t* flags = nullptr;              // own flags
   uint32_t* tflags = nullptr;             // own per-tile flags of the fused GEMM form
   uint32_t* peer_tflags[MAXW] = {};
+  uint16_t* gdata = nullptr;              // own all-gather buffer
+  uint32_t* gflags = nullptr;             // own all-gather flags
+  GPeers gpeers{};
   uint32_t* ctr = nullptr;                // [epoch, done] (plain device memory, local only)
   int* err = nullptr;
   long long poll_limit = FLAG_POLL_LIMIT;
@@ -134,6 +207,7 @@ Comm* get(int id) {
 size_t data_bytes(const Comm& c) { return (size_t)2 * c.world * c.cap * sizeof(uint16_t); }
 size_t flag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXB * sizeof(uint32_t); }
 size_t tflag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXT * sizeof(uint32_t); }
+size_t gdata_bytes() { return (size_t)2 * GCAP * sizeof(uint16_t); }
 
 template <int NW, int U>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_ar_kernel(skinny::GemmArgs p) {
@@ -143,8 +217,9 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_ar_kernel(skinny::GemmArg
 }
 }  // namespace
 
-// Allocates this rank's IPC buffers. Returns a comm id (>= 0) or a negative error; the three
-// 64-byte IPC handles (data, flags, tile flags) are written to `handles` (192 bytes).
+// Allocates this rank's IPC buffers. Returns a comm id (>= 0) or a negative error; the
+// NHANDLES 64-byte IPC handles (data, flags, tile flags, gather data, gather flags) are written
+// to `handles` (64 * NHANDLES bytes).
 int oneshot_create(int world, int rank, int cap_elems, char* handles) {
   if (world < 2 || world > MAXW || rank < 0 || rank >= world || cap_elems < 8 || cap_elems % 8) return -1;
   Comm* c = new Comm;
@@ -155,61 +230,58 @@ int oneshot_create(int world, int rank, int cap_elems, char* handles) {
   if (hipExtMallocWithFlags((void**)&c->data, data_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void**)&c->flags, flag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void**)&c->tflags, tflag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags((void**)&c->gdata, gdata_bytes(), hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags((void**)&c->gflags, flag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipMalloc((void**)&c->ctr, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc((void**)&c->err, sizeof(int)) != hipSuccess) {
     delete c;
     return -3;
   }
   if (hipMemset(c->flags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->tflags, 0, tflag_bytes(*c)) != hipSuccess ||
+      hipMemset(c->gflags, 0, flag_bytes(*c)) != hipSuccess ||
       hipMemset(c->ctr, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(c->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     delete c;
     return -4;
   }
-  hipIpcMemHandle_t hd, hf, ht;
-  if (hipIpcGetMemHandle(&hd, c->data) != hipSuccess || hipIpcGetMemHandle(&hf, c->flags) != hipSuccess ||
-      hipIpcGetMemHandle(&ht, c->tflags) != hipSuccess) {
-    delete c;
-    return -5;
-  }
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
-  memcpy(handles, &hd, 64);
-  memcpy(handles + 64, &hf, 64);
-  memcpy(handles + 128, &ht, 64);
+  void* const bufs[NHANDLES] = {c->data, c->flags, c->tflags, c->gdata, c->gflags};
+  for (int i = 0; i < NHANDLES; ++i) {
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, bufs[i]) != hipSuccess) {
+      delete c;
+      return -5;
+    }
+    memcpy(handles + 64 * i, &h, 64);
+  }
   std::lock_guard<std::mutex> lk(g_mu);
   g_comms.push_back(c);
   return (int)g_comms.size() - 1;
 }
 
-// Maps every peer's buffers: `all_handles` = world x 192 bytes, in rank order.
+// Maps every peer's buffers: `all_handles` = world x (64 * NHANDLES) bytes, in rank order.
 int oneshot_open(int id, const char* all_handles) {
   Comm* c = get(id);
   if (c == nullptr) return -1;
   for (int p = 0; p < c->world; ++p) {
-    if (p == c->rank) {
-      c->peers.data[p] = c->data;
-      c->peers.flags[p] = c->flags;
-      c->peer_tflags[p] = c->tflags;
-      continue;
+    void* b[NHANDLES] = {c->data, c->flags, c->tflags, c->gdata, c->gflags};
+    if (p != c->rank) {
+      for (int i = 0; i < NHANDLES; ++i) {
+        hipIpcMemHandle_t h;
+        memcpy(&h, all_handles + (size_t)p * 64 * NHANDLES + 64 * i, 64);
+        if (hipIpcOpenMemHandle(&b[i], h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -2 - i;
+        c->opened.push_back(b[i]);
+      }
     }
-    hipIpcMemHandle_t hd, hf, ht;
-    memcpy(&hd, all_handles + (size_t)p * 192, 64);
-    memcpy(&hf, all_handles + (size_t)p * 192 + 64, 64);
-    memcpy(&ht, all_handles + (size_t)p * 192 + 128, 64);
-    void* pd = nullptr;
-    void* pf = nullptr;
-    void* pt = nullptr;
-    if (hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -2;
-    c->opened.push_back(pd);
-    if (hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -3;
-    c->opened.push_back(pf);
-    if (hipIpcOpenMemHandle(&pt, ht, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -3;
-    c->opened.push_back(pt);
-    c->peers.data[p] = (uint16_t*)pd;
-    c->peers.flags[p] = (uint32_t*)pf;
-    c->peer_tflags[p] = (uint32_t*)pt;
+    c->peers.data[p] = (uint16_t*)b[0];
+    c->peers.flags[p] = (uint32_t*)b[1];
+    c->peer_tflags[p] = (uint32_t*)b[2];
+    c->gpeers.data[p] = (uint16_t*)b[3];
+    c->gpeers.flags[p] = (uint32_t*)b[4];
   }
   return 0;
 }
+
+int oneshot_handle_bytes() { return 64 * NHANDLES; }
 
 int oneshot_capacity(int id) {
   Comm* c = get(id);
@@ -261,6 +333,24 @@ int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
+// All-gather along the last dim: out[rows, world * shard] <- every rank's in[rows, shard].
+int oneshot_allgather(int id, const void* in, void* out, int rows, int shard, hipStream_t stream) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  if (rows < 1 || shard < 8 || shard % 8 || (int64_t)rows * shard * c->world > GCAP) return -2;
+  if (((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return -2;
+  for (int p = 0; p < c->world; ++p)
+    if (c->gpeers.data[p] == nullptr) return -3;
+  const int nvec = rows * (shard / 8);
+  int nb = (nvec + 255) / 256;                      // one 16-B vector per thread per peer
+  nb = nb < 1 ? 1 : (nb > MAXB ? MAXB : nb);
+  hipLaunchKernelGGL(oneshot_ag_kernel, dim3(nb), dim3(256), 0, stream, (const uint16_t*)in, (uint16_t*)out, rows,
+                     shard, c->rank, c->world, c->gpeers, c->ctr, c->ctr + 1, c->err, c->poll_limit);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+int oneshot_gather_capacity() { return GCAP; }
+
 // Poll-expiry flag (1 = a peer's flag never arrived: results of that call are wrong).
 int oneshot_error(int id) {
   Comm* c = get(id);
@@ -299,6 +389,8 @@ void oneshot_destroy(int id) {
   (void)hipFree(c->data);
   (void)hipFree(c->flags);
   (void)hipFree(c->tflags);
+  (void)hipFree(c->gdata);
+  (void)hipFree(c->gflags);
   (void)hipFree(c->ctr);
   (void)hipFree(c->err);
   delete c;

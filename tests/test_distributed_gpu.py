@@ -99,6 +99,10 @@ def _tp_check(nproc, model, layers, tokens=12):
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "tp_check.py"),
            "--model", model, "--layers", str(layers), "--tokens", str(tokens), "--out", out]
     env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if nproc == 2:
+        # two ranks sharing the GPU co-schedule reliably: decode on the fused GEMM + exchange
+        # (one rank per GPU enables it by default; more sharing ranks keep the separate K9)
+        env["ROUNDTABLE_FUSED_AR"] = "1"
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return torch.load(out, weights_only=True)
@@ -117,7 +121,10 @@ def test_tp_fused_decode_matches_tp1_on_shared_gpu(model, layers, tp):
     assert got["world"] == tp and got["fused"] and got["k9"], got
     # o / down ran as ONE launch each with the exchange in the epilogue (EPI_AR), after the
     # comm's self-test matched it bit for bit against GEMM + K9 on every rank
-    assert got["fused_ar"] and got["fused_ar_calls"] > 0, got
+    if tp == 2:
+        assert got["fused_ar"] and got["fused_ar_calls"] > 0, got
+    else:
+        assert not got["fused_ar"] and got["fused_ar_calls"] == 0, got
     assert ref["fused"] and ref["world"] == 1
     assert all(e is None for e in got["errors"]) and not got["flag_errors"], got["errors"]
     cos = torch.nn.functional.cosine_similarity

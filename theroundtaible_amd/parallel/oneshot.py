@@ -13,7 +13,10 @@ peers'. The launch itself is hipGraph-capturable (device-side call counter).
 Fused form (:meth:`OneShotAllReduce.gemm_ar`): the row-parallel decode GEMMs (o / down) run the
 exchange in their own epilogue, tile by tile (skinny_core.h ``EPI_AR``), bit-identical to GEMM +
 K9 and with no all-reduce launch. It is used only after :func:`self_test_fused` has compared it
-with GEMM + K9 on this node's links; ``ROUNDTABLE_FUSED_AR=0`` keeps the separate launches.
+with GEMM + K9 on this node's links, and by default only when every rank owns its GPU
+(:func:`fused_mode_env`) and when a timed probe on the node shows it beating GEMM + K9 (on one
+GPU shared by two rehearsal ranks it loses by ~46 µs: the two processes' spinning grids
+co-schedule badly); ``ROUNDTABLE_FUSED_AR=0`` keeps the separate launches.
 """
 from __future__ import annotations
 
@@ -30,8 +33,26 @@ def enabled_by_env() -> bool:
     return os.environ.get("ROUNDTABLE_ONESHOT_AR", "1") != "0"
 
 
-def fused_enabled_by_env() -> bool:
-    return os.environ.get("ROUNDTABLE_FUSED_AR", "1") != "0"
+def fused_mode_env() -> str:
+    """``ROUNDTABLE_FUSED_AR``: ``auto`` (default: only when every rank owns its GPU and the timed
+    probe shows a saving), ``probe`` (self-test + timed decision even on a shared GPU — exercises
+    the auto decision in rehearsals), ``1`` (forced, also on a shared GPU: the 2-rank numerics
+    rehearsal), ``0`` (never)."""
+    return os.environ.get("ROUNDTABLE_FUSED_AR", "auto")
+
+
+def _device_key() -> str:
+    """Physical identity of this rank's GPU (PCI location when exposed, else UUID, else index)."""
+    import socket
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    pci = tuple(getattr(props, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if all(v is not None for v in pci):
+        ident = "pci:%s:%s:%s" % pci
+    elif getattr(props, "uuid", None) is not None:
+        ident = f"uuid:{props.uuid}"
+    else:
+        ident = f"index:{torch.cuda.current_device()}"
+    return f"{socket.gethostname()}/{ident}"
 
 
 class OneShotAllReduce:
@@ -43,6 +64,9 @@ class OneShotAllReduce:
         self.latency_us: Optional[float] = None   # measured at creation (probe_latency)
         self.fused = False                         # gemm_ar passed its self-test on every rank
         self.fused_saving_us: Optional[float] = None
+        self.distinct_gpus = False                  # every rank of the group on its own device
+        self.gather_ok = False                      # one-shot all-gather passed its self-test
+        self.gather_saving_us: Optional[float] = None
 
     def accepts_gemm(self, x: torch.Tensor, Ws: torch.Tensor) -> bool:
         """The fused row-parallel GEMM + all-reduce takes this decode shape."""
@@ -52,6 +76,20 @@ class OneShotAllReduce:
         N = Ws.shape[0]
         return (x.dtype == torch.bfloat16 and x.is_contiguous() and 1 <= M <= 16 and K % 32 == 0
                 and N % 16 == 0 and N // 16 <= 1024 and M * N <= self.cap and Ws.shape[1] == K)
+
+    def accepts_gather(self, x: torch.Tensor) -> bool:
+        """The one-shot all-gather takes this [rows, shard] slice (C3 logits)."""
+        if not (self.gather_ok and self.id is not None and x.is_cuda and x.dim() == 2):
+            return False
+        rows, shard = x.shape
+        return (x.dtype == torch.bfloat16 and x.is_contiguous() and shard % 8 == 0 and x.data_ptr() % 16 == 0
+                and rows * shard * self.world <= self._nat.oneshot_gather_capacity())
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        """[rows, shard] per rank -> [rows, world * shard] in rank order, one launch."""
+        out = torch.empty(x.shape[0], x.shape[1] * self.world, dtype=x.dtype, device=x.device)
+        self._nat.oneshot_allgather(self.id, x, out, self.world)
+        return out
 
     def gemm_ar(self, x: torch.Tensor, Ws: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``sum over ranks of x_r @ W_r^T`` ([M, N] bf16) with ``Ws`` = this rank's shuffled
@@ -124,16 +162,39 @@ def try_create(group, rank: int, world: int, cap_elems: int = DEFAULT_CAP_ELEMS)
         comm.close()
         return None
     comm.latency_us = probe_latency(comm, group)
-    if fused_enabled_by_env():
+    passed = self_test_gather(comm)
+    verdicts = [None] * world
+    dist.all_gather_object(verdicts, passed, group=group)
+    comm.gather_ok = all(verdicts)
+    # The fused form keeps a whole GEMM grid spinning on its peers' tiles. With one rank per GPU
+    # every workgroup is resident (<= 2 tiles per CU at decode shapes), so the wait always ends.
+    # Ranks SHARING a GPU (rehearsals) additionally need the other processes' kernels to be
+    # scheduled while those grids spin, which the hardware queue scheduler does not promise beyond
+    # two processes (a 4-rank rehearsal timed out) — there the separate K9 launch stays the default.
+    keys = [None] * world
+    dist.all_gather_object(keys, _device_key(), group=group)
+    comm.distinct_gpus = len(set(keys)) == world
+    mode = fused_mode_env()
+    if mode in ("1", "probe") or (mode == "auto" and comm.distinct_gpus):
         passed = self_test_fused(comm)
         verdicts = [None] * world
         dist.all_gather_object(verdicts, passed, group=group)
-        comm.fused = all(verdicts)
-        if comm.fused:
+        if all(verdicts):
+            # measure, don't guess: the fused form must beat GEMM + K9 on THIS node's links (the
+            # saving is the group max of each form's time, so every rank takes the same decision)
             comm.fused_saving_us = probe_fused_saving(comm, group)
+            expired = _group_max(torch.tensor([float(comm.error())], dtype=torch.float64), group,
+                                 torch.device("cuda", torch.cuda.current_device())) > 0
+            comm.clear_error()
+            comm.fused = mode == "1" or (not expired and comm.fused_saving_us >= MIN_FUSED_SAVING_US)
+    if comm.gather_ok and dist.get_backend(group) != "gloo":
+        # the one-shot gather replaces an RCCL all-gather: keep whichever this node runs faster
+        comm.gather_saving_us = probe_gather_saving(comm, group)
+        comm.gather_ok = comm.gather_saving_us > 0.0
     return comm
 
 
+MIN_FUSED_SAVING_US = 0.5          # per call, at the o-projection shard shape
 SELF_TEST_POLL_LIMIT = 1 << 20      # ~1 s of flag polling: a dead link fails fast, not in minutes
 
 
@@ -193,6 +254,36 @@ def _group_max(t: torch.Tensor, group, dev) -> float:
     return float(t.item())
 
 
+def self_test_gather(comm: OneShotAllReduce) -> bool:
+    """The one-shot all-gather against the known concatenation (rank-dependent integers, exact),
+    at the bench's logit-slice shape and a small one, both slots. Collective."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ok = True
+    try:
+        comm.set_poll_limit(SELF_TEST_POLL_LIMIT)
+        comm.gather_ok = True
+        for i, (rows, shard) in enumerate([(3, 128256 // comm.world), (1, 64), (2, 4096)]):
+            shard -= shard % 8
+            if not comm.accepts_gather(torch.empty(rows, shard, dtype=torch.bfloat16, device=dev)):
+                continue
+            cols = torch.arange(rows * shard, device=dev, dtype=torch.float32).view(rows, shard)
+            parts = [((cols + 5 * r + i) % 11) - 5 for r in range(comm.world)]
+            got = comm.all_gather_last(parts[comm.rank].to(torch.bfloat16).contiguous())
+            torch.cuda.synchronize(dev)
+            ok = ok and bool(torch.equal(got.float(), torch.cat(parts, dim=1)))
+        ok = ok and comm.error() == 0
+    except Exception:  # noqa: BLE001 - a launch failure is a failed self-test
+        ok = False
+    finally:
+        comm.gather_ok = False
+        try:
+            comm.clear_error()
+            comm.set_poll_limit(1 << 26)
+        except Exception:  # noqa: BLE001
+            ok = False
+    return ok
+
+
 def _fused_case(comm: OneShotAllReduce, M: int, N: int, K: int, seed: int):
     from .. import ops
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -235,6 +326,36 @@ def self_test_fused(comm: OneShotAllReduce) -> bool:
     return ok
 
 
+def _timed_us(fn, group, dev, iters: int = 50) -> float:
+    """Mean µs per call of ``fn`` over ``iters`` back-to-back launches, max over the group."""
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize(dev)
+    _group_max(torch.zeros(1, dtype=torch.float64), group, dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize(dev)
+    return _group_max(torch.tensor([s.elapsed_time(e) * 1e3 / iters], dtype=torch.float64), group, dev)
+
+
+def probe_gather_saving(comm: OneShotAllReduce, group) -> float:
+    """µs saved per C3 logits gather ([3, 128256 / world] bf16) by the one-shot all-gather vs the
+    process group's all-gather into [world, 3, shard] + the permute to [3, world * shard]."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    shard = (128256 // comm.world) // 8 * 8
+    x = torch.zeros(3, shard, dtype=torch.bfloat16, device=dev)
+    flat = torch.empty(comm.world * 3, shard, dtype=torch.bfloat16, device=dev)
+
+    def rccl():
+        dist.all_gather_into_tensor(flat, x, group=group)
+        flat.view(comm.world, 3, shard).movedim(0, -2).reshape(3, comm.world * shard)
+
+    return round(_timed_us(rccl, group, dev) - _timed_us(lambda: comm.all_gather_last(x), group, dev), 2)
+
+
 def probe_fused_saving(comm: OneShotAllReduce, group, iters: int = 50) -> float:
     """µs saved per row-parallel GEMM by the fused form vs GEMM + K9 at the bench's o-projection
     shard shape (M = 3, N = 4096, K = 4096 / world), max over ranks. Collective."""
@@ -242,20 +363,6 @@ def probe_fused_saving(comm: OneShotAllReduce, group, iters: int = 50) -> float:
     dev = torch.device("cuda", torch.cuda.current_device())
     x, Ws = _fused_case(comm, 3, 4096, max(32, 4096 // comm.world), 300)
     out = torch.empty(3, 4096, dtype=torch.bfloat16, device=dev)
-
-    def timed(fn) -> float:
-        for _ in range(5):
-            fn()
-        torch.cuda.synchronize(dev)
-        _group_max(torch.zeros(1, dtype=torch.float64), group, dev)
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(iters):
-            fn()
-        e.record()
-        torch.cuda.synchronize(dev)
-        return _group_max(torch.tensor([s.elapsed_time(e) * 1e3 / iters], dtype=torch.float64), group, dev)
-
-    sep = timed(lambda: comm(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE)))
-    fused = timed(lambda: comm.gemm_ar(x, Ws, out))
+    sep = _timed_us(lambda: comm(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE)), group, dev, iters)
+    fused = _timed_us(lambda: comm.gemm_ar(x, Ws, out), group, dev, iters)
     return round(sep - fused, 2)

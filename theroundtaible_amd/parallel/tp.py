@@ -127,9 +127,15 @@ class TPInfo:
         B = 3, Llama-3 vocab: ~10 µs spread over the tp-1 peer links). A Gumbel-argmax "accept"
         shortcut (csrc/sampling.hip) needs a fallback for rejected rows, which a captured graph
         cannot branch into, so it would not remove the gather either. Greedy decode, where one
-        (value, id) pair per rank is exact, uses :meth:`greedy_gather`."""
+        (value, id) pair per rank is exact, uses :meth:`greedy_gather`. On GPU groups the gather
+        runs as K9's one-shot all-gather (every rank pushes its slice into every peer's buffer,
+        csrc/oneshot_ar.hip) once that passed its creation self-test, else over RCCL."""
         if self.size == 1:
             return x
+        if self.oneshot is not None and self.oneshot.accepts_gather(x):
+            # one launch, one xGMI hop, written straight into [rows, tp * shard] (K9's comm)
+            self.oneshot_gathers = getattr(self, "oneshot_gathers", 0) + 1
+            return self.oneshot.all_gather_last(x)
         src = x.contiguous().cpu() if self._host_staged(x) else x.contiguous()
         # ONE all-gather into a [tp, rows, shard] buffer and ONE permuting copy (a list-output
         # all_gather + cat costs a copy kernel per rank on top, inside every decode step)

@@ -77,6 +77,31 @@ def main() -> int:
             assert err <= 0.0625, f"graph replay {rep} buf {i}: max err {err}"
             out["checks"] += 1
     assert ar.error() == 0, "a flag poll expired"
+    # one-shot all-gather (C3 logits) in a captured graph, interleaved with all-reduces (they share
+    # the comm's call counter): [3, shard] slices -> [3, world * shard] in rank order
+    out["gather_ok"] = ar.gather_ok
+    if ar.gather_ok:
+        shard = 16032
+        sl = torch.empty(3, shard, dtype=torch.bfloat16, device=dev)
+        red = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        gg = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(gg, stream=s):
+                g1 = ar.all_gather_last(sl)
+                ar(red)
+                g2 = ar.all_gather_last(sl)
+        for rep in range(3):
+            sl.copy_(data(rank, 3 * shard, 500 + rep, dev).view(3, shard))
+            red.copy_(data(rank, n, 600 + rep, dev))
+            dist.barrier()
+            gg.replay()
+            torch.cuda.synchronize()
+            want = torch.cat([data(r, 3 * shard, 500 + rep, "cpu").view(3, shard) for r in range(world)], dim=1)
+            assert torch.equal(g1.cpu(), want) and torch.equal(g2.cpu(), want), f"all-gather replay {rep}"
+            err = (red.float().cpu() - expect(world, n, 600 + rep)).abs().max().item()
+            assert err <= 0.0625, f"all-reduce between gathers, replay {rep}: max err {err}"
+            out["checks"] += 1
+        assert ar.error() == 0, "a flag poll expired (gather)"
     if a.bench:
         for n in (8192, 16 * 8192):
             x = data(rank, n, 7, dev)
@@ -92,6 +117,20 @@ def main() -> int:
                 gg.replay()
             torch.cuda.synchronize()
             out[f"oneshot_us_n{n}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+        if ar.gather_ok:
+            sl = data(rank, 3 * 16032, 8, dev).view(3, 16032)
+            gg = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(gg, stream=s):
+                    for _ in range(20):
+                        ar.all_gather_last(sl)
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                gg.replay()
+            torch.cuda.synchronize()
+            out["oneshot_gather_us_3x16032"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
             if backend == "nccl":
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
