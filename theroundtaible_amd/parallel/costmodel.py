@@ -40,8 +40,13 @@ class Calibration:
     # K9 one-shot all-reduce per call: 5.4 us between 2 ranks' IPC buffers on ONE GPU
     # (tools/oneshot_check.py --bench, r03); the xGMI hop is an ESTIMATE (no 8-GPU node yet)
     ar_us: float = 8.0
-    # vocab-parallel logits gather (RCCL all-gather inside the graph) per step: estimate
-    gather_us: float = 10.0
+    # vocab-parallel logits gather per step: K9's one-shot all-gather, 9.4-9.6 us for [3, 16032] ->
+    # [3, 32064] between 2 ranks sharing one GPU (profiles/r03/k9_fused_gather_shared_gpu.md); RCCL's
+    # ring all-gather + permute is the fallback the creation probe compares it with
+    gather_us: float = 9.5
+    # the fused row-parallel GEMM + all-reduce (EPI_AR) removes the K9 launch; its saving per call is
+    # measured by the creation probe on the node (bench detail k9_fused_saving_us), 0 until then
+    fused_ar_saving_us: float = 0.0
     sampler_us: float = 26.0        # K6 + step bookkeeping, ONE launch (profiles/r03/bench_final_kernels_25rounds.md)
     step_overhead_us: float = 5.0   # graph-replay gaps per step (the bookkeeping is inside K6)
     # prefill: effective GEMM + attention throughput of the chunked varlen prefill (r02: 52.6 ms
@@ -67,7 +72,7 @@ def decode_step_us(cfg: ModelConfig, tp: int, B: int, ctx_shared: int, ctx_priva
               "down": H * F * 2}
     per_layer = {k: cal.gemm_floor_us[k] + b / bw for k, b in shapes.items()}
     attn = cal.attn_floor_us + _attn_kv_bytes(cfg, tp, ctx_shared, ctx_private, B) / (cal.attn_tbps * 1e6)
-    ar = 2 * cal.ar_us if tp > 1 else 0.0
+    ar = 2 * max(0.0, cal.ar_us - cal.fused_ar_saving_us) if tp > 1 else 0.0
     L = cfg.n_layers
     lm = cal.gemm_floor_us["lm_head"] + (-(-cfg.vocab // tp)) * H * 2 / bw
     br = {"gemm": L * sum(per_layer.values()) + lm, "attention": L * attn, "allreduce": L * ar,

@@ -65,7 +65,12 @@ def main(paths) -> int:
         print(f"| {n} | {comp:.0f} | {dstep:.3f} | {par:.1f} | " + " | ".join(cells) + " |")
     print("\nK9 per call measured between ranks sharing one GPU (IPC, no xGMI hop): "
           "5.4 us (2 ranks, 16 KB) — tools/oneshot_check.py --bench, profiles/r03/k9_shared_gpu.log.")
-    print("The driver's 8-GPU run (SCALE_rNN.json) confirms or refutes the column that matches the real xGMI latency.")
+    print(f"Logits gather per step: {cal.gather_us} us (K9 one-shot all-gather, 2 ranks sharing one GPU, "
+          "profiles/r03/k9_fused_gather_shared_gpu.md).")
+    print("The driver's 8-GPU run (SCALE_rNN.json) confirms or refutes the column that matches the real xGMI latency; "
+          "its bench detail carries the node's own K9 latency (`k9_us`, measured at engine creation) and the "
+          "measured per-call saving of the fused GEMM + all-reduce (`k9_fused_saving_us`, used when > 0.5 us: "
+          "subtract it from the K9 column).")
     return 0
 
 
