@@ -128,6 +128,31 @@ def _overlap_order_ok(events) -> bool:
     return True
 
 
+def _predict(args, T: int, engine) -> dict:
+    """The cost model's prediction for THIS strong-scaling run (profiles/r03/tp_cost_model.md),
+    re-evaluated with the K9 latency / fused saving / gather cost the engine just measured on the
+    node's own links — so the driver's N-GPU record carries prediction and measurement side by
+    side. Only for the configuration the simulated compute was measured at."""
+    from theroundtaible_amd.parallel.costmodel import Calibration, load_simulated, strong_round_ms
+    simr = load_simulated(T)
+    if simr is None:
+        return {"available": False, "reason": f"no simulated tp{T} record (parallel/calib/sim{T}.json)"}
+    c = simr["config"]
+    same = (c["model"] == args.model and c["new_tokens_per_turn"] == args.new_tokens
+            and c["knights_per_table"] == args.knights_per_table and c["round_mode"] == args.round_mode
+            and c["prompt_layout"] == args.layout and simr["steps"] == args.steps and simr["warmup"] == args.warmup)
+    if not same:
+        return {"available": False, "reason": "configuration differs from the simulated run"}
+    os_ = getattr(engine.tp, "oneshot", None)
+    cal = Calibration()
+    k9 = os_.latency_us if os_ is not None and os_.latency_us else cal.ar_us
+    saving = os_.fused_saving_us if os_ is not None and os_.fused and os_.fused_saving_us else 0.0
+    gather = cal.gather_us    # one-shot gather as measured on one GPU; the probe keeps the faster of it / RCCL
+    return {"available": True, "simulated_compute_ms_per_round": simr["ms_per_round"],
+            "k9_us": k9, "fused_saving_us": saving, "gather_us": gather,
+            "predicted_ms_per_round": round(strong_round_ms(simr, T, k9, gather, saving), 1)}
+
+
 def main() -> int:
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -341,6 +366,8 @@ def main() -> int:
                    "engine_decode_ms_per_round": round(sum(dec_ms.values()) / n_timed, 2),
                    "host_ms_per_round": round(ms_round - sum(eng_ms.values()) / n_timed, 2)},
     }
+    if cl.rank == 0 and not sim and args.scaling == "strong" and T > 1 and n_tables == 1:
+        out["detail"]["prediction"] = _predict(args, T, engine)
     if args.c1_events:
         with open(f"{args.c1_events}.r{cl.rank}.json", "w") as f:
             json.dump({"rank": cl.rank, "events": pool.events, "ns": pool.event_ns}, f)

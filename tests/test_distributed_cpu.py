@@ -235,6 +235,24 @@ def test_strong_scaling_bench_one_table_tp(nproc):
     assert out["config"]["tables"] == 1 and out["config"]["knights"] == 3
     assert out["config"]["parallelism"] == f"tp{nproc}" and out["config"]["tp"] == nproc
     assert out["detail"]["decode_tokens"] == 3 * 8 * 2 and out["detail"]["failed_turns"] == 0
+    # the cost-model prediction rides along only for the configuration it was measured at
+    assert out["detail"]["prediction"]["available"] is False
+
+
+def test_strong_prediction_matches_cost_model_table():
+    """bench.py's per-run prediction (detail.prediction) is the tools/tp_cost.py curve: the
+    simulated rank-0 compute of that tp + 2L K9 calls and one gather per step + prefill rings."""
+    from theroundtaible_amd.parallel.costmodel import load_simulated, strong_round_ms
+    for n, want in ((2, 1345), (4, 1032), (8, 915)):      # profiles/r03/tp_cost_model.md, K9 5 us
+        sim = load_simulated(n)
+        assert sim is not None and sim["config"]["tp"] == n
+        assert abs(strong_round_ms(sim, n, 5.0, 9.5) - want) < 1.0
+    one = load_simulated(1)
+    assert strong_round_ms(one, 1, 5.0, 9.5) == one["ms_per_round"]
+    # a fused all-reduce that saves s us per call removes 2L x s per step
+    sim8 = load_simulated(8)
+    d = strong_round_ms(sim8, 8, 8.0, 9.5) - strong_round_ms(sim8, 8, 8.0, 9.5, fused_saving_us=3.0)
+    assert abs(d - 512 * 2 * 32 * 3.0 / 1e3) < 1e-6
 
 
 def test_strong_scaling_matches_single_rank_tokens():

@@ -163,3 +163,38 @@ def split_plans(model: str, knights: int, n_gpus: int, fits=None, **kw) -> List[
             out.append((ms, [(k, t) for k in sizes]))
     out.sort(key=lambda x: (x[0], sum(t for _, t in x[1])))
     return out
+
+
+# bench.py --simulate-tp N records of the driver configuration (copies of profiles/r03/sim*.json,
+# the tools/tp_cost.py inputs), shipped with the package: bench.py reads them on the GPU box
+SIM_DIR = __import__("os").path.join(__import__("os").path.dirname(__file__), "calib")
+
+
+def load_simulated(n: int) -> Optional[dict]:
+    """The ``bench.py --simulate-tp n`` record (``sim{n}.json``; n = 1 is the plain 1-GPU run)."""
+    import json
+    import os
+    path = os.path.join(SIM_DIR, f"sim{n}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def strong_round_ms(sim: dict, n: int, k9_us: float, gather_us: float, fused_saving_us: float = 0.0,
+                    cal: Optional[Calibration] = None) -> float:
+    """Predicted ms per round of the strong-scaling bench on n GPUs: the simulated rank-0 compute
+    of that tp (collectives elided) + per decode step 2L effective all-reduces (K9 latency minus
+    the fused form's saving) and one logits gather + the prefill ring all-reduces."""
+    cal = cal or Calibration()
+    cfg = get_config(sim["config"]["model"].split(" ")[0])
+    steps = sim["config"]["new_tokens_per_turn"]
+    comp = sim["ms_per_round"]
+    if n == 1:
+        return comp
+    ar = max(0.0, k9_us - fused_saving_us)
+    decode_comm = steps * (2 * cfg.n_layers * ar + gather_us) / 1e3
+    pre_tok = sim["detail"]["prefill_tokens"] / max(1, sim["steps"])
+    msg = pre_tok * cfg.hidden * 2
+    prefill_ar = 2 * cfg.n_layers * (2 * (n - 1) / n * msg / (cal.prefill_ar_gbps * 1e9) * 1e3 + 0.02)
+    return comp + decode_comm + prefill_ar

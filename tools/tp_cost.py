@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main(paths) -> int:
     from theroundtaible_amd.models.config import get_config
-    from theroundtaible_amd.parallel.costmodel import Calibration
+    from theroundtaible_amd.parallel.costmodel import Calibration, strong_round_ms
     sims = {}
     for p in paths:
         d = json.load(open(p))
@@ -55,12 +55,11 @@ def main(paths) -> int:
         d = sims[n]
         comp = d["ms_per_round"]
         dstep = d["detail"]["engine_decode_ms_per_round"] / steps
-        msg = pre_tok * cfg.hidden * 2
-        par = 0.0 if n == 1 else 2 * L * (2 * (n - 1) / n * msg / (cal.prefill_ar_gbps * 1e9) * 1e3 + 0.02)
+        # the prefill ring all-reduces alone = the prediction with free decode collectives
+        par = strong_round_ms(d, n, 0.0, 0.0, cal=cal) - comp
         cells = []
         for us in (5, 8, 12, 20):
-            comm = 0.0 if n == 1 else steps * (2 * L * us + cal.gather_us) / 1e3
-            tot = comp + comm + par
+            tot = strong_round_ms(d, n, us, cal.gather_us, cal=cal)
             cells.append(f"{tot:.0f} ({dec_tok / tot * 1e3:.0f})")
         print(f"| {n} | {comp:.0f} | {dstep:.3f} | {par:.1f} | " + " | ".join(cells) + " |")
     print("\nK9 per call measured between ranks sharing one GPU (IPC, no xGMI hop): "
