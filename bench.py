@@ -280,15 +280,17 @@ def main() -> int:
     last = min(rounds, args.consensus_round) if args.consensus_round else rounds
     timed = range(args.warmup + 1, last + 1)
     dec = pre = reused = forced = 0
-    # engine time per timed round (the slowest turn of the round: turns of one engine batch run
-    # together) vs the round's wall clock: the rest is host work (prompts, parse, files, C1)
+    # engine time per timed round (parallel: the slowest turn of the round, turns of one engine
+    # batch run together) vs the round's wall clock: the rest is host work (prompts, parse, files, C1)
     eng_ms, pre_ms, dec_ms = {}, {}, {}
+    # (sequential rounds: the knights' turns run one after another, so their engine times add up)
+    agg = (lambda a, b: a + b) if args.round_mode == "sequential" else max
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
-                eng_ms[e.round] = max(eng_ms.get(e.round, 0.0), float(e.metrics.get("turn_ms", 0.0)))
-                pre_ms[e.round] = max(pre_ms.get(e.round, 0.0), float(e.metrics.get("prefill_ms", 0.0)))
-                dec_ms[e.round] = max(dec_ms.get(e.round, 0.0), float(e.metrics.get("decode_ms", 0.0)))
+                eng_ms[e.round] = agg(eng_ms.get(e.round, 0.0), float(e.metrics.get("turn_ms", 0.0)))
+                pre_ms[e.round] = agg(pre_ms.get(e.round, 0.0), float(e.metrics.get("prefill_ms", 0.0)))
+                dec_ms[e.round] = agg(dec_ms.get(e.round, 0.0), float(e.metrics.get("decode_ms", 0.0)))
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
