@@ -82,13 +82,13 @@ class OneShotAllReduce:
         if not (self.gather_ok and self.id is not None and x.is_cuda and x.dim() == 2):
             return False
         rows, shard = x.shape
-        return (x.dtype == torch.bfloat16 and x.is_contiguous() and shard % 8 == 0 and x.data_ptr() % 16 == 0
+        return (x.dtype == torch.bfloat16 and x.is_contiguous() and shard % 8 == 0
                 and rows * shard * self.world <= self._nat.oneshot_gather_capacity())
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """[rows, shard] per rank -> [rows, world * shard] in rank order, one launch."""
         out = torch.empty(x.shape[0], x.shape[1] * self.world, dtype=x.dtype, device=x.device)
-        self._nat.oneshot_allgather(self.id, x, out, self.world)
+        self._nat.oneshot_allgather(self.id, _aligned(x), out, self.world)
         return out
 
     def gemm_ar(self, x: torch.Tensor, Ws: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -96,14 +96,22 @@ class OneShotAllReduce:
         row-parallel shard: one launch, the K9 exchange in the epilogue."""
         if out is None:
             out = torch.empty(x.shape[0], Ws.shape[0], dtype=x.dtype, device=x.device)
-        self._nat.oneshot_gemm_ar(self.id, out, x, Ws)
+        self._nat.oneshot_gemm_ar(self.id, out, _aligned(x), Ws)
         return out
 
     def accepts(self, x: torch.Tensor) -> bool:
+        # rank-invariant conditions only (shape, dtype, layout): every rank of the group must take
+        # the same path, so a rank-dependent property such as the address alignment is handled
+        # by staging (__call__), never by falling back on one rank alone
         return (self.id is not None and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
-                and x.numel() % 8 == 0 and 0 < x.numel() <= self.cap and x.data_ptr() % 16 == 0)
+                and x.numel() % 8 == 0 and 0 < x.numel() <= self.cap)
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if x.data_ptr() % 16:
+            t = x.clone()                 # fresh allocations are 16-B aligned
+            self._nat.oneshot_allreduce(self.id, t)
+            x.copy_(t)
+            return x
         self._nat.oneshot_allreduce(self.id, x)
         return x
 
@@ -123,6 +131,11 @@ class OneShotAllReduce:
         if self.id is not None:
             self._nat.oneshot_destroy(self.id)
             self.id = None
+
+
+def _aligned(x: torch.Tensor) -> torch.Tensor:
+    """``x`` itself when 16-B aligned (the kernels' vector loads), else an aligned copy."""
+    return x if x.data_ptr() % 16 == 0 else x.clone()
 
 
 def try_create(group, rank: int, world: int, cap_elems: int = DEFAULT_CAP_ELEMS) -> Optional[OneShotAllReduce]:
