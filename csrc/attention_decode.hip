@@ -90,13 +90,15 @@ __global__ void __launch_bounds__(256) decode_combine_kernel(AttnArgs p) {
 
 
 // q [B, Hq, D]; k_cache [NB, Hkv, 32, D]; v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32;
+// defer_combine: leave the separate combine to the caller (*deferred = 1 when it was needed);
 // part_o >= B*Hq*slot_stride*D floats, part_ml >= B*Hq*slot_stride*4 floats, counters >= B*Hkv ints
 // (zeroed once). groups: nullptr or [B][3] {first, n, shared blocks} (shared-prefix groups,
 // attn_core.h); slot_stride >= max n * num_splits (0 = num_splits, no groups).
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
-                        hipStream_t stream) {
+                        hipStream_t stream, int defer_combine, int* deferred) {
+  if (deferred != nullptr) *deferred = 0;
   if (B == 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16) return -1;
   if (num_splits < 1) num_splits = 1;
@@ -129,7 +131,10 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   else if (D == 64) RT_PD(64);
   else return -2;
 #undef RT_PD
-  if (args.ext_combine) {
+  if (args.ext_combine && defer_combine && D == 128) {
+    // the caller runs the combine inside the next launch (combine_o.hip: combine + o-projection)
+    if (deferred != nullptr) *deferred = 1;
+  } else if (args.ext_combine) {
     const dim3 cgrid(B * Hq, D / 32);
     if (D == 128) hipLaunchKernelGGL(decode_combine_kernel<128>, cgrid, dim3(256), 0, stream, args);
     else hipLaunchKernelGGL(decode_combine_kernel<64>, cgrid, dim3(256), 0, stream, args);

@@ -18,7 +18,7 @@ void launch_gelu(void* out, const void* x, int64_t n, hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
-                        hipStream_t stream);
+                        hipStream_t stream, int defer_combine, int* deferred);
 int prefill_rows_per_tile(int G, int D);
 int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                    const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv, int D,
@@ -155,10 +155,10 @@ void rope_and_cache(torch::Tensor q_out, torch::Tensor qkv, torch::Tensor positi
                     rope, cur_stream());
 }
 
-void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
-                            torch::Tensor block_tables, torch::Tensor ctx_lens, double scale, int64_t num_splits,
-                            torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor counters,
-                            c10::optional<torch::Tensor> groups, int64_t slot_stride) {
+int64_t paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
+                               torch::Tensor block_tables, torch::Tensor ctx_lens, double scale, int64_t num_splits,
+                               torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor counters,
+                               c10::optional<torch::Tensor> groups, int64_t slot_stride, bool defer_combine) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
@@ -183,13 +183,15 @@ void paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_
               "split workspace too small");
   check_type(counters, torch::kInt32, "counters");
   TORCH_CHECK(counters.numel() >= B * k_cache.size(1), "split counters too small");
+  int deferred = 0;
   const int rc = launch_paged_decode(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                      block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), part_o.data_ptr<float>(),
                                      part_ml.data_ptr<float>(), counters.data_ptr<int>(), (int)B, (int)Hq,
                                      (int)k_cache.size(1), (int)D,
                                      (int)block_tables.size(1), (float)scale, (int)num_splits, gp, (int)stride,
-                                     cur_stream());
+                                     cur_stream(), defer_combine ? 1 : 0, &deferred);
   TORCH_CHECK(rc == 0, "paged_attention_decode: unsupported configuration (rc=", rc, ")");
+  return deferred;
 }
 
 void prefill_attention(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
@@ -627,7 +629,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("paged_attention_decode", &paged_attention_decode, py::arg("out"), py::arg("q"), py::arg("k_cache"),
         py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("scale"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("counters"), py::arg("groups") = py::none(),
-        py::arg("slot_stride") = 0);
+        py::arg("slot_stride") = 0, py::arg("defer_combine") = false);
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile, py::arg("G"), py::arg("D") = 128);
   m.def("prefill_attention", &prefill_attention);
   m.def("silu_and_mul", &silu_and_mul);

@@ -16,7 +16,7 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
-                        hipStream_t stream);
+                        hipStream_t stream, int defer_combine, int* deferred);
 int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
                         int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream);
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,
@@ -63,16 +63,16 @@ int main() {
   EXPECT(launch_shuffle_weight(nullptr, nullptr, nullptr, 48, 64, 0, 0, 1, nullptr) == -1);      // SwiGLU halves of 24 rows
   // decode attention: group size, head dim, split range
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 30, 8,
-                             128, 4, 0.1f, 4, nullptr, 0, nullptr) == -1);
+                             128, 4, 0.1f, 4, nullptr, 0, nullptr, 0, nullptr) == -1);
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 64, 2,
-                             128, 4, 0.1f, 4, nullptr, 0, nullptr) == -1);   // G = 32 > 16
+                             128, 4, 0.1f, 4, nullptr, 0, nullptr, 0, nullptr) == -1);   // G = 32 > 16
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 32, 8,
-                             128, 4, 0.1f, 65, nullptr, 0, nullptr) == -3);  // splits > MAXS
+                             128, 4, 0.1f, 65, nullptr, 0, nullptr, 0, nullptr) == -3);  // splits > MAXS
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 32, 8,
-                             128, 4, 0.1f, 4, nullptr, 0, nullptr) == 0);    // empty batch: no launch
+                             128, 4, 0.1f, 4, nullptr, 0, nullptr, 0, nullptr) == 0);    // empty batch: no launch
   static const int grp[3] = {0, 1, 0};
   EXPECT(launch_paged_decode(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 2, 32, 8,
-                             128, 4, 0.1f, 4, grp, 2, nullptr) == -4);   // group slots < splits
+                             128, 4, 0.1f, 4, grp, 2, nullptr, 0, nullptr) == -4);   // group slots < splits
   // K8 block copy: empty list launches nothing; unaligned block size / empty layer set refused
   EXPECT(launch_kv_block_copy(nullptr, nullptr, nullptr, nullptr, 0, 32, 16, 8192, nullptr) == 0);
   EXPECT(launch_kv_block_copy(nullptr, nullptr, nullptr, nullptr, 2, 32, 16, 8190, nullptr) == -1);

@@ -162,9 +162,10 @@ class LlamaModel:
     def forward_decode_fused(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
                              hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Decode step with every norm / residual / activation fused into the MFMA GEMMs
-        (csrc/gemm_skinny.hip): per layer qkv(+RMSNorm, +RoPE/KV-cache write) -> K3 (split-KV
-        combined in-kernel) -> o(+residual) -> gate_up(+RMSNorm, SwiGLU) -> down(+residual).
-        5 launches per layer, no norm / rope / reduce kernels."""
+        (csrc/gemm_skinny.hip): per layer qkv(+RMSNorm, +RoPE/KV-cache write) -> K3 (+ its split
+        combine launch) -> o(+residual) -> gate_up(+RMSNorm, SwiGLU) -> down(+residual); no norm /
+        rope / reduce kernels. (Folding the combine into the o launch measured slower:
+        tools/experiments/combine_o.hip.)"""
         cfg = self.cfg
         eps = cfg.norm_eps
         dec = self.decode_weights()

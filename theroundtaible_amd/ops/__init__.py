@@ -115,7 +115,8 @@ class DecodeWorkspace:
         # per-(sequence, kv head) split arrival counters; the kernel re-arms them to 0 itself.
         # Sized by n_heads (>= n_kv_heads) so one workspace serves every GQA ratio.
         self.counters = torch.zeros(max_batch * n_heads, dtype=torch.int32, device=device)
-        # persistent decode-layer kernel: phase counters (self-re-arming) and the poll-expiry flag
+        # persistent / experiment kernels: phase counters (self-re-arming) and the poll-expiry flag
+        # (tools/experiments: decode_layer.hip, combine_o.hip)
         self.sync = torch.zeros(8, dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
 

@@ -1,6 +1,7 @@
 // pybind11 bindings of the EXPERIMENT kernels kept out of the product extension (measured
 // slower than the five-launch fused decode or never adopted; profiles/experiments/): the
-// persistent decode layer, the loader-wave LDS-ring GEMM and the MALL prefetch. Built on demand
+// persistent decode layer, the loader-wave LDS-ring GEMM, the MALL prefetch and the split combine
+// folded into the o-projection launch. Built on demand
 // by tools/experiments/build_exp.py into tools/experiments/_exp*.so.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
@@ -16,6 +17,9 @@ int decode_layer_grid();
 int launch_ring_gemm(void* out, const void* x, const void* Ws, int M, int N, int K, int grid, int variant,
                      hipStream_t stream);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
+int launch_combine_o(void* attn_out, const float* part_o, const float* part_ml, const int* groups, int stride,
+                     int num_splits, int B, int Hq, int Hkv, int D, const void* Ws, void* res, int N, int* bar,
+                     int* err, hipStream_t stream);
 
 namespace {
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -100,6 +104,39 @@ void prefetch(torch::Tensor t, int64_t nwg, torch::Tensor sink) {
   launch_prefetch(t.data_ptr(), t.numel() * t.element_size(), (int)nwg, (uint32_t*)sink.data_ptr(), cur_stream());
 }
 
+// K3 split combine + o-projection + residual in one launch (tools/experiments/combine_o.hip), after a
+// paged_attention_decode call that returned 1 (combine deferred) with the same workspace.
+void combine_o_gemm(torch::Tensor attn_out, torch::Tensor part_o, torch::Tensor part_ml,
+                    c10::optional<torch::Tensor> groups, int64_t slot_stride, int64_t num_splits, int64_t Hkv,
+                    torch::Tensor Ws, torch::Tensor res, torch::Tensor bar, torch::Tensor err) {
+  check_bf16(attn_out, "attn_out");
+  check_bf16(Ws, "Ws");
+  check_bf16(res, "res");
+  TORCH_CHECK(attn_out.dim() == 3, "attn_out must be [B, Hq, D]");
+  const int64_t B = attn_out.size(0), Hq = attn_out.size(1), D = attn_out.size(2);
+  TORCH_CHECK(Ws.dim() == 2 && Ws.size(1) == Hq * D && res.dim() == 2 && res.size(0) == B && res.size(1) == Ws.size(0),
+              "combine_o_gemm: Ws [N, Hq*D], res [B, N]");
+  check_type(part_o, torch::kFloat32, "partial_o");
+  check_type(part_ml, torch::kFloat32, "partial_ml");
+  check_type(bar, torch::kInt32, "bar");
+  check_type(err, torch::kInt32, "err");
+  TORCH_CHECK(bar.numel() >= 2 && err.numel() >= 1, "combine_o_gemm: bar [2], err [1]");
+  const int* gp = nullptr;
+  int64_t stride = num_splits;
+  if (groups.has_value() && groups->defined()) {
+    check_type(*groups, torch::kInt32, "groups");
+    TORCH_CHECK(groups->numel() >= 3 * B && slot_stride >= num_splits, "groups / slot_stride");
+    gp = groups->data_ptr<int>();
+    stride = slot_stride;
+  }
+  TORCH_CHECK(part_o.numel() >= B * Hq * stride * D && part_ml.numel() >= B * Hq * stride * 4, "split workspace too small");
+  const int rc = launch_combine_o(attn_out.data_ptr(), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), gp,
+                                  (int)stride, (int)num_splits, (int)B, (int)Hq, (int)Hkv, (int)D, Ws.data_ptr(),
+                                  res.data_ptr(), (int)Ws.size(0), bar.data_ptr<int>(), err.data_ptr<int>(),
+                                  cur_stream());
+  TORCH_CHECK(rc == 0, "combine_o_gemm: unsupported configuration (rc=", rc, ")");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_exp, m) {
@@ -112,4 +149,7 @@ PYBIND11_MODULE(_exp, m) {
   m.def("ring_gemm_exp", &ring_gemm_exp, py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("grid") = 0,
         py::arg("variant") = 0);
   m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));
+  m.def("combine_o_gemm", &combine_o_gemm, py::arg("attn_out"), py::arg("part_o"), py::arg("part_ml"),
+        py::arg("groups"), py::arg("slot_stride"), py::arg("num_splits"), py::arg("Hkv"), py::arg("Ws"),
+        py::arg("res"), py::arg("bar"), py::arg("err"));
 }
