@@ -627,10 +627,23 @@ def cmd_bench(args, ui: UI) -> int:
 
 
 def cmd_serve(args, ui: UI) -> int:
+    tp = max(1, int(getattr(args, "tp", 1) or 1))
+    if tp > 1 and "WORLD_SIZE" not in os.environ:
+        # one rank per GPU of the tensor-parallel group, started before any GPU call
+        from .parallel.launch import launch_ranks
+        if args.device != "cpu":
+            import torch     # device_count() does not initialise the GPU on this image
+            if torch.cuda.device_count() < tp:
+                raise ConfigError(f"serve --tp {tp} needs {tp} GPUs, {torch.cuda.device_count()} visible",
+                                  hint="Lower --tp, or run on a node with enough GPUs.")
+        return launch_ranks(tp, list(getattr(args, "raw_argv", sys.argv[1:])), args.device == "cpu",
+                            f"serve {args.model} tp={tp}")
     from .serve import build_server
     srv = build_server(args.model, weights=args.weights, device=args.device, dtype=args.dtype, host=args.host,
                        port=args.port, max_batch=args.max_batch, max_tokens=args.max_tokens,
-                       use_graphs=not args.no_graphs, num_blocks=args.num_blocks)
+                       use_graphs=not args.no_graphs, num_blocks=args.num_blocks, tp=tp)
+    if srv is None:            # a follower rank of serve --tp N: served rank 0 until shutdown
+        return 0
     ui.ok(f"  ✓ {args.model} on {srv.engine.device}: {srv.engine.kv_capacity_tokens} KV tokens resident capacity")
     ui.dim(f"  serving {srv.url}/v1/chat/completions  (OpenAI)  and  {srv.url}/api/chat  (Ollama)")
     try:
@@ -733,6 +746,8 @@ def build_parser() -> argparse.ArgumentParser:
     sv.add_argument("--max-tokens", type=int, default=512, help="default completion budget per request")
     sv.add_argument("--num-blocks", type=int, default=None, help="KV blocks (default: sized from free memory)")
     sv.add_argument("--no-graphs", action="store_true")
+    sv.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree: serve one model over N GPUs (N ranks; rank 0 serves HTTP)")
     sv.set_defaults(fn=cmd_serve)
     b = sub.add_parser("bench", help="Run the roundtable benchmark (wraps bench.py)")
     b.add_argument("bench_args", nargs=argparse.REMAINDER)
@@ -753,6 +768,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     apply_debug_env()          # ROUNDTABLE_DEBUG=1: serialized kernels + paging guards (before any HIP call)
     raw_argv = list(sys.argv[1:] if argv is None else argv)
     args = build_parser().parse_args(argv)
+    args.raw_argv = raw_argv
     ui = UI(quiet=args.quiet)
     try:
         if args.fn in (cmd_discuss, cmd_summon, cmd_apply, cmd_code_red):

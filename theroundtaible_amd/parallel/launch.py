@@ -91,6 +91,12 @@ def maybe_relaunch(argv: List[str], root: Optional[str] = None, quiet: bool = Fa
             raise ConfigError(f"the knight placement needs {n} GPU ranks ({why}) but {have} GPU(s) are visible",
                               hint="Lower engine.tp / engine.gpus in .roundtable/config.json, or run on a "
                                    "node with enough GPUs.")
+    return launch_ranks(n, argv, cpu, why, quiet)
+
+
+def launch_ranks(n: int, argv: List[str], cpu: bool, why: str, quiet: bool = False) -> int:
+    """Run ``roundtable <argv>`` as ``n`` SPMD ranks (a child ``torch.distributed.run``, started
+    before this process touches a GPU) and return its exit code."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -103,5 +109,5 @@ def maybe_relaunch(argv: List[str], root: Optional[str] = None, quiet: bool = Fa
     if cpu:
         env.setdefault("OMP_NUM_THREADS", "1")
     if not quiet:
-        print(f"  Launching {n} ranks for the knight placement ({why})", file=sys.stderr, flush=True)
+        print(f"  Launching {n} ranks ({why})", file=sys.stderr, flush=True)
     return subprocess.run(cmd, env=env).returncode

@@ -12,6 +12,14 @@ Serving model:
 
 * one :class:`~theroundtaible_amd.engine.Engine` per process (one process per GPU; run
   several ``serve`` processes for several GPUs);
+* a model too large or too slow for one GPU is served **tensor-parallel** (``serve --tp N``:
+  N ranks, one per GPU, the Megatron split of parallel/tp.py with K9 / RCCL collectives): rank 0
+  runs the HTTP front end and the scheduler on a :class:`MirroredEngine`, which broadcasts every
+  engine operation (admit = prefill + first token, decode chunk, release) over the gloo control
+  plane before running it; ranks 1..N-1 execute the same operations in the same order
+  (:func:`serve_follower`), so every collective inside them lines up. Sampling is a counter RNG
+  keyed by (seed, sequence, position) over all-gathered logits, so every rank draws the same
+  tokens; rank 0's are the ones returned;
 * continuous batching (:class:`Scheduler`): between decode chunks finished requests leave
   and waiting ones are prefilled and join, so concurrent clients share one hipGraph replay
   per token (up to ``max_batch``) — the batching the round table uses for parallel knights;
@@ -227,6 +235,65 @@ class Scheduler:
             active = still
 
 
+class MirroredEngine:
+    """Rank 0's view of a tensor-parallel engine: the scheduler's engine operations are announced
+    to the follower ranks (:func:`serve_follower`) over the control plane, then run locally —
+    the followers run the same call with the same arguments, so the TP collectives inside
+    match. Everything else (tokenizer, stats, capacity, health) reads the local engine."""
+
+    def __init__(self, engine: Engine, cluster):
+        self._engine, self._cluster = engine, cluster
+        self._lock = threading.Lock()    # one announced operation at a time, in issue order
+
+    def __getattr__(self, name):
+        return getattr(self._engine, name)
+
+    def _announce(self, op: tuple) -> None:
+        self._cluster.broadcast_object(op)
+
+    def start_turns(self, turns):
+        with self._lock:
+            self._announce(("start", list(turns)))
+            return self._engine.start_turns(turns)
+
+    def continue_decode(self, seqs, turns, last, steps):
+        with self._lock:
+            self._announce(("decode", [s.key for s in seqs], list(turns), [int(x) for x in last], int(steps)))
+            return self._engine.continue_decode(seqs, turns, last, steps)
+
+    def release(self, key: str) -> None:
+        with self._lock:
+            self._announce(("release", key))
+            self._engine.release(key)
+
+    def stop_followers(self) -> None:
+        with self._lock:
+            self._announce(("stop",))
+
+
+def serve_follower(engine: Engine, cluster) -> int:
+    """Ranks 1..N-1 of ``serve --tp N``: run rank 0's engine operations in its order until it
+    announces ``stop``. Returns the number of operations executed. An operation that raises
+    here raises on rank 0 too (same inputs, agreed device-flag checks), which reports it."""
+    n = 0
+    while True:
+        op = cluster.broadcast_object(None)
+        kind = op[0]
+        if kind == "stop":
+            return n
+        try:
+            if kind == "start":
+                engine.start_turns(op[1])
+            elif kind == "decode":
+                seqs = [engine.kv.seqs[k] for k in op[1]]
+                engine.continue_decode(seqs, op[2], op[3], op[4])
+            elif kind == "release":
+                engine.release(op[1])
+        except Exception:  # noqa: BLE001 - rank 0 reports the request's error
+            pass
+        n += 1
+
+
 @dataclass
 class _Output:
     text: str
@@ -283,7 +350,8 @@ class RoundtableServer:
                          "owned_by": "theroundtaible-amd"}]})
                 elif self.path.rstrip("/") in ("/health", ""):
                     self._send(200, {"status": "ok" if server.engine.healthy else "unhealthy",
-                                     "model": server.model_name, "device": str(server.engine.device)})
+                                     "model": server.model_name, "device": str(server.engine.device),
+                                     "tp": int(server.engine.tp.size)})
                 elif self.path.rstrip("/") == "/metrics":
                     self._send(200, server.metrics_text(), "text/plain; version=0.0.4")
                 else:
@@ -460,17 +528,39 @@ class RoundtableServer:
         self.httpd.shutdown()
         self.httpd.server_close()
         self.sched.close()
+        if isinstance(self.engine, MirroredEngine):
+            self.engine.stop_followers()
 
 
 def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", dtype: str = "bf16",
                  host: str = "127.0.0.1", port: int = 8000, max_batch: int = 16, max_tokens: int = 512,
-                 use_graphs: bool = True, num_blocks: Optional[int] = None) -> RoundtableServer:
+                 use_graphs: bool = True, num_blocks: Optional[int] = None,
+                 tp: int = 1) -> Optional[RoundtableServer]:
+    """The server (rank 0), or — on a follower rank of a ``tp > 1`` launch — None after that
+    rank has served rank 0's operations until shutdown."""
     # a checkpoint directory defines the architecture: preset + shape overrides from config.json
     from .utils.local_detect import resolve_model
     model, overrides = resolve_model(model, weights)
+    cluster, tpi = None, None
+    if tp > 1:
+        import torch.distributed as dist
+        from .parallel.cluster import init_cluster
+        from .parallel.tp import TPInfo
+        cluster = init_cluster(prefer_gpu=device != "cpu")
+        if cluster.world != tp:
+            raise ValueError(f"serve --tp {tp} needs {tp} ranks, {cluster.world} joined")
+        tpi = TPInfo(size=tp, rank=cluster.rank, group=dist.group.WORLD)
+        if device != "cpu":
+            device = cluster.device
     ecfg = EngineConfig(model=model, weights=weights, device=device, dtype=dtype, use_graphs=use_graphs,
                         max_batch=max_batch, num_blocks=num_blocks, model_overrides=overrides)
     if ecfg.device == "cpu":
         ecfg.dtype = "fp32" if dtype == "bf16" else dtype
         ecfg.use_graphs = False
+    if tpi is not None:
+        engine = Engine(ecfg, tpi)
+        if cluster.rank != 0:
+            serve_follower(engine, cluster)
+            return None
+        return RoundtableServer(MirroredEngine(engine, cluster), model, host, port, max_batch, max_tokens)
     return RoundtableServer(Engine(ecfg), model, host, port, max_batch, max_tokens)
