@@ -38,6 +38,20 @@ def _ask(url, prompts):
     return out
 
 
+def _stop(p):
+    """End the process group this test started (launcher + ranks), if still running."""
+    for sig, wait in ((signal.SIGTERM, 30), (signal.SIGKILL, 30)):
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            break
+        try:
+            p.wait(timeout=wait)
+            break
+        except subprocess.TimeoutExpired:
+            continue
+
+
 def test_serve_tp2_matches_tp1():
     prompts = ["De ronde tafel opent de zitting.", "Welke ridder spreekt eerst?", "Een korte vraag."]
     ref = build_server("tiny-llama", weights="random-full:1", device="cpu", port=0, max_batch=4, max_tokens=8,
@@ -74,12 +88,7 @@ def test_serve_tp2_matches_tp1():
         metrics = urllib.request.urlopen(url + "/metrics", timeout=10).read().decode()
         assert "roundtable_requests_total 4" in metrics
     finally:
-        os.killpg(p.pid, signal.SIGTERM)       # the process group this test started (launcher + ranks)
-        try:
-            p.wait(timeout=30)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait(timeout=30)
+        _stop(p)
 
 
 def _serve_proc(extra_env, args, port):
@@ -123,9 +132,4 @@ def test_serve_tp2_on_shared_gpu():
         metrics = urllib.request.urlopen(url + "/metrics", timeout=10).read().decode()
         assert "roundtable_requests_total 4" in metrics and "roundtable_request_errors_total 0" in metrics, metrics
     finally:
-        os.killpg(p.pid, signal.SIGTERM)
-        try:
-            p.wait(timeout=30)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait(timeout=30)
+        _stop(p)

@@ -631,7 +631,8 @@ def cmd_serve(args, ui: UI) -> int:
     if tp > 1 and "WORLD_SIZE" not in os.environ:
         # one rank per GPU of the tensor-parallel group, started before any GPU call
         from .parallel.launch import launch_ranks
-        if args.device != "cpu":
+        # (ROUNDTABLE_DIST_BACKEND=gloo: the rehearsal mode of parallel/cluster.py, ranks share GPUs)
+        if args.device != "cpu" and os.environ.get("ROUNDTABLE_DIST_BACKEND", "").lower() != "gloo":
             import torch     # device_count() does not initialise the GPU on this image
             if torch.cuda.device_count() < tp:
                 raise ConfigError(f"serve --tp {tp} needs {tp} GPUs, {torch.cuda.device_count()} visible",
