@@ -97,6 +97,9 @@ def parse():
                         "ends in a forced consensus JSON scoring 6, then 9 in this round, so the tables reach "
                         "consensus and stop there (0 = off; use warmup + steps to end inside the timed region)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    p.add_argument("--write-calibration", default=None,
+                   help="(N > 1) write the node's measured K9 latency / fused saving as a cost-model calibration "
+                        "JSON (parallel/costmodel.py default_calibration, $ROUNDTABLE_CALIBRATION)")
     return p.parse_args()
 
 
@@ -370,6 +373,13 @@ def main() -> int:
     }
     if cl.rank == 0 and not sim and args.scaling == "strong" and T > 1 and n_tables == 1:
         out["detail"]["prediction"] = _predict(args, T, engine)
+    if cl.rank == 0 and args.write_calibration and getattr(engine.tp, "oneshot", None) is not None:
+        os_ = engine.tp.oneshot
+        cal = {"ar_us": os_.latency_us,
+               "fused_ar_saving_us": os_.fused_saving_us if os_.fused and os_.fused_saving_us else 0.0,
+               "source": f"bench.py tp{T} on {N} GPU(s), K9 probe at engine creation", "measured_unix": time.time()}
+        with open(args.write_calibration, "w") as f:
+            json.dump(cal, f, indent=1)
     if args.c1_events:
         with open(f"{args.c1_events}.r{cl.rank}.json", "w") as f:
             json.dump({"rank": cl.rank, "events": pool.events, "ns": pool.event_ns}, f)

@@ -102,3 +102,23 @@ def test_init_manual_tp_overrides_placement(project, monkeypatch):
     assert [cfg["adapter_config"][a]["engine"]["gpus"] for a in ("claude-cli", "gemini-cli", "openai-cli")] == \
         [[0, 1], [2, 3], [4, 5]]
     assert "placement" not in cfg["engine"]
+
+
+def test_measured_calibration_changes_the_plan(tmp_path, monkeypatch):
+    """$ROUNDTABLE_CALIBRATION (bench.py --write-calibration after an N-GPU run) replaces the
+    assumed K9 latency: a slow measured xGMI all-reduce makes the planner give the lone 8B
+    table fewer GPUs than the default, a fused form that saves most of it gives it more."""
+    from theroundtaible_amd.parallel import costmodel
+    knights = [{"name": n, "model": "llama3-8b"} for n in "ABC"]
+    default_tp = plan_placement(knights, node())[0].tp
+    path = tmp_path / "cal.json"
+    path.write_text(json.dumps({"ar_us": 60.0, "fused_ar_saving_us": 0.0, "source": "test"}))
+    monkeypatch.setenv(costmodel.CALIBRATION_ENV, str(path))
+    assert costmodel.default_calibration().ar_us == 60.0
+    slow_tp = plan_placement(knights, node())[0].tp
+    assert slow_tp < default_tp
+    path.write_text(json.dumps({"ar_us": 60.0, "fused_ar_saving_us": 58.0}))
+    import os
+    os.utime(path, (os.path.getatime(path), os.path.getmtime(path) + 5))   # new content, new mtime
+    assert costmodel.default_calibration().fused_ar_saving_us == 58.0
+    assert plan_placement(knights, node())[0].tp >= default_tp

@@ -55,6 +55,35 @@ class Calibration:
     prefill_ar_gbps: float = 120.0  # RCCL ring all-reduce bus bandwidth per link (estimate)
 
 
+CALIBRATION_ENV = "ROUNDTABLE_CALIBRATION"
+_CAL_CACHE: Dict[str, tuple] = {}
+
+
+def default_calibration() -> Calibration:
+    """The calibration the model uses when none is passed: the built-in constants, overridden
+    field by field by the JSON file ``$ROUNDTABLE_CALIBRATION`` names — e.g. the one
+    ``bench.py --write-calibration`` writes after an N-GPU run, which carries the node's own
+    measured K9 latency and fused-form saving (the xGMI numbers a 1-GPU box cannot measure), so
+    ``init --placement auto`` plans with measured, not assumed, collective costs."""
+    import json
+    import os
+    path = os.environ.get(CALIBRATION_ENV, "")
+    if not path or not os.path.exists(path):
+        return Calibration()
+    mt = os.path.getmtime(path)
+    hit = _CAL_CACHE.get(path)
+    if hit is not None and hit[0] == mt:
+        return hit[1]
+    with open(path) as f:
+        data = json.load(f)
+    cal = Calibration()
+    for k, v in data.items():
+        if k in cal.__dataclass_fields__ and isinstance(v, (int, float)) and not isinstance(v, bool):
+            setattr(cal, k, float(v))
+    _CAL_CACHE[path] = (mt, cal)
+    return cal
+
+
 def _attn_kv_bytes(cfg: ModelConfig, tp: int, ctx_shared: int, ctx_private: int, B: int) -> float:
     kv_heads = max(1, cfg.n_kv_heads // tp)
     per_tok = kv_heads * cfg.head_dim * 2 * 2          # K and V, bf16, one layer
@@ -64,7 +93,7 @@ def _attn_kv_bytes(cfg: ModelConfig, tp: int, ctx_shared: int, ctx_private: int,
 def decode_step_us(cfg: ModelConfig, tp: int, B: int, ctx_shared: int, ctx_private: int = 0,
                    cal: Optional[Calibration] = None) -> Tuple[float, Dict[str, float]]:
     """Predicted µs of one decode step (one token for each of the B knights) per rank."""
-    cal = cal or Calibration()
+    cal = cal or default_calibration()
     H, D = cfg.hidden, cfg.head_dim
     hq, hkv, F = cfg.n_heads // tp, max(1, cfg.n_kv_heads // tp), cfg.ffn // tp
     bw = cal.hbm_tbps * 1e6          # bytes per µs
@@ -82,7 +111,7 @@ def decode_step_us(cfg: ModelConfig, tp: int, B: int, ctx_shared: int, ctx_priva
 
 def prefill_ms(cfg: ModelConfig, tp: int, tokens: int, ctx: int, cal: Optional[Calibration] = None) -> float:
     """Chunked prefill of ``tokens`` new tokens after ``ctx`` resident ones, per rank."""
-    cal = cal or Calibration()
+    cal = cal or default_calibration()
     if tokens <= 0:
         return 0.0
     n = cfg.n_params() - cfg.vocab * cfg.hidden        # the embedding is a gather
@@ -186,7 +215,7 @@ def strong_round_ms(sim: dict, n: int, k9_us: float, gather_us: float, fused_sav
     """Predicted ms per round of the strong-scaling bench on n GPUs: the simulated rank-0 compute
     of that tp (collectives elided) + per decode step 2L effective all-reduces (K9 latency minus
     the fused form's saving) and one logits gather + the prefill ring all-reduces."""
-    cal = cal or Calibration()
+    cal = cal or default_calibration()
     cfg = get_config(sim["config"]["model"].split(" ")[0])
     steps = sim["config"]["new_tokens_per_turn"]
     comp = sim["ms_per_round"]
