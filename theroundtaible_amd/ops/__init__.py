@@ -133,7 +133,10 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: i
     # grouped (shared-prefix) decode: a workgroup streams 1/n of the group's shared keys, so the
     # launch is shorter and its fixed latency chain weighs more — 3/4 of the CUs measured best
     # (B=3, shared 22K/40K: 8 splits 30.8/42.7 us vs 10 splits 31.7/43.8, r2_gattn_v1.log)
-    cus = num_cus * 3 // 4 if grouped else num_cus
+    # A lone sequence (B = 1: sequential rounds) shares nothing, so it takes the whole chip: B = 1,
+    # Llama-3-8B, 10K / 25K / 40K keys: 24 splits 15.9 / 26.3 / 36.8 us, 32 splits 15.0 / 25.9 /
+    # 35.7 (profiles/r03/attn_b1_splits.md)
+    cus = num_cus * 3 // 4 if grouped and batch > 1 else num_cus
     want = cus // max(1, batch * n_kv_heads)        # never more workgroups than CUs: a second
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
