@@ -155,9 +155,21 @@ class DecodeGraph:
         self._reset_dummy()
         with torch.no_grad():
             self._prep()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g), torch.no_grad():
-            self._body()
+        # Python's cyclic GC must not run inside the capture: collecting an unreachable engine or
+        # graph there frees device memory / destroys a hipGraph while the stream is capturing,
+        # which aborts the process (seen when a test's earlier engine was collected mid-capture).
+        # Collect now, outside, and keep the collector off until the capture has ended.
+        import gc
+        gc.collect()
+        was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g), torch.no_grad():
+                self._body()
+        finally:
+            if was_enabled:
+                gc.enable()
         self.graph = g
         self._reset_dummy()
 
