@@ -54,8 +54,10 @@ def parse():
     p.add_argument("--steps", type=int, default=3, help="timed rounds")
     p.add_argument("--warmup", type=int, default=1, help="untimed rounds (round 1 includes the initial prefill)")
     p.add_argument("--model", default="llama3-8b")
-    p.add_argument("--knights-per-gpu", type=int, default=3,
-                   help="knights hosted per GPU (per TP group when --tp > 1)")
+    p.add_argument("--knights-per-gpu", type=int, default=None,
+                   help="knights hosted per GPU group (a TP group when --tp > 1); default: the whole table "
+                        "(strong) / 3 (weak). BASELINE config 5 = --tp 4 --knights-per-table 2 --knights-per-gpu 1 "
+                        "on 8 GPUs: two disjoint TP=4 groups, one knight each")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong (default): one 3-knight table, one engine tensor-parallel over all N GPUs; "
                         "weak: N tables, one GPU group each")
@@ -97,6 +99,11 @@ def parse():
                         "ends in a forced consensus JSON scoring 6, then 9 in this round, so the tables reach "
                         "consensus and stop there (0 = off; use warmup + steps to end inside the timed region)")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    p.add_argument("--stage-timeout", type=float, default=240.0,
+                   help="seconds any stage (a round, a capture) may take on any rank, and the process-group "
+                        "collective timeout; past it rank 0 prints the failure line and every rank exits")
+    p.add_argument("--init-timeout", type=float, default=900.0,
+                   help="the same for start-up (rendezvous, weights, K9 creation: a fresh box pages torch in)")
     p.add_argument("--write-calibration", default=None,
                    help="(N > 1) write the node's measured K9 latency / fused saving as a cost-model calibration "
                         "JSON (parallel/costmodel.py default_calibration, $ROUNDTABLE_CALIBRATION)")
@@ -156,10 +163,42 @@ def _predict(args, T: int, engine) -> dict:
             "predicted_ms_per_round": round(strong_round_ms(simr, T, k9, gather, saving), 1)}
 
 
+def _failure_line(args, world: int, rec: dict) -> dict:
+    """Rank 0's one JSON line for a run that could not finish (utils/failsafe.py): the stage and
+    rank that failed instead of a measurement."""
+    return {"metric": f"aggregate knight tokens/sec ({args.knights_per_table}-knight discuss, {args.round_mode} rounds)",
+            "value": None, "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": None, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+            "dtype": "bf16" if args.device != "cpu" else "fp32", "data": "synthetic prompts, random-init weights",
+            "config": {"model": args.model, "knights_per_table": args.knights_per_table, "round_mode": args.round_mode,
+                       "prompt_layout": args.layout, "tp": args.tp or None},
+            "error": rec.get("error"), "failed_stage": rec.get("failed_stage"), "failed_rank": rec.get("failed_rank"),
+            "failures": rec.get("failures", [])}
+
+
 def main() -> int:
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _self_launch(args)
+    from theroundtaible_amd.utils import failsafe
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    # every stage of this rank runs under a time limit, and any rank's failure ends the whole run
+    # with ONE JSON line from rank 0 naming the stage (VERDICT r3 #4): a wedged collective never
+    # eats the driver's window in silence
+    guard = failsafe.RunGuard(rank, world, lambda rec: print(json.dumps(_failure_line(args, world, rec)), flush=True),
+                              default_s=args.stage_timeout,
+                              limits={"start": args.init_timeout, "init": args.init_timeout,
+                                      "engine_load": args.init_timeout, "k9_create": args.init_timeout}).start()
+    try:
+        rc = _run(args, failsafe)
+    except BaseException as e:  # noqa: BLE001 - every failure becomes the run's JSON line
+        guard.fail(failsafe.current_stage(), f"{type(e).__name__}: {e}")
+        return 3
+    guard.finish()
+    return rc
+
+
+def _run(args, failsafe) -> int:
     from theroundtaible_amd.utils.debug import apply_debug_env
     if apply_debug_env():
         print("bench: ROUNDTABLE_DEBUG=1 — kernels serialized, numbers are NOT performance data", file=sys.stderr)
@@ -172,7 +211,10 @@ def main() -> int:
     from theroundtaible_amd.parallel.cluster import init_cluster
     from theroundtaible_amd.types import RoundtableConfig
 
-    cl = init_cluster(prefer_gpu=args.device != "cpu")
+    failsafe.set_stage("init")
+    # collectives time out a little after the stage guard fires (utils/failsafe.py), so a stall is
+    # reported by the guard's JSON line rather than by a process-group abort; <= 300 s by default
+    cl = init_cluster(prefer_gpu=args.device != "cpu", timeout_s=int(args.stage_timeout) + 30)
     N = cl.world
     if N != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but {N} rank(s) joined (WORLD_SIZE); refusing to "
@@ -183,9 +225,9 @@ def main() -> int:
     if sim and N != 1:
         raise SystemExit("--simulate-tp runs ONE process (it models one rank of a tp group)")
     T = args.tp if args.tp > 0 else (N if args.scaling == "strong" else 1)
-    if args.scaling == "strong":
-        # one table on one TP group: every GPU of the group hosts all of the table's knights
-        args.knights_per_gpu = kpt
+    if args.knights_per_gpu is None:
+        # strong: one table on one TP group, every GPU of the group hosts all of the table's knights
+        args.knights_per_gpu = kpt if args.scaling == "strong" else 3
     if N % T:
         raise SystemExit(f"--tp {T} must divide the {N} launched GPUs")
     from theroundtaible_amd.models.config import get_config
@@ -211,6 +253,7 @@ def main() -> int:
         tables.append(knights)
     local_names = [n for n, ranks in placement.items() if cl.rank in ranks]
 
+    failsafe.set_stage("tp_groups")
     tp = None
     if sim > 1:
         from theroundtaible_amd.parallel.tp import SimulatedTP
@@ -221,6 +264,7 @@ def main() -> int:
         pgs = [dist.new_group(r) for r in group_ranks]   # collective: same order on every rank
         g = cl.rank // T
         tp = TPInfo(size=T, rank=cl.rank % T, group=pgs[g])
+    failsafe.set_stage("engine_load")
     t_load = time.perf_counter()
     engine = Engine(EngineConfig(model=args.model, weights=args.weights, device=device,
                                  use_graphs=not args.no_graphs and device != "cpu",
@@ -241,6 +285,7 @@ def main() -> int:
     pool = DistributedPool(cl, placement, local, engine.tokenizer, max_reply_tokens=args.new_tokens + 512)
     load_s = time.perf_counter() - t_load
 
+    failsafe.set_stage("setup")
     rounds = args.warmup + args.steps
     workdir = tempfile.mkdtemp(prefix=f"rt-bench-r{cl.rank}-")
     orchs = []
@@ -263,6 +308,7 @@ def main() -> int:
     timing = {}
 
     def on_round(rnd: int, ms: float):
+        failsafe.set_stage(f"round {rnd + 1}" if rnd < rounds else "report")
         if rnd == args.warmup:
             if device.startswith("cuda"):
                 torch.cuda.synchronize()
@@ -278,6 +324,7 @@ def main() -> int:
         cl.barrier()
         timing["t0"] = time.perf_counter()
     runner = run_tables_parallel if args.round_mode == "parallel" else run_tables_sequential
+    failsafe.set_stage("round 1")
     runner(orchs, [f"{TOPIC} (tafel {t})" for t in range(n_tables)], on_round=on_round)
     elapsed = cl.max_scalar(timing["t1"] - timing["t0"])
     last = min(rounds, args.consensus_round) if args.consensus_round else rounds
@@ -315,7 +362,7 @@ def main() -> int:
     ms_round = elapsed / n_timed * 1e3
     value = dec / elapsed if elapsed > 0 else 0.0
     ref_bound_ms = kpt * 120_000.0
-    if args.scaling == "strong" and n_tables == 1:
+    if n_tables == 1:
         metric = f"aggregate knight tokens/sec (one {kpt}-knight discuss, {args.round_mode} rounds)"
     else:
         metric = f"aggregate knight tokens/sec ({kpt}-knight discuss tables, {args.round_mode} rounds)"
@@ -371,6 +418,17 @@ def main() -> int:
                    "engine_decode_ms_per_round": round(sum(dec_ms.values()) / n_timed, 2),
                    "host_ms_per_round": round(ms_round - sum(eng_ms.values()) / n_timed, 2)},
     }
+    # per-rank facts every rank contributes (one gloo gather): who took part in C1, and whether
+    # each rank's decode ran as captured graphs
+    per_rank = cl.all_gather_object({"c1_contributions": getattr(pool, "c1_contributions", 0),
+                                     "graph_replays": engine.stats.get("graph_replays", 0),
+                                     "capture_fallbacks": engine.stats.get("capture_fallbacks", 0),
+                                     "use_graphs": bool(engine.ecfg.use_graphs)})
+    out["detail"]["c1_contributions_per_rank"] = [r["c1_contributions"] for r in per_rank]
+    out["detail"]["graph_replays_per_rank"] = [r["graph_replays"] for r in per_rank]
+    out["detail"]["capture_fallbacks"] = sum(r["capture_fallbacks"] for r in per_rank)
+    out["detail"]["graphs_per_rank"] = [r["use_graphs"] for r in per_rank]
+    out["detail"]["c1_disagreements"] = getattr(pool, "c1_disagreements", 0)
     if cl.rank == 0 and not sim and args.scaling == "strong" and T > 1 and n_tables == 1:
         out["detail"]["prediction"] = _predict(args, T, engine)
     if cl.rank == 0 and args.write_calibration and getattr(engine.tp, "oneshot", None) is not None:

@@ -32,6 +32,22 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(GemmArgs p) {
   gemm_tile<PRO, EPI, NW, U, false>(p, blockIdx.x, sm, st0, false, blockIdx.x == 0);
 }
 
+// the dynamic LDS of an ALDS launch: [16] row sums of squares, then the staged rows
+RT_DEVICE ALds alds_view(int kspan) {
+  extern __shared__ float alds_dyn[];
+  return ALds{reinterpret_cast<uint16_t*>(alds_dyn + 16), alds_dyn, kspan + 8};
+}
+
+// The same launch with the A operand staged in LDS (skinny_core.h ALDS): tensor-parallel shard
+// shapes, where the per-k-step activation loads, not HBM, bound the launch.
+template <int PRO, int EPI, int NW, int U>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_alds_kernel(GemmArgs p) {
+  __shared__ GemmSmem<nacc<EPI>(), NW> sm;
+  Stage<PRO, EPI, U> st0;
+  const ALds al = alds_view(p.K);
+  gemm_tile<PRO, EPI, NW, U, false, true>(p, blockIdx.x, sm, st0, false, blockIdx.x == 0, nullptr, &al);
+}
+
 // CU-balanced launch for tile counts that are not a multiple of the CU count (gate_up of
 // Llama-3-8B / Mistral-7B: 896 tiles on 256 CUs = 3.5 per CU, so half the CUs stream a 4th
 // tile while the rest idle): the last R = T mod CUs tiles run as two K-halves each (SplitX in
@@ -72,7 +88,7 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_bal_kernel(GemmArgs p, in
 // Placement (speed only, never correctness): with T % 8 == 0 the S parts of a tile get block ids
 // b, b + 8, ... — one XCD under round-robin dispatch, so the combine reads same-XCD partials.
 // NORM_ADD: every part of tile 0 publishes its K range of x + x2.
-template <int PRO, int EPI, int NW, int U>
+template <int PRO, int EPI, int NW, int U, bool ALDS = false>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_splitk_kernel(GemmArgs p, int* __restrict__ ws, int S) {
   __shared__ GemmSmem<nacc<EPI>(), NW> sm;
   Stage<PRO, EPI, U> st0;
@@ -88,7 +104,13 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_splitk_kernel(GemmArgs p,
     part = b % S;
   }
   const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)tile * S * SPLIT_STRIDE, ws + tile, part, S};
-  gemm_tile<PRO, EPI, NW, U, false>(p, tile, sm, st0, false, tile == 0, &sx);
+  if constexpr (ALDS) {
+    const int ks = p.K / 32;
+    const ALds al = alds_view(32 * ((ks + S - 1) / S + 1));
+    gemm_tile<PRO, EPI, NW, U, false, true>(p, tile, sm, st0, false, tile == 0, &sx, &al);
+  } else {
+    gemm_tile<PRO, EPI, NW, U, false>(p, tile, sm, st0, false, tile == 0, &sx);
+  }
 }
 
 int device_cus() {
@@ -193,6 +215,20 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// ALDS decision (skinny_core.h): RT_GEMM_ALDS=0 never, =1 whenever the staged rows fit, default:
+// when they fit and the launch has at most one workgroup per CU (tensor-parallel shard shapes;
+// with several workgroups per CU the activation loads hide under HBM and the staging LDS would
+// cost occupancy). Staged rows + row sums <= 48 KB, so the workgroup stays under 64 KB of LDS.
+constexpr int ALDS_MAX_BYTES = 48 * 1024;
+bool use_alds(int M, int kspan, int wgs, int cus) {
+  static const int mode = [] {
+    const char* e = getenv("RT_GEMM_ALDS");
+    return e ? atoi(e) : -1;
+  }();
+  if (mode == 0 || skinny::alds_bytes(M, kspan) > ALDS_MAX_BYTES) return false;
+  return mode == 1 || (cus > 0 && wgs <= cus);
+}
+
 int split_workspace_ints(int max_split_tiles) { return SPLIT_CTRS + max_split_tiles * 2 * SPLIT_STRIDE; }
 
 // Split-K part count for a T-tile, ks-k-step GEMM on `cus` CUs (0 = no split-K): the most parts
@@ -248,6 +284,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
                     eps, re, (const uint16_t*)x2, (uint16_t*)xo};
       args.kmajor = forced_order();
       const dim3 grid(T * S);
+      const int kspan = 32 * ((K / 32 + S - 1) / S + 1);
+      const bool alds = use_alds(M, kspan, T * S, device_cus());
+      const size_t lds = alds ? (size_t)skinny::alds_bytes(M, kspan) : 0;
       // (NW, U) of the split-K parts: 8 waves x 2 steps — one part per CU streams with twice
       // the bytes in flight of 4 waves (r03 microbench, Llama-3-8B tp 4 qkv 8.79 -> 7.98 us; tp 2/8
       // shards within noise; 4x4 no better: profiles/r03/gemm_tp_splitk_cfg_sweep.md).
@@ -264,6 +303,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
       hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 4, 2>), grid, dim3(256), 0, stream, args, split_ws, S);  \
     else if (skcfg == 404)                                                                                          \
       hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 4, 4>), grid, dim3(256), 0, stream, args, split_ws, S);  \
+    else if (alds)                                                                                                  \
+      hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 8, 2, true>), grid, dim3(512), lds, stream, args, split_ws, \
+                         S);                                                                                        \
     else                                                                                                            \
       hipLaunchKernelGGL((skinny_gemm_splitk_kernel<P, E, 8, 2>), grid, dim3(512), 0, stream, args, split_ws, S);  \
   } while (0)
@@ -340,6 +382,8 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   }();
   const int cfg = cfg_env ? cfg_env : ((N / 16) >= 384 ? 402 : 404);
   dim3 grid(N / 16);
+  const bool alds = !cfg_env && use_alds(M, K, N / 16, device_cus());
+  const size_t lds = alds ? (size_t)skinny::alds_bytes(M, K) : 0;
 #define RT_SG(P, E)                                                                                          \
   do {                                                                                                       \
     switch (cfg) {                                                                                           \
@@ -354,8 +398,13 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
                 eps, re, (const uint16_t*)x2, (uint16_t*)xo};
   args.kmajor = forced_order();
-#define RT_SGV(P, E, NWV, UV) \
-  hipLaunchKernelGGL((skinny_gemm_kernel<P, E, NWV, UV>), grid, dim3(NWV * 64), 0, stream, args)
+#define RT_SGV(P, E, NWV, UV)                                                                                  \
+  do {                                                                                                         \
+    if (alds)                                                                                                  \
+      hipLaunchKernelGGL((skinny_gemm_alds_kernel<P, E, NWV, UV>), grid, dim3(NWV * 64), lds, stream, args);   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((skinny_gemm_kernel<P, E, NWV, UV>), grid, dim3(NWV * 64), 0, stream, args);          \
+  } while (0)
   if (pro == PRO_PLAIN && epi == EPI_STORE) RT_SG(PRO_PLAIN, EPI_STORE);
   else if (pro == PRO_NORM && epi == EPI_STORE) RT_SG(PRO_NORM, EPI_STORE);
   else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_SG(PRO_PLAIN, EPI_RESID);

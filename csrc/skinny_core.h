@@ -262,6 +262,90 @@ RT_DEVICE void consume(const Stage<PRO, EPI, U>& st, float4_& acc, float4_& acc2
   }
 }
 
+// ---- A operand staged in LDS (ALDS) -------------------------------------------------------
+// With the activation fragments loaded from global memory, every k-step of every wave issues one
+// 16-B/lane activation load (two for NORM_ADD) beside its weight load: 2-3x the vector-memory
+// instructions of the weight stream, through the CU's one texture path. At tensor-parallel shard
+// shapes (few KB to ~100 KB of weights per workgroup) that — not HBM — bounds the launch
+// (tools/probes/stream_probe.hip: a pure 16-B/lane stream of 192 x 128 KB takes 6.5 us, the
+// tp2 qkv GEMM of the same bytes 9.6 us). ALDS stages rows [0, M) of the workgroup's K range
+// ONCE (NORM_ADD: the bf16 sum x + x2, published to `xo` by the publishing workgroup; NORM /
+// NORM_ADD: each row's sum of squares, from the same values), then every k-step reads its A
+// fragment with one ds_read_b128 — the global loads of the k-loop are the weights alone.
+struct ALds {
+  uint16_t* a;     // [M][astride] bf16
+  float* ssq;      // [16] sum of squares of each staged row (NORM / NORM_ADD)
+  int astride;     // elements per staged row: K range + 8 (rows 4 banks apart)
+};
+constexpr int ALDS_BATCH = 8;   // 16-B loads per lane in flight while staging one row
+
+// Rows are spread over the waves (row m on wave m % NW); within a row the 64 lanes take 16-B
+// units, ALDS_BATCH per lane per round trip (clamped re-reads at the tail are L2 hits, never
+// stored twice).
+template <int PRO, int NW>
+RT_DEVICE void stage_a(const GemmArgs& p, int s_lo, int nsteps, const ALds& L, uint16_t* __restrict__ xo) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int K = p.K, kb = s_lo * 32, n8 = (nsteps - s_lo) * 4;
+  for (int m = wid; m < p.M; m += NW) {
+    const uint16_t* xr = p.x + (size_t)m * K + kb;
+    const uint16_t* x2r = PRO == PRO_NORM_ADD ? p.x2 + (size_t)m * K + kb : xr;
+    uint16_t* dst = L.a + (size_t)m * L.astride;
+    float ss = 0.f;
+    for (int u0 = 0; u0 < n8; u0 += 64 * ALDS_BATCH) {
+      short8 a[ALDS_BATCH], b[ALDS_BATCH];
+#pragma unroll
+      for (int j = 0; j < ALDS_BATCH; ++j) {
+        const int u = min(u0 + 64 * j + lane, n8 - 1);
+        a[j] = *reinterpret_cast<const short8*>(xr + 8 * u);
+        if constexpr (PRO == PRO_NORM_ADD) b[j] = *reinterpret_cast<const short8*>(x2r + 8 * u);
+      }
+#pragma unroll
+      for (int j = 0; j < ALDS_BATCH; ++j) {
+        const int u = u0 + 64 * j + lane;
+        short8 av = a[j];
+        if constexpr (PRO == PRO_NORM_ADD) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            av[e] = (short)rt::f2bf(rt::bf2f((uint16_t)a[j][e]) + rt::bf2f((uint16_t)b[j][e]));
+        }
+        if (u < n8) {
+          *reinterpret_cast<short8*>(dst + 8 * u) = av;
+          if (PRO == PRO_NORM_ADD && xo != nullptr) *reinterpret_cast<short8*>(xo + (size_t)m * K + kb + 8 * u) = av;
+          if constexpr (PRO != PRO_PLAIN) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float f = rt::bf2f((uint16_t)av[e]);
+              ss = fmaf(f, f, ss);
+            }
+          }
+        }
+      }
+    }
+    if constexpr (PRO != PRO_PLAIN) {
+      ss = rt::wave_sum(ss);
+      if (lane == 0) L.ssq[m] = ss;
+    }
+  }
+}
+
+template <int PRO, int EPI, int NW, int U>
+RT_DEVICE void consume_lds(const Stage<PRO, EPI, U>& st, float4_& acc, float4_& acc2, int s0, int nsteps,
+                           const uint16_t* __restrict__ arow) {
+  // arow = this lane's staged row + 8g - 32 s_lo: the A fragment of k-step s is arow[32 s .. +8)
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (s0 + NW * u < nsteps) {
+      const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const short8*>(arow + (s0 + NW * u) * 32));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u]), acc, 0, 0, 0);
+      if constexpr (EPI == EPI_SWIGLU)
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u]), acc2, 0, 0, 0);
+    }
+  }
+}
+
+// dynamic LDS bytes of the ALDS staging for M rows of a K range of `kspan` elements
+__host__ __device__ inline int alds_bytes(int M, int kspan) { return 64 + M * (kspan + 8) * 2; }
+
 // Stage-0 weight prefetch of `tile` for the calling wave (no activation loads): lets a
 // persistent kernel put a tile's first weight bytes in flight before its inputs are ready.
 template <int PRO, int EPI, int NW, int U>
@@ -344,10 +428,11 @@ RT_DEVICE void ar_exchange(const GemmArgs& p, int tile, float v, int m, int n, b
 
 // One 16-column tile. `st0` may hold this tile's prefetched stage-0 weights (prefetched=true).
 // `publish_xo`: this workgroup writes the NORM_ADD sum to p.xo.
-template <int PRO, int EPI, int NW, int U, bool SC1>
+template <int PRO, int EPI, int NW, int U, bool SC1, bool ALDS = false>
 RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>& sm, Stage<PRO, EPI, U>& st0,
                          bool prefetched,
-                         bool publish_xo, const SplitX* sx = nullptr) {
+                         bool publish_xo, const SplitX* sx = nullptr, const ALds* al = nullptr) {
+  static_assert(!(ALDS && SC1), "the LDS-staged A operand is for standalone launches");
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int M = p.M, N = p.N, K = p.K;
@@ -377,7 +462,16 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   const int w0 = s_lo + wid;   // this wave's first k-step
   const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
   if (!prefetched) issue_w<PRO, EPI, NW, U>(st0, wt, wt2, w0, nsteps, lane, sstride);
-  issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, w0, nsteps);
+  const uint16_t* arow = nullptr;
+  if constexpr (ALDS) {
+    // stage-0 weights are in flight; stage A once (its loads overlap theirs), then the k-loop
+    stage_a<PRO, NW>(p, s_lo, nsteps, *al,
+                     (PRO == PRO_NORM_ADD && publish_xo && p.xo != nullptr) ? p.xo : nullptr);
+    __syncthreads();
+    arow = al->a + (size_t)(row_ok ? r : 0) * al->astride + 8 * g - 32 * s_lo;
+  } else {
+    issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, w0, nsteps);
+  }
   // Epilogue operands that do not depend on the GEMM are loaded NOW, so their round trips hide
   // under the k-loop instead of following the last MFMA: the residual element (RESID) and the
   // K/V slot, position and cos/sin pair (ROPE). Unconditional, rows clamped (no branch for the
@@ -395,16 +489,27 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
     e_s = cs[(re.D >> 1) + (pp >> 1)];
   }
   int j = 0;
-  for (; j + 1 < nst; j += 2) {
-    const int s = w0 + SPAN * j;
-    issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane, sstride);
-    issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
-    consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
-    issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane, sstride);
-    issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
-    consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
+  if constexpr (ALDS) {
+    for (; j + 1 < nst; j += 2) {
+      const int s = w0 + SPAN * j;
+      issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane, sstride);
+      consume_lds<PRO, EPI, NW, U>(st0, acc, acc2, s, nsteps, arow);
+      issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane, sstride);
+      consume_lds<PRO, EPI, NW, U>(st1, acc, acc2, s + SPAN, nsteps, arow);
+    }
+    if (j < nst) consume_lds<PRO, EPI, NW, U>(st0, acc, acc2, w0 + SPAN * j, nsteps, arow);
+  } else {
+    for (; j + 1 < nst; j += 2) {
+      const int s = w0 + SPAN * j;
+      issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane, sstride);
+      issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
+      consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
+      issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane, sstride);
+      issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
+      consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
+    }
+    if (j < nst) consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps, xo_r, xo_s);
   }
-  if (j < nst) consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps, xo_r, xo_s);
 
   // C layout: acc[i] = C[m = 4g + i][n = r]
 #pragma unroll
@@ -412,7 +517,7 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
     sm.red[wid][0][4 * g + i][r] = acc[i];
     if constexpr (EPI == EPI_SWIGLU) sm.red[wid][(EPI == EPI_SWIGLU) ? 1 : 0][4 * g + i][r] = acc2[i];
   }
-  if constexpr (PRO != PRO_PLAIN) {
+  if constexpr (PRO != PRO_PLAIN && !ALDS) {
     ssq += __shfl_xor(ssq, 16, 64);
     ssq += __shfl_xor(ssq, 32, 64);
     if (g == 0) sm.sq[wid][r] = ssq;
@@ -425,9 +530,10 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       v += sm.red[w][0][m][n];
-      if constexpr (PRO != PRO_PLAIN) ss += sm.sq[w][m];
+      if constexpr (PRO != PRO_PLAIN && !ALDS) ss += sm.sq[w][m];
       if constexpr (EPI == EPI_SWIGLU) up += sm.red[w][(EPI == EPI_SWIGLU) ? 1 : 0][m][n];
     }
+    if constexpr (PRO != PRO_PLAIN && ALDS) ss = al->ssq[m];
   }
   if (sx != nullptr) {   // split tile: hand this part's sums over, the last arrival finishes
     // hand-off (MI355X_MICROARCH, sc1 table row 1): 4-B sc1 payload stores -> every wave's

@@ -36,7 +36,7 @@ from ..models.llama import AttnMeta
 from ..models.weights import materialize
 from ..parallel.tp import TPInfo
 from ..prompt import Prompt, PromptLike, Segment
-from ..utils import trace
+from ..utils import failsafe, trace
 from .kv_cache import KVCacheOOM, PagedKVCache, SeqState
 from .sampler import SamplingParams
 from .tokenizer import EngineTokenizer, get_tokenizer
@@ -106,8 +106,8 @@ class Engine:
         self.cfg: ModelConfig = get_config(ecfg.model, **ecfg.model_overrides)
         self.device = torch.device(ecfg.device)
         self.on_gpu = self.device.type == "cuda"
-        if self.on_gpu and self.tp.size > 1 and self.tp.backend() != "nccl":
-            ecfg.use_graphs = False      # host-staged (gloo) collectives cannot be captured in a hipGraph
+        # host-staged (gloo) collectives cannot be captured in a hipGraph: graphs stay on for such a
+        # group only if every in-step collective is a device-side K9 kernel (decided after K9 set-up)
         self.dtype = _dtype(ecfg.dtype)
         if not self.on_gpu and self.dtype == torch.float16:
             self.dtype = torch.float32
@@ -131,7 +131,13 @@ class Engine:
                 self.model.decode_weights(drop_originals=(mode == "shuffled"))
                 self.weight_residency = mode
         if self.on_gpu and self.tp.size > 1:
-            self.tp.setup_oneshot()      # K9: collective over the TP group; RCCL stays the fallback
+            with failsafe.stage("k9_create"):
+                self.tp.setup_oneshot()      # K9: collective over the TP group; RCCL stays the fallback
+            # a decode step whose every collective is a K9 kernel (all-reduce, and the one-shot
+            # logits gather) can be captured even when the group's host collectives are gloo (the
+            # shared-GPU rehearsal): agree on it, so every rank captures or none does
+            if ecfg.use_graphs and self.tp.backend() != "nccl":
+                ecfg.use_graphs = not self.tp.any_rank(not self.k9_only_step())
         if not hasattr(self, "weight_residency"):
             self.weight_residency = "dual"
         self.load_s = time.perf_counter() - t0
@@ -172,6 +178,12 @@ class Engine:
                 nb = 256   # CPU plumbing runs: 8K resident tokens per engine
         if self.ecfg.max_kv_tokens:
             nb = min(nb, (self.ecfg.max_kv_tokens + bs - 1) // bs + self.ecfg.max_batch)
+        if self.tp.size > 1:
+            # every rank of a tensor-parallel knight must hold the SAME pool: the block allocator
+            # then makes identical decisions on every rank, so a KVCacheOOM is raised on all of
+            # them or none (a pool sized from one rank's free memory, e.g. a second rehearsal rank
+            # on a shared GPU, could run out alone and skip collectives its peers enter)
+            nb = self.tp.group_min(int(nb))
         return PagedKVCache(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, int(nb), bs,
                             self.device, self.dtype)
 
@@ -778,9 +790,8 @@ class Engine:
                       t.timeout_s) for t in turns]
         eos = self.tokenizer.stop_ids
         t0 = time.perf_counter()
-        runner = self._graph_for(len(seqs), max(sq.length for sq in seqs) + steps + 1, grouped=groups is not None,
-                                 dist_greedy=self.dist_greedy(chunk)) \
-            if self.on_gpu and self.ecfg.use_graphs else None
+        runner = self._agreed_graph(len(seqs), max(sq.length for sq in seqs) + steps + 1, groups is not None,
+                                    self.dist_greedy(chunk))
         with trace.range(f"decode chunk B={len(seqs)} steps={steps}"):
             if runner is not None:
                 toks = runner.run(self, seqs, chunk, first, steps + 1, time.perf_counter() + 1e9, eos, groups)
@@ -817,17 +828,7 @@ class Engine:
         for s, n in zip(seqs, max_new):
             self.kv.ensure_capacity(s, s.length + steps)
         eos = self.tokenizer.stop_ids
-        runner = None
-        if self.on_gpu and self.ecfg.use_graphs:
-            try:
-                runner = self._graph_for(B, max(s.length for s in seqs) + steps, grouped=groups is not None,
-                                         dist_greedy=self.dist_greedy(turns))
-            except RuntimeError as e:   # e.g. a collective that refuses stream capture: stay eager
-                if self.tp.size == 1:
-                    raise
-                import warnings
-                warnings.warn(f"hipGraph capture failed under tp={self.tp.size} ({e}); decoding eagerly")
-                self.ecfg.use_graphs = False
+        runner = self._agreed_graph(B, max(s.length for s in seqs) + steps, groups is not None, self.dist_greedy(turns))
         with trace.range(f"decode B={B} steps={steps}"):
             if runner is not None:
                 toks = runner.run(self, seqs, turns, first, steps, deadline, eos, groups)
@@ -851,6 +852,13 @@ class Engine:
             # resident = prompt + kept tokens except the last (its K/V was never computed)
             s.tokens.extend(g)
             self.kv.truncate(s, s.length - 1 if g else s.length)
+        if self.on_gpu:
+            # the device ids are produced on this engine's stream; consumers on other streams (the
+            # C1 exchange) wait on this event before reading them (parallel/exchange.py)
+            ev = torch.cuda.Event()
+            ev.record(self.stream or torch.cuda.current_stream(self.device))
+            for d in self._dev_gen:
+                d.ready_event = ev
         return gen, steps
 
     def group_table(self, groups, B: int) -> Optional[torch.Tensor]:
@@ -918,8 +926,46 @@ class Engine:
             self.kv.truncate(s, s.length)
 
     def dist_greedy(self, turns: Sequence[Turn]) -> bool:
-        """TP knight decoding greedily: C3 moves (value, id) per rank instead of the logits."""
-        return self.tp.size > 1 and all(t.params.temperature <= 0 for t in turns)
+        """TP knight decoding greedily: C3 moves (value, id) per rank instead of the logits —
+        except in a captured step over a gloo group, where that host-staged gather cannot run:
+        there the logits go through K9's one-shot gather and the sampler takes the argmax."""
+        if self.tp.size == 1 or not all(t.params.temperature <= 0 for t in turns):
+            return False
+        return not (self.on_gpu and self.ecfg.use_graphs and self.tp.backend() != "nccl")
+
+    def k9_only_step(self) -> bool:
+        """Every collective of a decode step runs as a device-side K9 kernel: the all-reduces
+        (K9 / fused EPI_AR) and the vocab gather (one-shot gather)."""
+        os_ = self.tp.oneshot
+        return os_ is not None and bool(getattr(os_, "gather_ok", False))
+
+    def _agreed_graph(self, B: int, max_ctx: int, grouped: bool, dist_greedy: bool):
+        """The captured decode step, or None (eager). A capture that fails on ANY rank of a
+        tensor-parallel group sends EVERY rank to eager decode (one agreement round): a rank
+        replaying a graph whose K9 calls no peer issues would wait out each poll bound."""
+        if not (self.on_gpu and self.ecfg.use_graphs):
+            return None
+        runner, err = None, None
+        try:
+            with failsafe.stage("capture"):
+                runner = self._graph_for(B, max_ctx, grouped=grouped, dist_greedy=dist_greedy)
+        except RuntimeError as e:   # e.g. a collective that refuses stream capture
+            err = e
+        if self.tp.size > 1:
+            failed = self.tp.any_rank(err is not None)
+        else:
+            if err is not None:
+                raise err
+            failed = False
+        if failed:
+            import warnings
+            warnings.warn(f"hipGraph capture failed on a rank of the tp={self.tp.size} group "
+                          f"({err if err is not None else 'peer rank'}); every rank decodes eagerly")
+            self.ecfg.use_graphs = False
+            self.graphs.clear()
+            self.stats["capture_fallbacks"] = self.stats.get("capture_fallbacks", 0) + 1
+            return None
+        return runner
 
     def _graph_for(self, B: int, max_ctx: int, grouped: bool = False, dist_greedy: bool = False) -> "DecodeGraph":
         from .graphs import DecodeGraph

@@ -14,6 +14,9 @@ dummy sequence living in a reserved scratch block and are discarded.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
+import threading
 import time
 from typing import List, Sequence
 
@@ -24,6 +27,30 @@ from ..errors import EngineTimeout
 from ..models.llama import AttnMeta
 
 MAX_STEPS = 8192
+
+_gc_lock = threading.Lock()
+_gc_depth = 0
+_gc_was_enabled = False
+
+
+@contextlib.contextmanager
+def no_gc_during_capture():
+    """Python's cyclic collector off while any thread captures a graph: the first capture to
+    enter collects and disables it, the last one to leave restores the state found on entry."""
+    global _gc_depth, _gc_was_enabled
+    with _gc_lock:
+        if _gc_depth == 0:
+            gc.collect()
+            _gc_was_enabled = gc.isenabled()
+            gc.disable()
+        _gc_depth += 1
+    try:
+        yield
+    finally:
+        with _gc_lock:
+            _gc_depth -= 1
+            if _gc_depth == 0 and _gc_was_enabled:
+                gc.enable()
 
 
 class DecodeGraph:
@@ -158,18 +185,12 @@ class DecodeGraph:
         # Python's cyclic GC must not run inside the capture: collecting an unreachable engine or
         # graph there frees device memory / destroys a hipGraph while the stream is capturing,
         # which aborts the process (seen when a test's earlier engine was collected mid-capture).
-        # Collect now, outside, and keep the collector off until the capture has ended.
-        import gc
-        gc.collect()
-        was_enabled = gc.isenabled()
-        gc.disable()
-        try:
+        # The collector switch is process-wide and engines capture from their own threads
+        # (orchestrator.execute_plan), so it is reference-counted: off while ANY capture runs.
+        with no_gc_during_capture():
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), torch.no_grad():
                 self._body()
-        finally:
-            if was_enabled:
-                gc.enable()
         self.graph = g
         self._reset_dummy()
 
@@ -211,8 +232,11 @@ class DecodeGraph:
         first_host = first[:B].tolist()
         done_at = steps
         pending = None
+        replays = engine.stats.get("graph_replays", 0)
         for i in range(1, steps):
             self.graph.replay()
+            replays += 1
+            engine.stats["graph_replays"] = replays
             if i % chunk == 0:
                 if engine.debug_checks:
                     self.check_guard()

@@ -112,12 +112,19 @@ class DistributedPool:
                                                for k, _ in pairs):
             # every knight of the batch spans EVERY rank (one tensor-parallel group: the strong-
             # scaling layout): each rank already holds every result, identical across the group
-            # (same sampled ids from the same gathered logits) — no C1 round is needed
-            self.exchange_ms.append(0.0)
-            self.c1_skipped = getattr(self, "c1_skipped", 0) + 1
-            return [local_res[i] for i in range(len(pairs))]
+            # (same sampled ids from the same gathered logits) — no token exchange is needed. The
+            # ranks still agree on each turn's ok / error status (one small gloo gather): a turn
+            # that failed on some ranks only (a per-rank deadline, a host-side error) takes the
+            # normal C1 path below, so every rank records the leader's outcome
+            status = [isinstance(local_res[i], BaseException) for i in range(len(pairs))]
+            if all(s == status for s in self.cluster.all_gather_object(status)):
+                self.exchange_ms.append(0.0)
+                self.c1_skipped = getattr(self, "c1_skipped", 0) + 1
+                return [local_res[i] for i in range(len(pairs))]
+            self.c1_disagreements = getattr(self, "c1_disagreements", 0) + 1
         # contributions from the knights this rank leads
         led = [i for i in mine_idx if self.leader(pairs[i][0].knight_name) == rank]
+        self.c1_contributions = getattr(self, "c1_contributions", 0) + len(led)
         t0 = time.perf_counter()
         meta = {}
         ids_contrib = []

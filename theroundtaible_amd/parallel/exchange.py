@@ -55,10 +55,18 @@ class TokenExchange:
         if mine and all(d is not None for d in devs):
             src = self._src
             src.fill_(-1)
+            cur = torch.cuda.current_stream(src.device) if src.is_cuda else None
             for r, ((slot, ids, *_), d) in enumerate(zip(mine, devs)):
                 src[r, 0] = slot
                 src[r, 1] = len(ids)
                 if len(ids):
+                    if cur is not None and d.is_cuda:
+                        # the ids were written on the engine's stream: order this copy after them
+                        # and keep their memory alive until this stream has read it
+                        ev = getattr(d, "ready_event", None)
+                        if ev is not None:
+                            cur.wait_event(ev)
+                        d.record_stream(cur)
                     src[r, 2:2 + len(ids)].copy_(d.reshape(-1)[:len(ids)].to(src.device, non_blocking=True))
             self.device_path += 1
         else:

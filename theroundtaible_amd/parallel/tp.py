@@ -92,10 +92,16 @@ class TPInfo:
         turn on every rank of a TP knight when one rank's K9 flag wait expired)."""
         if self.size == 1:
             return flag
+        return self.group_min(0 if flag else 1) == 0
+
+    def group_min(self, v: int) -> int:
+        """The minimum of ``v`` over the group (host-side agreement, one small collective)."""
+        if self.size == 1:
+            return v
         dev = "cpu" if self.backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
-        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return bool(int(t.item()))
+        t = torch.tensor([v], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
 
     def greedy_gather(self, local: torch.Tensor, vocab: int) -> torch.Tensor:
         """C3 for greedy decoding without moving the logits: every rank takes the argmax of its
@@ -167,22 +173,15 @@ class SimulatedTP(TPInfo):
         return x
 
     def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
+        """The plain shard GEMM followed by the (no-op) all-reduce: no K9 comm exists here."""
         from .. import ops
-        return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
-
-    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
-        """Decode row-parallel linear (o / down on shuffled weights) + C2: ONE launch with the
-        K9 exchange fused into the GEMM epilogue when the one-shot comm passed its fused self-test,
-        else the skinny GEMM followed by :meth:`all_reduce`."""
-        from .. import ops
-        os_ = self.oneshot
-        if self.size > 1 and os_ is not None and os_.accepts_gemm(x, Ws):
-            self.fused_ar_calls = getattr(self, "fused_ar_calls", 0) + 1
-            return os_.gemm_ar(x, Ws)
         return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
 
     def any_rank(self, flag: bool) -> bool:
         return flag
+
+    def group_min(self, v: int) -> int:
+        return v
 
     def greedy_gather(self, local: torch.Tensor, vocab: int) -> torch.Tensor:
         lim = max(1, min(local.shape[1], vocab))

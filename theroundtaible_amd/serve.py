@@ -244,43 +244,69 @@ class MirroredEngine:
     def __init__(self, engine: Engine, cluster):
         self._engine, self._cluster = engine, cluster
         self._lock = threading.Lock()    # one announced operation at a time, in issue order
+        self.diverged: Optional[str] = None   # set when a follower's outcome differed from ours
 
     def __getattr__(self, name):
         return getattr(self._engine, name)
 
-    def _announce(self, op: tuple) -> None:
+    def _run(self, op: tuple, fn):
+        """Announce ``op``, run it here, then agree on every rank's outcome (one gloo gather):
+        equal inputs give equal outcomes on every rank (the KV pools are agreed at creation), so a
+        mismatch means the group's state has diverged — the followers leave their loop, and this
+        engine refuses every later operation instead of entering collectives no peer will join."""
+        if self.diverged is not None:
+            raise RuntimeError(f"tensor-parallel group stopped: {self.diverged}")
         self._cluster.broadcast_object(op)
+        res, err = None, None
+        try:
+            res = fn()
+        except Exception as e:  # noqa: BLE001 - re-raised after the agreement round
+            err = e
+        outs = self._cluster.all_gather_object(_outcome(err))
+        if any(o != outs[0] for o in outs):
+            self.diverged = f"ranks disagree on {op[0]!r}: {outs}"
+            self._engine.healthy = False
+            raise RuntimeError(f"tensor-parallel group stopped: {self.diverged}") from err
+        if err is not None:
+            raise err
+        return res
 
     def start_turns(self, turns):
         with self._lock:
-            self._announce(("start", list(turns)))
-            return self._engine.start_turns(turns)
+            return self._run(("start", list(turns)), lambda: self._engine.start_turns(turns))
 
     def continue_decode(self, seqs, turns, last, steps):
         with self._lock:
-            self._announce(("decode", [s.key for s in seqs], list(turns), [int(x) for x in last], int(steps)))
-            return self._engine.continue_decode(seqs, turns, last, steps)
+            return self._run(("decode", [s.key for s in seqs], list(turns), [int(x) for x in last], int(steps)),
+                             lambda: self._engine.continue_decode(seqs, turns, last, steps))
 
     def release(self, key: str) -> None:
         with self._lock:
-            self._announce(("release", key))
-            self._engine.release(key)
+            self._run(("release", key), lambda: self._engine.release(key))
 
     def stop_followers(self) -> None:
         with self._lock:
-            self._announce(("stop",))
+            if self.diverged is None:
+                self._cluster.broadcast_object(("stop",))
+
+
+def _outcome(err: Optional[BaseException]) -> tuple:
+    """What every rank of the group must agree on after an operation: ok, or the error's type."""
+    return ("ok",) if err is None else ("err", type(err).__name__)
 
 
 def serve_follower(engine: Engine, cluster) -> int:
     """Ranks 1..N-1 of ``serve --tp N``: run rank 0's engine operations in its order until it
-    announces ``stop``. Returns the number of operations executed. An operation that raises
-    here raises on rank 0 too (same inputs, agreed device-flag checks), which reports it."""
+    announces ``stop``. Returns the number of operations executed. After each operation the
+    ranks gather their outcomes (MirroredEngine._run): rank 0 reports a request's error; if
+    any rank's outcome differs, every rank leaves the loop (the group has diverged)."""
     n = 0
     while True:
         op = cluster.broadcast_object(None)
         kind = op[0]
         if kind == "stop":
             return n
+        err = None
         try:
             if kind == "start":
                 engine.start_turns(op[1])
@@ -289,9 +315,12 @@ def serve_follower(engine: Engine, cluster) -> int:
                 engine.continue_decode(seqs, op[2], op[3], op[4])
             elif kind == "release":
                 engine.release(op[1])
-        except Exception:  # noqa: BLE001 - rank 0 reports the request's error
-            pass
+        except Exception as e:  # noqa: BLE001 - rank 0 reports the request's error
+            err = e
+        outs = cluster.all_gather_object(_outcome(err))
         n += 1
+        if any(o != outs[0] for o in outs):
+            return n
 
 
 @dataclass
