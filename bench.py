@@ -144,9 +144,9 @@ def _predict(args, T: int, engine) -> dict:
     node's own links — so the driver's N-GPU record carries prediction and measurement side by
     side. Only for the configuration the simulated compute was measured at."""
     from theroundtaible_amd.parallel.costmodel import Calibration, load_simulated, strong_round_ms
-    simr = load_simulated(T)
+    simr = load_simulated(T, args.round_mode)
     if simr is None:
-        return {"available": False, "reason": f"no simulated tp{T} record (parallel/calib/sim{T}.json)"}
+        return {"available": False, "reason": f"no simulated tp{T} {args.round_mode} record (parallel/calib/)"}
     c = simr["config"]
     same = (c["model"] == args.model and c["new_tokens_per_turn"] == args.new_tokens
             and c["knights_per_table"] == args.knights_per_table and c["round_mode"] == args.round_mode

@@ -54,8 +54,9 @@ int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* c
 int oneshot_create(int world, int rank, int cap_elems, char* handles);
 int oneshot_open(int id, const char* all_handles);
 int oneshot_capacity(int id);
-int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream);
-int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, hipStream_t stream);
+int oneshot_allreduce(int id, void* inout, int n, void* res, hipStream_t stream);
+int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, void* res,
+                    hipStream_t stream);
 int oneshot_allgather(int id, const void* in, void* out, int rows, int shard, hipStream_t stream);
 int oneshot_gather_capacity();
 int oneshot_handle_bytes();
@@ -410,10 +411,17 @@ void py_oneshot_open(int64_t id, py::bytes all_handles, int64_t world) {
   const int rc = oneshot_open((int)id, hs.data());
   TORCH_CHECK(rc == 0, "oneshot_open: hipIpcOpenMemHandle failed (rc=", rc, ")");
 }
-void py_oneshot_allreduce(int64_t id, torch::Tensor x) {
+// res (optional): the residual form, res = bf16(res + bf16(sum over ranks of x)) in place, x kept.
+void py_oneshot_allreduce(int64_t id, torch::Tensor x, c10::optional<torch::Tensor> res) {
   check_bf16(x, "oneshot_allreduce input");
   TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= oneshot_capacity((int)id), "oneshot_allreduce: size");
-  const int rc = oneshot_allreduce((int)id, x.data_ptr(), (int)x.numel(), cur_stream());
+  void* rp = nullptr;
+  if (res.has_value()) {
+    check_bf16(*res, "oneshot_allreduce res");
+    TORCH_CHECK(res->numel() == x.numel(), "oneshot_allreduce: res must match x");
+    rp = res->data_ptr();
+  }
+  const int rc = oneshot_allreduce((int)id, x.data_ptr(), (int)x.numel(), rp, cur_stream());
   TORCH_CHECK(rc == 0, "oneshot_allreduce failed (rc=", rc, ")");
 }
 // One-shot all-gather along the last dim (C3 logits): out [rows, world * shard] from in [rows, shard].
@@ -427,14 +435,23 @@ void py_oneshot_allgather(int64_t id, torch::Tensor in, torch::Tensor out, int64
   TORCH_CHECK(rc == 0, "oneshot_allgather: unsupported configuration (rc=", rc, ")");
 }
 // Row-parallel decode GEMM with the K9 exchange fused into its epilogue (EPI_AR).
-void py_oneshot_gemm_ar(int64_t id, torch::Tensor out, torch::Tensor x, torch::Tensor Ws) {
+// res (optional): the residual form — res [M,N] += the all-reduced product (bf16-rounded), in place.
+void py_oneshot_gemm_ar(int64_t id, torch::Tensor out, torch::Tensor x, torch::Tensor Ws,
+                        c10::optional<torch::Tensor> res) {
   check_bf16(out, "oneshot_gemm_ar out");
   check_bf16(x, "oneshot_gemm_ar x");
   check_bf16(Ws, "oneshot_gemm_ar Ws");
   TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "oneshot_gemm_ar: x [M,K], Ws [N,K]");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) == Ws.size(0), "oneshot_gemm_ar: out [M,N]");
+  void* rp = nullptr;
+  if (res.has_value()) {
+    check_bf16(*res, "oneshot_gemm_ar res");
+    TORCH_CHECK(res->dim() == 2 && res->size(0) == x.size(0) && res->size(1) == Ws.size(0),
+                "oneshot_gemm_ar: res [M,N]");
+    rp = res->data_ptr();
+  }
   const int rc = oneshot_gemm_ar((int)id, out.data_ptr(), x.data_ptr(), Ws.data_ptr(), (int)x.size(0),
-                                 (int)Ws.size(0), (int)x.size(1), cur_stream());
+                                 (int)Ws.size(0), (int)x.size(1), rp, cur_stream());
   TORCH_CHECK(rc == 0, "oneshot_gemm_ar: unsupported configuration (rc=", rc, ")");
 }
 
@@ -600,8 +617,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_prep", &decode_prep);
   m.def("oneshot_create", &py_oneshot_create, py::arg("world"), py::arg("rank"), py::arg("cap_elems"));
   m.def("oneshot_open", &py_oneshot_open, py::arg("id"), py::arg("all_handles"), py::arg("world"));
-  m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"));
-  m.def("oneshot_gemm_ar", &py_oneshot_gemm_ar, py::arg("id"), py::arg("out"), py::arg("x"), py::arg("Ws"));
+  m.def("oneshot_allreduce", &py_oneshot_allreduce, py::arg("id"), py::arg("x"), py::arg("res") = py::none());
+  m.def("oneshot_gemm_ar", &py_oneshot_gemm_ar, py::arg("id"), py::arg("out"), py::arg("x"), py::arg("Ws"),
+        py::arg("res") = py::none());
   m.def("oneshot_allgather", &py_oneshot_allgather, py::arg("id"), py::arg("in"), py::arg("out"), py::arg("world"));
   m.def("oneshot_gather_capacity", []() { return oneshot_gather_capacity(); });
   m.def("oneshot_capacity", [](int64_t id) { return oneshot_capacity((int)id); });

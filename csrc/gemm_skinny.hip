@@ -215,18 +215,20 @@ int launch_unshuffle_weight(void* W, const void* Ws, int N, int K, int rope_rows
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// ALDS decision (skinny_core.h): RT_GEMM_ALDS=0 never, =1 whenever the staged rows fit, default:
-// when they fit and the launch has at most one workgroup per CU (tensor-parallel shard shapes;
-// with several workgroups per CU the activation loads hide under HBM and the staging LDS would
-// cost occupancy). Staged rows + row sums <= 48 KB, so the workgroup stays under 64 KB of LDS.
+// ALDS decision (skinny_core.h): RT_GEMM_ALDS=1 whenever the staged rows fit, =2 when they fit
+// and the launch has at most one workgroup per CU, unset / 0 never. Staged rows + row sums
+// <= 48 KB, so the workgroup stays under 64 KB of LDS.
 constexpr int ALDS_MAX_BYTES = 48 * 1024;
 bool use_alds(int M, int kspan, int wgs, int cus) {
+  // default OFF: measured slower than the pipelined activation loads on every shard shape except
+  // the NORM_ADD prologue, which the decode path no longer uses (tools/probes/gemm_variants.py,
+  // profiles/r04/gemm_variants.md); RT_GEMM_ALDS=1 forces it, =2 is the "shard shapes" rule
   static const int mode = [] {
     const char* e = getenv("RT_GEMM_ALDS");
-    return e ? atoi(e) : -1;
+    return e ? atoi(e) : 0;
   }();
   if (mode == 0 || skinny::alds_bytes(M, kspan) > ALDS_MAX_BYTES) return false;
-  return mode == 1 || (cus > 0 && wgs <= cus);
+  return mode == 1 || (mode == 2 && cus > 0 && wgs <= cus);
 }
 
 int split_workspace_ints(int max_split_tiles) { return SPLIT_CTRS + max_split_tiles * 2 * SPLIT_STRIDE; }
@@ -380,7 +382,15 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     if (sscanf(e, "%dx%d", &nw, &u) != 2) return 0;
     return nw * 100 + u;
   }();
-  const int cfg = cfg_env ? cfg_env : ((N / 16) >= 384 ? 402 : 404);
+  // 129-224 tiles of >= 64 KB (tensor-parallel shards: tp2 qkv 192 tiles) stream on most of the
+  // CUs: 8 waves keep twice the bytes in flight per CU (tp2 qkv norm+rope 7.86 -> 7.34 us;
+  // tools/probes/stream_probe.hip 192 x 128 KB 8x2 6.53 / 4x4 6.99 us). Fewer tiles (48-96) stay
+  // at 4 x 4: 16 x 2 streams faster there in the probe (48 x 128 KB 5.32 vs 6.00 us) but loses in
+  // the GEMM (tp8 qkv 6.74 -> 7.24 us: the 16-wave LDS reduction and epilogue).
+  const int T16 = N / 16;
+  int cfg_shape = T16 >= 384 ? 402 : 404;
+  if (K >= 2048 && T16 > 128 && T16 <= 224) cfg_shape = 802;
+  const int cfg = cfg_env ? cfg_env : cfg_shape;
   dim3 grid(N / 16);
   const bool alds = !cfg_env && use_alds(M, K, N / 16, device_cus());
   const size_t lds = alds ? (size_t)skinny::alds_bytes(M, K) : 0;
@@ -388,6 +398,7 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   do {                                                                                                       \
     switch (cfg) {                                                                                           \
       case 402: RT_SGV(P, E, 4, 2); break;                                                                   \
+      case 1602: RT_SGV(P, E, 16, 2); break;                                                                 \
       case 802: RT_SGV(P, E, 8, 2); break;                                                                   \
       case 408: RT_SGV(P, E, 4, 8); break;                                                                   \
       case 804: RT_SGV(P, E, 8, 4); break;                                                                   \

@@ -44,9 +44,12 @@ struct Peers {
   uint32_t* flags[MAXW];   // rank p's flags: [2 slots][world][MAXB]
 };
 
+// res != nullptr: the residual form — the sum is rounded to bf16 and added into res in place,
+// res = bf16(res + bf16(sum)) (exactly what the next layer's NORM_ADD prologue used to form), and
+// `inout` is left as it was; the next GEMM then reads res with a plain NORM prologue.
 __global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ inout, int n, int rank, int world,
                                                          int cap, Peers P, uint32_t* epoch_ctr, uint32_t* done_ctr,
-                                                         int* err, long long poll_limit) {
+                                                         int* err, long long poll_limit, uint16_t* __restrict__ res) {
   const uint32_t epoch = __hip_atomic_load(epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int slot = (int)(epoch & 1u);
   const int nb = gridDim.x, blk = blockIdx.x;
@@ -95,12 +98,21 @@ __global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ 
         acc[2 * j + 1] += rt::bf2f((uint16_t)(w[j] >> 16));
       }
     }
+    if (res != nullptr) {
+      const vec rv = reinterpret_cast<const vec*>(res)[v];
+      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] = rt::bf2f((uint16_t)(rw[j] & 0xffffu)) + rt::bf2f(rt::f2bf(acc[2 * j]));
+        acc[2 * j + 1] = rt::bf2f((uint16_t)(rw[j] >> 16)) + rt::bf2f(rt::f2bf(acc[2 * j + 1]));
+      }
+    }
     vec o;
     o.x = rt::pack2(acc[0], acc[1]);
     o.y = rt::pack2(acc[2], acc[3]);
     o.z = rt::pack2(acc[4], acc[5]);
     o.w = rt::pack2(acc[6], acc[7]);
-    reinterpret_cast<vec*>(inout)[v] = o;
+    reinterpret_cast<vec*>(res != nullptr ? res : inout)[v] = o;
   }
   // 5. the last workgroup out advances the call counter (every workgroup has read it)
   __syncthreads();
@@ -289,30 +301,35 @@ int oneshot_capacity(int id) {
 }
 
 // In-place sum over the group of `n` bf16 elements at `inout` (device pointer, 16-B aligned).
-int oneshot_allreduce(int id, void* inout, int n, hipStream_t stream) {
+// res (optional, [n] bf16, 16-B aligned): the residual form (see oneshot_ar_kernel).
+int oneshot_allreduce(int id, void* inout, int n, void* res, hipStream_t stream) {
   Comm* c = get(id);
   if (c == nullptr) return -1;
-  if (n <= 0 || n % 8 || n > c->cap || ((uintptr_t)inout & 15)) return -2;
+  if (n <= 0 || n % 8 || n > c->cap || ((uintptr_t)inout & 15) || ((uintptr_t)res & 15)) return -2;
   for (int p = 0; p < c->world; ++p)
     if (c->peers.data[p] == nullptr) return -3;   // oneshot_open not called
   int nb = n / 2048;                                // ~4 KB of slice per workgroup
   nb = nb < 1 ? 1 : (nb > MAXB ? MAXB : nb);
   hipLaunchKernelGGL(oneshot_ar_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
-                     c->cap, c->peers, c->ctr, c->ctr + 1, c->err, c->poll_limit);
+                     c->cap, c->peers, c->ctr, c->ctr + 1, c->err, c->poll_limit, (uint16_t*)res);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
 // Fused row-parallel decode GEMM + all-reduce: out[M, N] = sum over ranks of x_r[M, K] . W_r[N, K]^T,
 // every rank calling with its own shard (Ws shuffled by shuffle_weight, plain layout rule).
 // Same (NW, U) rule as the standalone plain launch (gemm_skinny.hip): 4 x 4 below 384 tiles.
-int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, hipStream_t stream) {
+// res (optional, [M, N] bf16): the residual form — res = bf16(res + bf16(sum)) in place, `out`
+// untouched (may be null).
+int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int N, int K, void* res,
+                    hipStream_t stream) {
   Comm* c = get(id);
   if (c == nullptr) return -1;
   if (M < 1 || M > 16 || K % 32 || N % 16 || N / 16 > MAXT || (int64_t)M * N > c->cap) return -2;
   if (((uintptr_t)out & 15) || ((uintptr_t)x & 15) || ((uintptr_t)Ws & 15)) return -2;
+  if (out == nullptr && res == nullptr) return -2;
   for (int p = 0; p < c->world; ++p)
     if (c->peers.data[p] == nullptr || c->peer_tflags[p] == nullptr) return -3;
-  skinny::GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const rt::short8*)Ws, nullptr, M, N, K, N, 0.f,
+  skinny::GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const rt::short8*)Ws, (uint16_t*)res, M, N, K, N, 0.f,
                         skinny::RopeEpi{}, nullptr, nullptr};
   for (int p = 0; p < c->world; ++p) {
     args.ar.data[p] = c->peers.data[p];

@@ -413,7 +413,12 @@ RT_DEVICE void ar_exchange(const GemmArgs& p, int tile, float v, int m, int n, b
     const uint16_t* own = ar.data[ar.rank] + (size_t)slot * ar.world * ar.cap + (size_t)m * N + tile * 16 + n;
     float acc = 0.f;
     for (int r = 0; r < ar.world; ++r) acc += rt::bf2f(r == ar.rank ? mine : own[(size_t)r * ar.cap]);
-    p.out[(size_t)m * p.ldo + tile * 16 + n] = rt::f2bf(acc);
+    if (p.res != nullptr) {   // residual form: res = bf16(res + bf16(sum)), in place
+      uint16_t* rp = p.res + (size_t)m * N + tile * 16 + n;
+      *rp = rt::f2bf(rt::bf2f(*rp) + rt::bf2f(rt::f2bf(acc)));
+    } else {
+      p.out[(size_t)m * p.ldo + tile * 16 + n] = rt::f2bf(acc);
+    }
   }
   // 5. the last workgroup out advances the call counter (every workgroup has read it)
   __syncthreads();

@@ -89,7 +89,7 @@ def test_strong_scaling_sampled_decode_on_shared_gpu():
     assert out["detail"]["decode_tokens"] == 3 * 16 * 2, out["_log"]
 
 
-def _tp_check(nproc, model, layers, tokens=12):
+def _tp_check(nproc, model, layers, tokens=12, extra=(), fused_ar=None):
     gc.collect()
     torch.cuda.empty_cache()
     port = free_port()
@@ -97,9 +97,9 @@ def _tp_check(nproc, model, layers, tokens=12):
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "tp_check.py"),
-           "--model", model, "--layers", str(layers), "--tokens", str(tokens), "--out", out]
+           "--model", model, "--layers", str(layers), "--tokens", str(tokens), "--out", out, *extra]
     env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    if nproc == 2:
+    if fused_ar if fused_ar is not None else nproc == 2:
         # two ranks sharing the GPU co-schedule reliably: decode on the fused GEMM + exchange
         # (one rank per GPU enables it by default; more sharing ranks keep the separate K9)
         env["ROUNDTABLE_FUSED_AR"] = "1"
@@ -111,8 +111,8 @@ def _tp_check(nproc, model, layers, tokens=12):
 @pytest.mark.parametrize("model,layers,tp", [("llama3-8b", 2, 2), ("llama3-8b", 2, 4), ("llama3-8b", 2, 8),
                                              ("llama3-70b", 2, 4)])
 def test_tp_fused_decode_matches_tp1_on_shared_gpu(model, layers, tp):
-    """the tensor-parallel FUSED decode with real shards — split-K NORM_ADD
-    qkv / gate_up, ping-pong residual, K9 one-shot all-reduces between the ranks, vocab-parallel
+    """the tensor-parallel FUSED decode with real shards — split-K gate_up,
+    the residual added by the all-reduce epilogues, K9 one-shot all-reduces between the ranks, vocab-parallel
     lm_head — against a tp=1 engine with the same ``random-dev`` weights on the same GPU:
     prefill and decode logits cosine > 0.999, greedy tokens identical, no failed turn, no
     expired K9 wait; o / down on the fused GEMM + all-reduce launch. Llama-3-8B shapes (the strong-scaling bench) and Llama-3-70B (config 5)."""
@@ -174,3 +174,27 @@ def test_c1_speculative_prefill_striped_on_shared_gpu():
     # (other GEMM shapes), so its bf16 K/V round differently (the fp32 CPU test pins equality)
     assert d["speculative_kept_tokens_rank0"] > 0, on["_log"]
     assert off["detail"]["decode_tokens"] == d["decode_tokens"]
+
+
+@pytest.mark.parametrize("model,layers,tp,fused", [("llama3-8b", 2, 2, True), ("llama3-8b", 2, 4, True),
+                                                   ("llama3-8b", 2, 8, False), ("llama3-70b", 2, 4, False)])
+def test_tp_captured_decode_across_ranks_on_shared_gpu(model, layers, tp, fused):
+    """the hot path of the driver's N-GPU run — the hipGraph-CAPTURED tensor-
+    parallel decode step (K9 all-reduces adding into the residual, the one-shot logits gather,
+    split-K shard GEMMs) — replayed by every rank of a gloo rehearsal group (every in-step
+    collective is a K9 kernel, so the step captures though the host group is gloo). EPI_AR (the
+    exchange in the o / down epilogues) forced on at tp 2 and 4. Greedy ids equal the tp=1
+    engine, logits cosine > 0.999, graph replays on EVERY rank, no capture fallback, no expired
+    K9 wait (a short poll bound: a rehearsal the scheduler does not co-run fails, never spins)."""
+    ref = _tp_check(1, model, layers, extra=("--graphs",))
+    got = _tp_check(tp, model, layers, extra=("--graphs", "--poll-limit", "65536"), fused_ar=fused)
+    assert got["world"] == tp and got["k9"], got
+    assert all(got["graphs_per_rank"]) and got["capture_fallbacks"] == 0, got
+    assert len(got["graph_replays_per_rank"]) == tp and min(got["graph_replays_per_rank"]) > 0, got
+    if fused:
+        assert got["fused_ar"] and min(got["fused_ar_calls_per_rank"]) > 0, got
+    assert all(e is None for e in got["errors"]) and not got["flag_errors"], (got["errors"], got["flag_errors"])
+    cos = torch.nn.functional.cosine_similarity
+    c_dec = float(cos(got["decode_logits"][None], ref["decode_logits"][None]))
+    assert c_dec > 0.999, c_dec
+    assert got["ids"] == ref["ids"], (got["ids"], ref["ids"])

@@ -189,40 +189,33 @@ class LlamaModel:
 
     def forward_decode_fused_tp(self, ids: torch.Tensor, positions: torch.Tensor, kv, meta: AttnMeta,
                                 hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Tensor-parallel fused decode (Megatron split): o/down are row-parallel,
-        so their outputs are partial sums — stored plainly, all-reduced over RCCL (C2, inside the
-        hipGraph), and added to the residual by the NEXT GEMM's NORM_ADD prologue, whose
-        workgroup 0 also writes the new residual (ping-pong buffers, never in place). The lm_head
-        is vocab-parallel + all-gather (C3). 5 kernels per layer: when the K9 comm passed its fused
-        self-test, o / down carry the all-reduce in their epilogue (``tp.row_parallel``), else
-        5 kernels + 2 all-reduce launches."""
+        """Tensor-parallel fused decode (Megatron split), the same 4 GEMMs per
+        layer as tp 1: qkv (RMSNorm + RoPE/KV-cache epilogue) -> K3 -> o -> gate_up (RMSNorm +
+        SwiGLU) -> down. o / down are row-parallel: their partial sums are all-reduced over the
+        group (C2) and added into the residual stream in place by the same launch — the K9 exchange
+        in the GEMM epilogue when the one-shot comm passed its fused self-test, else the GEMM + a
+        K9 launch in its residual form (``tp.row_parallel(res=)``). The lm_head is vocab-parallel
+        + all-gather (C3). Round 3 instead handed the partial to the next GEMM's NORM_ADD
+        prologue, which re-added it in every workgroup: 1-3 us per GEMM at shard shapes
+        (profiles/r04/gemm_variants.md). qkv never takes split-K (its seam cost more than the
+        48-192 unsplit tiles lose; same table)."""
         cfg, tp = self.cfg, self.tp
         eps = cfg.norm_eps
         dec = self.decode_weights()
+        # the residual stream is updated in place by every row-parallel launch
         res = hidden if hidden is not None else F.embedding(ids, self.w["embed"]).contiguous()
-        bufs = [res, torch.empty_like(res)]
-        cur = 0
         B = ids.shape[0]
-        h = None
-        # split-K wherever a shard has fewer tiles than CUs (qkv / gate_up at tp >= 2)
         sk = dict(split_ws=dec["split_ws"], split_mode=ops.SPLIT_K)
         for l, lw in enumerate(dec["layers"]):
             kc, vc = kv.k_layer(l), kv.v_layer(l)
-            if h is None:
-                q = ops.skinny_gemm_rope(bufs[cur], lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kc, vc,
-                                         meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps, **sk)
-            else:
-                q = ops.skinny_gemm_rope(bufs[cur], lw["wqkv"], ops.PRO_NORM_ADD, positions, self.cos_sin, kc, vc,
-                                         meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps,
-                                         x2=h, xout=bufs[1 - cur], **sk)
-                cur = 1 - cur
+            q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kc, vc,
+                                     meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps,
+                                     split_ws=dec["split_ws"], split_mode=0)
             a = self.attention(q, kc, vc, meta)
-            h = tp.row_parallel(a.reshape(B, -1), lw["wo"], **sk)
-            g = ops.skinny_gemm(bufs[cur], lw["w_gate_up"], ops.PRO_NORM_ADD, ops.EPI_SWIGLU, eps=eps, x2=h,
-                                xout=bufs[1 - cur], **sk)
-            cur = 1 - cur
-            h = tp.row_parallel(g, lw["w_down"], **sk)
-        logits = ops.skinny_gemm(bufs[cur], dec["lm_head"], ops.PRO_NORM_ADD, ops.EPI_STORE, eps=eps, x2=h, **sk)
+            tp.row_parallel(a.reshape(B, -1), lw["wo"], res=res, **sk)
+            g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps, **sk)
+            tp.row_parallel(g, lw["w_down"], res=res, **sk)
+        logits = ops.skinny_gemm(res, dec["lm_head"], ops.PRO_NORM, ops.EPI_STORE, eps=eps, **sk)
         if meta.local_logits:
             return logits
         logits = tp.all_gather_last(logits)

@@ -199,11 +199,12 @@ def split_plans(model: str, knights: int, n_gpus: int, fits=None, **kw) -> List[
 SIM_DIR = __import__("os").path.join(__import__("os").path.dirname(__file__), "calib")
 
 
-def load_simulated(n: int) -> Optional[dict]:
-    """The ``bench.py --simulate-tp n`` record (``sim{n}.json``; n = 1 is the plain 1-GPU run)."""
+def load_simulated(n: int, round_mode: str = "parallel") -> Optional[dict]:
+    """The ``bench.py --simulate-tp n`` record (``sim{n}.json``; n = 1 is the plain 1-GPU run;
+    sequential rounds: ``sim{n}_seq.json``)."""
     import json
     import os
-    path = os.path.join(SIM_DIR, f"sim{n}.json")
+    path = os.path.join(SIM_DIR, f"sim{n}.json" if round_mode == "parallel" else f"sim{n}_seq.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -217,13 +218,16 @@ def strong_round_ms(sim: dict, n: int, k9_us: float, gather_us: float, fused_sav
     the fused form's saving) and one logits gather + the prefill ring all-reduces."""
     cal = cal or default_calibration()
     cfg = get_config(sim["config"]["model"].split(" ")[0])
-    steps = sim["config"]["new_tokens_per_turn"]
+    # decode steps per round: one batched decode (parallel rounds), or one per speaker (sequential:
+    # reference semantics, /root/reference/src/orchestrator.ts:361-536, every step at B = 1)
+    turns = sim["config"]["knights_per_table"] if sim["config"].get("round_mode") == "sequential" else 1
+    steps = sim["config"]["new_tokens_per_turn"] * turns
     comp = sim["ms_per_round"]
     if n == 1:
         return comp
     ar = max(0.0, k9_us - fused_saving_us)
     decode_comm = steps * (2 * cfg.n_layers * ar + gather_us) / 1e3
-    pre_tok = sim["detail"]["prefill_tokens"] / max(1, sim["steps"])
+    pre_tok = sim["detail"]["prefill_tokens"] / max(1, sim["steps"]) / turns
     msg = pre_tok * cfg.hidden * 2
-    prefill_ar = 2 * cfg.n_layers * (2 * (n - 1) / n * msg / (cal.prefill_ar_gbps * 1e9) * 1e3 + 0.02)
+    prefill_ar = turns * 2 * cfg.n_layers * (2 * (n - 1) / n * msg / (cal.prefill_ar_gbps * 1e9) * 1e3 + 0.02)
     return comp + decode_comm + prefill_ar

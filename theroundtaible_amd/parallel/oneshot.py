@@ -91,9 +91,17 @@ class OneShotAllReduce:
         self._nat.oneshot_allgather(self.id, _aligned(x), out, self.world)
         return out
 
-    def gemm_ar(self, x: torch.Tensor, Ws: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def gemm_ar(self, x: torch.Tensor, Ws: torch.Tensor, out: Optional[torch.Tensor] = None,
+                res: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``sum over ranks of x_r @ W_r^T`` ([M, N] bf16) with ``Ws`` = this rank's shuffled
-        row-parallel shard: one launch, the K9 exchange in the epilogue."""
+        row-parallel shard: one launch, the K9 exchange in the epilogue. ``res``: the residual
+        form — ``res = bf16(res + bf16(sum))`` in place (returned), nothing else written."""
+        if res is not None:
+            if res.data_ptr() % 16 == 0 and res.is_contiguous():
+                self._nat.oneshot_gemm_ar(self.id, res, _aligned(x), Ws, res)
+                return res
+            # (rank-invariant collective either way: the same fused call, then a local add)
+            return res.add_(self.gemm_ar(x, Ws, out))
         if out is None:
             out = torch.empty(x.shape[0], Ws.shape[0], dtype=x.dtype, device=x.device)
         self._nat.oneshot_gemm_ar(self.id, out, _aligned(x), Ws)
@@ -106,7 +114,14 @@ class OneShotAllReduce:
         return (self.id is not None and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
                 and x.numel() % 8 == 0 and 0 < x.numel() <= self.cap)
 
-    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, res: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """In-place sum over the group; with ``res``: ``res = bf16(res + bf16(sum))`` in place
+        (the residual form, ``x`` left as it was), returns ``res``."""
+        if res is not None:
+            if x.data_ptr() % 16 == 0 and res.data_ptr() % 16 == 0 and res.is_contiguous():
+                self._nat.oneshot_allreduce(self.id, x, res)
+                return res
+            return res.add_(self(x))      # same single K9 call on every rank, then a local add
         if x.data_ptr() % 16:
             t = x.clone()                 # fresh allocations are 16-B aligned
             self._nat.oneshot_allreduce(self.id, t)

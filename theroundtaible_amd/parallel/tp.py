@@ -76,16 +76,27 @@ class TPInfo:
                 dist.all_reduce(x, group=self.group)
         return x
 
-    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
+    def all_reduce_into(self, x: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+        """C2 with the residual add fused: ``res = bf16(res + bf16(sum over ranks of x))`` in
+        place (K9's residual form; host collectives + a bf16 add otherwise, the same bits)."""
+        if self.size > 1 and self.oneshot is not None and self.oneshot.accepts(x):
+            return self.oneshot(x, res=res)
+        return res.add_(self.all_reduce(x))
+
+    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, res: Optional[torch.Tensor] = None,
+                     **gemm_kw) -> torch.Tensor:
         """Decode row-parallel linear (o / down on shuffled weights) + C2: ONE launch with the
         K9 exchange fused into the GEMM epilogue when the one-shot comm passed its fused self-test,
-        else the skinny GEMM followed by :meth:`all_reduce`."""
+        else the skinny GEMM followed by :meth:`all_reduce`. ``res``: the decode residual stream —
+        the all-reduced output is added into it in place (the same epilogue / K9 launch), so the
+        next GEMM reads it with a plain RMSNorm prologue, exactly as at tp 1."""
         from .. import ops
         os_ = self.oneshot
         if self.size > 1 and os_ is not None and os_.accepts_gemm(x, Ws):
             self.fused_ar_calls = getattr(self, "fused_ar_calls", 0) + 1
-            return os_.gemm_ar(x, Ws)
-        return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
+            return os_.gemm_ar(x, Ws, res=res)
+        y = ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw)
+        return self.all_reduce(y) if res is None else self.all_reduce_into(y, res)
 
     def any_rank(self, flag: bool) -> bool:
         """True if ``flag`` is set on any rank of the group (host-side agreement, e.g. to fail a
@@ -172,9 +183,14 @@ class SimulatedTP(TPInfo):
         self.sim_all_reduces = getattr(self, "sim_all_reduces", 0) + 1
         return x
 
-    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, **gemm_kw) -> torch.Tensor:
-        """The plain shard GEMM followed by the (no-op) all-reduce: no K9 comm exists here."""
+    def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, res: Optional[torch.Tensor] = None,
+                     **gemm_kw) -> torch.Tensor:
+        """The shard GEMM with the (no-op) all-reduce elided; the residual add stays (RESID
+        epilogue: the work the fused K9 epilogue does besides communicating)."""
         from .. import ops
+        if res is not None:
+            self.sim_all_reduces = getattr(self, "sim_all_reduces", 0) + 1
+            return ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, **gemm_kw)
         return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
 
     def any_rank(self, flag: bool) -> bool:

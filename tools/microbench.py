@@ -112,7 +112,7 @@ def bench_gemm(M):
 
 def bench_gemm_tp(M, tp, model="llama3-8b"):
     """The per-rank decode GEMMs of a tensor-parallel knight, exactly as forward_decode_fused_tp
-    issues them (NORM_ADD prologues, STORE epilogues before the all-reduce, split-K workspace):
+    issues them (NORM prologues; o / down with the residual add the all-reduce epilogue carries):
     qkv [(Hq+2Hkv)/tp * D, H], o [H, Hq*D/tp], gate_up [2 F/tp, H], down [H, F/tp], lm_head
     [V/tp, H]. RT_SPLITK / RT_SPLITK_TARGET pin the split (read once per process)."""
     from theroundtaible_amd.models.config import get_config
@@ -131,8 +131,8 @@ def bench_gemm_tp(M, tp, model="llama3-8b"):
     slots = torch.arange(M, device=DEV, dtype=torch.int64) + 40
     sw = ops.split_workspace(DEV)
     sk = dict(split_ws=sw, split_mode=ops.SPLIT_K)
-    shapes = [("qkv (norm_add+rope+cache)", (hq + 2 * hkv) * d, hid), ("o (store)", hid, hq * d),
-              ("gate_up (norm_add+swiglu)", 2 * ffn, hid), ("down (store)", hid, ffn), ("lm_head (norm_add)", vs, hid)]
+    shapes = [("qkv (norm+rope+cache)", (hq + 2 * hkv) * d, hid), ("o (+resid)", hid, hq * d),
+              ("gate_up (norm+swiglu)", 2 * ffn, hid), ("down (+resid)", hid, ffn), ("lm_head (norm)", vs, hid)]
     total = 0.0
     for name, N, K in shapes:
         nbytes = N * K * 2
@@ -140,16 +140,16 @@ def bench_gemm_tp(M, tp, model="llama3-8b"):
         rope = name.startswith("qkv")
         Ws = [ops.shuffle_weight(bf(N, K, scale=0.02), swiglu=name.startswith("gate_up"),
                                  rope_heads=hq + hkv if rope else 0, head_dim=d if rope else 0) for _ in range(copies)]
-        if rope:
-            fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM_ADD, pos, cs, kc, vc, slots, hq, hkv, d,
-                                                x2=x2, xout=xo, **sk)
+        if rope:   # the decode path never splits qkv (models/llama.py forward_decode_fused_tp)
+            fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d,
+                                                split_ws=sw, split_mode=0)
         elif name.startswith("gate_up"):
-            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM_ADD, ops.EPI_SWIGLU, x2=x2, xout=xo, **sk)
+            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM, ops.EPI_SWIGLU, **sk)
         elif name.startswith("lm_head"):
-            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM_ADD, ops.EPI_STORE, x2=x2, **sk)
-        else:
+            fn = lambda i: ops.skinny_gemm(x, Ws[i % copies], ops.PRO_NORM, ops.EPI_STORE, **sk)
+        else:      # row-parallel: the residual add of the all-reduce epilogue, communication elided
             inp = a_in if name.startswith("o ") else g_in
-            fn = lambda i, inp=inp: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_STORE, **sk)
+            fn = lambda i, inp=inp: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_RESID, res=xo, **sk)
         us = timed(fn)
         T = N // 16 // (2 if name.startswith("gate_up") else 1)
         S = ops.native().splitk_parts(T, K // 32, torch.cuda.get_device_properties(0).multi_processor_count,

@@ -7,9 +7,10 @@ One process per rank (torchrun). Ranks may share one GPU (ROUNDTABLE_DIST_BACKEN
 or own one each (RCCL + K9 over xGMI). Every rank:
 
 1. prefills a fixed prompt (column/row-parallel hipBLASLt GEMMs + C2 all-reduce) -> logits;
-2. runs ONE fused decode step by hand (split-K shard GEMMs, NORM_ADD ping-pong residual, K9
-   one-shot all-reduces, vocab-parallel lm_head + C3 all-gather) -> logits;
-3. greedy-decodes ``--tokens`` tokens through ``run_turns`` (C3 distributed argmax).
+2. runs ONE fused decode step by hand (shard GEMMs, K9 one-shot all-reduces adding into the
+   residual, vocab-parallel lm_head + C3 all-gather) -> logits;
+3. greedy-decodes ``--tokens`` tokens through ``run_turns`` (C3 distributed argmax; with
+   ``--graphs`` the captured decode step, replayed once per token on every rank).
 
 Rank 0 writes {prefill_logits, decode_logits, ids, ...} to ``--out`` (torch.save). The tp=1
 reference is the same script with ``--nproc-per-node 1``; tests/test_distributed_gpu.py compares.
@@ -31,7 +32,11 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--tokens", type=int, default=12)
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--graphs", action="store_true", help="hipGraph decode (RCCL groups only; gloo stays eager)")
+    ap.add_argument("--graphs", action="store_true",
+                    help="hipGraph decode: RCCL groups, or gloo groups whose every in-step collective is K9")
+    ap.add_argument("--poll-limit", type=int, default=0,
+                    help="K9 flag-wait bound in polls (0 = the comm's default): a rehearsal whose ranks share a "
+                         "GPU fails fast instead of spinning if the scheduler does not co-run their grids")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     import torch
@@ -48,6 +53,8 @@ def main() -> int:
     e = Engine(EngineConfig(model=a.model, weights=f"random-dev:{a.seed}", device=cl.device, dtype="bf16",
                             max_kv_tokens=4096, kv_cache_fraction=0.05, use_graphs=a.graphs,
                             weight_residency="dual", model_overrides={"n_layers": a.layers}), tp)
+    if a.poll_limit and getattr(e.tp, "oneshot", None) is not None:
+        e.tp.oneshot.set_poll_limit(a.poll_limit)
     prompt = "De ronde tafel bespreekt tensor-parallelle ridders over xGMI. " * 6
     ids = e.encode_prompt(prompt)
     s = e.kv.seq("probe")
@@ -67,7 +74,15 @@ def main() -> int:
     sp = SamplingParams(temperature=0.0, max_new_tokens=a.tokens, ignore_eos=True, stop_on_consensus=False)
     outs = e.run_turns([Turn("K1", prompt, sp), Turn("K2", prompt + " Tweede ridder.", sp)])
     flag_errors = e.device_flag_errors()
+    per_rank = cl.all_gather_object({"replays": int(e.stats.get("graph_replays", 0)),
+                                     "graphs": bool(e.ecfg.use_graphs),
+                                     "fallbacks": int(e.stats.get("capture_fallbacks", 0)),
+                                     "fused_ar_calls": int(getattr(e.tp, "fused_ar_calls", 0))})
     rec = {"world": cl.world, "backend": cl.backend, "fused": bool(fused),
+           "graph_replays_per_rank": [r["replays"] for r in per_rank],
+           "graphs_per_rank": [r["graphs"] for r in per_rank],
+           "capture_fallbacks": sum(r["fallbacks"] for r in per_rank),
+           "fused_ar_calls_per_rank": [r["fused_ar_calls"] for r in per_rank],
            "k9": bool(getattr(e.tp, "oneshot", None)),
            "fused_ar": bool(getattr(getattr(e.tp, "oneshot", None), "fused", False)),
            "fused_ar_calls": int(getattr(e.tp, "fused_ar_calls", 0)), "prefill_logits": pre[0].cpu(), "decode_logits": dec[0].cpu(),

@@ -39,13 +39,16 @@ def main(paths) -> int:
     cfg = get_config("llama3-8b")
     cal = Calibration()
     L = cfg.n_layers
-    steps = base["config"]["new_tokens_per_turn"]
+    mode = base["config"].get("round_mode", "parallel")
+    turns = base["config"]["knights_per_table"] if mode == "sequential" else 1
+    steps = base["config"]["new_tokens_per_turn"] * turns
     rounds = base["steps"]
     pre_tok = base["detail"]["prefill_tokens"] / rounds          # new tokens prefilled per round (all knights)
     dec_tok = base["detail"]["decode_tokens"] / rounds
-    print("# Strong-scaling cost model: one 3-knight Llama-3-8B table on a tp=N engine\n")
+    print(f"# Strong-scaling cost model: one 3-knight Llama-3-8B table on a tp=N engine ({mode} rounds)\n")
+    how = "3 knights batched" if mode == "parallel" else "the 3 speakers one after another, B = 1"
     print(f"Workload = the driver's bench config: {rounds} timed rounds, {steps} decode steps per round "
-          f"(3 knights batched), {pre_tok:.0f} prefill tokens per round, shared layout, parallel rounds.\n")
+          f"({how}), {pre_tok:.0f} prefill tokens per round, shared layout, {mode} rounds.\n")
     print("Per-rank compute measured on ONE MI355X with `bench.py --simulate-tp N` (rank 0's exact shard, "
           "collectives elided); collectives added from the per-call latencies below.\n")
     print("| N | compute ms/round (measured) | decode ms/step (measured) | prefill AR ms/round | "
