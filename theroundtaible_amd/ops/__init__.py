@@ -121,7 +121,20 @@ class DecodeWorkspace:
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: int = 64,
+_CUS: dict = {}
+
+
+def device_cus(device=None) -> int:
+    """Compute units of ``device`` (the current GPU; 256 = MI355X when no GPU is visible)."""
+    if not torch.cuda.is_available():
+        return 256
+    idx = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    if idx not in _CUS:
+        _CUS[idx] = int(torch.cuda.get_device_properties(idx).multi_processor_count)
+    return _CUS[idx]
+
+
+def decode_splits(batch: int, n_kv_heads: int, num_cus: Optional[int] = None, max_splits: int = 64,
                   grouped: bool = False) -> int:
     """Split-KV count fixed per (batch bucket, kv heads): at most one 8-wave workgroup per CU
     (measured on MI355X, profiles/r01_microbench_v1.log: B=3, ctx 6000 -> 8 splits 22 µs,
@@ -136,6 +149,7 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: int = 256, max_splits: i
     # A lone sequence (B = 1: sequential rounds) shares nothing, so it takes the whole chip: B = 1,
     # Llama-3-8B, 10K / 25K / 40K keys: 24 splits 15.9 / 26.3 / 36.8 us, 32 splits 15.0 / 25.9 /
     # 35.7 (profiles/r03/attn_b1_splits.md)
+    num_cus = device_cus() if num_cus is None else num_cus
     cus = num_cus * 3 // 4 if grouped and batch > 1 else num_cus
     want = cus // max(1, batch * n_kv_heads)        # never more workgroups than CUs: a second
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
