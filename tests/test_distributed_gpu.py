@@ -198,3 +198,19 @@ def test_tp_captured_decode_across_ranks_on_shared_gpu(model, layers, tp, fused)
     c_dec = float(cos(got["decode_logits"][None], ref["decode_logits"][None]))
     assert c_dec > 0.999, c_dec
     assert got["ids"] == ref["ids"], (got["ids"], ref["ids"])
+
+
+def test_config5_topology_two_tp2_groups_on_shared_gpu():
+    """BASELINE config 5's topology rehearsed on one MI355X: 4 gloo ranks form two
+    DISJOINT TP=2 groups, one knight each (`--tp 2 --knights-per-table 2 --knights-per-gpu 1`);
+    each group decodes its knight alone, C1 crosses the groups from the two group leaders only
+    (ranks 0 and 2), no turn fails. (Transcript equality with one rank is pinned on fp32 CPU
+    ranks: tests/test_failsafe_cpu.py::test_config5_topology_two_tp_groups; in bf16 the tp2 and
+    tp1 sums round differently.)"""
+    out = _bench(("--tp", "2", "--knights-per-table", "2", "--knights-per-gpu", "1", "--kv-fraction", "0.05"),
+                 nproc=4)
+    d = out["detail"]
+    assert out["config"]["knights"] == 2 and out["config"]["tp"] == 2, out["_log"]
+    assert "groups" in out["config"]["parallelism"], out["config"]
+    assert d["failed_turns"] == 0 and d["decode_tokens"] == 2 * 16 * 2, out["_log"]
+    assert [c > 0 for c in d["c1_contributions_per_rank"]] == [True, False, True, False], d

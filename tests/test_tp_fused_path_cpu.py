@@ -1,4 +1,4 @@
-"""The tensor-parallel FUSED decode step (``forward_decode_fused_tp``: NORM_ADD ping-pong residual,
+"""The tensor-parallel FUSED decode step (``forward_decode_fused_tp``: the residual updated in place by the all-reduce,
 ``TPInfo.row_parallel`` for o / down, vocab-parallel lm_head + gather) on CPU reference ops over
 gloo, against the unsharded tp=1 fused step with the same ``random-full`` weights.
 

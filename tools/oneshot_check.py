@@ -56,6 +56,26 @@ def main() -> int:
         err = (x.float().cpu() - expect(world, n, tag)).abs().max().item()
         assert err <= 0.0625, f"n={n}: max err {err}"
         out["checks"] += 1
+    # residual form (the tensor-parallel decode path): res = bf16(res + bf16(sum)), the input kept
+    for tag, n in ((40, 4096), (41, 3 * 4096)):
+        x = data(rank, n, tag, dev)
+        x0 = x.clone()
+        res = data(0, n, tag + 100, dev)          # the residual stream is identical on every rank
+        want = (data(0, n, tag + 100, "cpu").float() + expect(world, n, tag)).to(torch.bfloat16)
+        ar(x, res=res)
+        torch.cuda.synchronize()
+        assert torch.equal(res.cpu(), want) and torch.equal(x, x0), f"residual form n={n}"
+        out["checks"] += 1
+    if ar.fused:   # the fused GEMM + exchange with the residual add in its epilogue
+        from theroundtaible_amd.parallel.oneshot import _fused_case
+        xg, Ws = _fused_case(ar, 3, 4096, 512, 77)
+        base = data(0, 3 * 4096, 77, dev).view(3, 4096)
+        want = base.clone().add_(ar.gemm_ar(xg, Ws))
+        got = ar.gemm_ar(xg, Ws, res=base.clone())
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), "fused residual form"
+        out["checks"] += 1
+        out["fused_residual_checked"] = True
     # hipGraph: three calls captured, replayed; inputs refreshed in place before each replay
     n = 8192
     bufs = [torch.empty(n, dtype=torch.bfloat16, device=dev) for _ in range(3)]
