@@ -187,7 +187,7 @@ def test_tp_captured_decode_across_ranks_on_shared_gpu(model, layers, tp, fused)
     engine, logits cosine > 0.999, graph replays on EVERY rank, no capture fallback, no expired
     K9 wait (a short poll bound: a rehearsal the scheduler does not co-run fails, never spins)."""
     ref = _tp_check(1, model, layers, extra=("--graphs",))
-    got = _tp_check(tp, model, layers, extra=("--graphs", "--poll-limit", "65536"), fused_ar=fused)
+    got = _tp_check(tp, model, layers, extra=("--graphs", "--poll-limit", "1048576"), fused_ar=fused)
     assert got["world"] == tp and got["k9"], got
     assert all(got["graphs_per_rank"]) and got["capture_fallbacks"] == 0, got
     assert len(got["graph_replays_per_rank"]) == tp and min(got["graph_replays_per_rank"]) > 0, got
