@@ -20,6 +20,8 @@ for s in "$@"; do
          done
          steps+=("seq1:400:python -u bench.py --round-mode sequential --steps 20 --warmup 5 --out gpurun_out/r04/sim1_seq.json") ;;
     bench) steps+=("bench1:200:python -u bench.py --steps 20 --warmup 5 --out gpurun_out/r04/sim1.json") ;;
+    smp) steps+=("smp:120:python -u tools/sampler_probe.py") ;;
+    capture) steps+=("capture:900:python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_distributed_gpu.py -k 'captured or config5'") ;;
     prof) for n in 8 1; do
             if [ "$n" = 1 ]; then a=""; else a="--simulate-tp $n"; fi
             steps+=("prof$n:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04/prof$n -o p -- python3 bench.py $a --steps 5 --warmup 2 && python3 tools/prof_summary.py gpurun_out/r04/prof$n gpurun_out/r04/prof${n}_kernels.md --drop-trace")

@@ -1,5 +1,5 @@
 import sys, torch, time
-sys.path.insert(0, '/root/repo')
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 from theroundtaible_amd import ops
 DEV='cuda'
 def t(fn, n=20):
