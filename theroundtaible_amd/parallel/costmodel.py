@@ -27,12 +27,15 @@ from ..models.config import ModelConfig, get_config
 @dataclass
 class Calibration:
     # decode GEMM: floor (launch + first round trip + epilogue) and sustained weight stream.
-    # tools/microbench.py --only gemm_tp (profiles/r03/gemm_tp_shards_*.md): o tp8 4.2 MB 3.2 us,
-    # down tp8 14.7 MB 5.1 us, gate_up tp8 29 MB 10.5 us, qkv tp8 6.3 MB 8.3 us; tp1 qkv 50 MB
-    # 11.2-14.5 us, gate_up 235 MB 40.6 us, down 117 MB 19.1 us, lm_head 1.05 GB 176 us
+    # tools/microbench.py --only gemm_tp, round 4 (profiles/r04/microbench_gemm_tp_gattn.log: NORM
+    # prologues, residual epilogues): o tp8 4.2 MB 3.5 us, down tp8 14.7 MB 5.1 us, gate_up tp8
+    # 29 MB 9.4 us, qkv tp8 6.3 MB 6.8 us, tp2 qkv 25 MB 7.4 us; tp1 qkv 50 MB 11.2 us, gate_up
+    # 235 MB 36-40 us, down 117 MB 19 us, lm_head 1.05 GB 150-176 us. A pure 16-B/lane weight stream
+    # of a launch costs 2.2 us (1 workgroup) to 3.5 us (256 x 16 KB) before its bytes
+    # (tools/probes/stream_probe.hip, profiles/r04/stream_probe.csv)
     hbm_tbps: float = 6.0
     gemm_floor_us: Dict[str, float] = field(default_factory=lambda: {
-        "qkv": 6.5, "o": 2.5, "gate_up": 5.5, "down": 2.5, "lm_head": 2.5})
+        "qkv": 5.7, "o": 2.8, "gate_up": 4.6, "down": 2.7, "lm_head": 2.5})
     # grouped decode attention: floor + K/V stream (profiles/r02_bench_kernels_final_s5.md: 25.9 us
     # per layer at ~40K shared keys, tp1; r03 split cap for small KV-head shards)
     attn_floor_us: float = 8.0
