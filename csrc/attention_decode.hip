@@ -22,9 +22,10 @@ __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
 // slots at 4 query heads (r03 probe). Here every (row, 32-dim chunk) gets its own workgroup of
 // 8 dim-lanes x NSL slot-lanes (NSL = blockDim / 8, sized by the host to the row's slots, <= 128),
 // each lane owning SPL slots whose loads are ALL issued before the first merge: one round trip
-// per launch instead of one per 32 slots (round 3: 6 dependent trips at 192 slots, 6.6 us).
-// Merge order is fixed (lane-local slots in index order, then xor-shuffle pairs, then the waves
-// in index order through LDS), so the result does not depend on timing.
+// per launch instead of one per 32 slots (round 3: 6 dependent trips at 192 slots, 6.6 us), and
+// that trip overlaps the group-record lookup (the host's slot bound needs no record).
+// Merge order is fixed (lane-local slots in index order, then xor-shuffle pairs, then a tree
+// over the waves through LDS), so the result does not depend on timing.
 // Partials were stored write-through by the previous launch: the kernel boundary orders them.
 template <int D, int SPL>
 __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
@@ -34,16 +35,33 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
   const int nsl = blockDim.x >> 3;
   const int d0 = blockIdx.y * 32 + 4 * dl;
   const int G = p.Hq / p.Hkv;
-  int n = 1;
-  if (p.groups != nullptr) {
-    const int b0 = p.groups[3 * b], nn = p.groups[3 * b + 1], sh = p.groups[3 * b + 2];
-    if (!(nn < 1 || nn * G > 16 || b0 < 0 || b < b0 || b - b0 >= nn || sh < 0)) n = nn;   // as attn_item
-  }
-  const int nslots = n * p.num_splits;
-  if (nslots == 1) return;                     // written directly by the attention launch
   const int stride = p.slot_stride > 0 ? p.slot_stride : p.num_splits;
+  // the host's sizing: every split of every member of the largest group (slots past the row's
+  // own count are inside the row's stride and loaded, never merged)
+  const int nmax = p.groups != nullptr ? min(stride, (16 / G) * p.num_splits) : p.num_splits;
   const float* __restrict__ po = p.part_o + (size_t)row * stride * D;
   const float* __restrict__ pml = p.part_ml + (size_t)row * stride * 4;
+  // the group record and the first chunk's partials are independent: both requests go out
+  // before either is used, the vector loads first (the compiler waits for a conditional block's
+  // scalar loads at its end; round 3 paid the group lookup as a trip ahead of the partials)
+  float4_ mlv[SPL], ov[SPL];
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    const int s = min(sl + j * nsl, nmax - 1);
+    mlv[j] = *reinterpret_cast<const float4_*>(pml + (size_t)s * 4);
+    ov[j] = *reinterpret_cast<const float4_*>(po + (size_t)s * D + d0);
+  }
+  int b0 = 0, nn = 1, sh = 0;
+  if (p.groups != nullptr) {
+    b0 = p.groups[3 * b];
+    nn = p.groups[3 * b + 1];
+    sh = p.groups[3 * b + 2];
+  }
+  int n = 1;
+  if (p.groups != nullptr && !(nn < 1 || nn * G > 16 || b0 < 0 || b < b0 || b - b0 >= nn || sh < 0))
+    n = nn;                                    // as attn_item
+  const int nslots = n * p.num_splits;
+  if (nslots == 1) return;                     // written directly by the attention launch
   float M = -INFINITY, L = 0.f;
   float4_ O = {0.f, 0.f, 0.f, 0.f};
   auto merge = [&](float m2, float l2, float4_ o2) {
@@ -54,10 +72,12 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
     L = L * a + f * l2;
     M = Mc;
   };
-  // chunks of SPL x NSL slots (one chunk at the launch's sizing; more only for rows with more
-  // slots than the host sized for, e.g. wide groups of a small-head model)
-  for (int base = 0; base < nslots; base += SPL * nsl) {
-    float4_ mlv[SPL], ov[SPL];
+#pragma unroll
+  for (int j = 0; j < SPL; ++j)
+    if (sl + j * nsl < nslots) merge(mlv[j][0], mlv[j][1], ov[j]);
+  // more chunks only for rows with more slots than the host sized for (not reached when the
+  // group record is well-formed: n * G <= 16)
+  for (int base = SPL * nsl; base < nslots; base += SPL * nsl) {
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {            // every load of the chunk in flight before any merge
       const int s = min(base + sl + j * nsl, nslots - 1);
@@ -69,13 +89,12 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
       if (base + sl + j * nsl < nslots) merge(mlv[j][0], mlv[j][1], ov[j]);
   }
   // the 8 slot-lanes of a wave (lane bits 3..5), then the waves through LDS; fixed order
-#pragma unroll
-  for (int x = 8; x < 64; x <<= 1) {
+  auto xmerge = [&](int x, bool upper) {
     const float m2 = __shfl_xor(M, x, 64), l2 = __shfl_xor(L, x, 64);
     float4_ o2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) o2[i] = __shfl_xor(O[i], x, 64);
-    if (sl & (x >> 3)) {   // the upper partner takes the lower's state first: same order on both
+    if (upper) {   // the upper partner takes the lower's state first: same order on both
       const float mm = M, ll = L;
       const float4_ oo = O;
       M = m2; L = l2; O = o2;
@@ -83,7 +102,9 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
     } else {
       merge(m2, l2, o2);
     }
-  }
+  };
+#pragma unroll
+  for (int x = 8; x < 64; x <<= 1) xmerge(x, sl & (x >> 3));
   __shared__ float red[16][8][6];
   const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   if ((threadIdx.x & 63) < 8) {
@@ -91,13 +112,25 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
     e[0] = O[0]; e[1] = O[1]; e[2] = O[2]; e[3] = O[3]; e[4] = M; e[5] = L;
   }
   __syncthreads();
-  if (threadIdx.x < 8) {
-    for (int w = 1; w < nwaves; ++w) {
+  // the waves' states as a tree on the first wave: lane (w, dl) of 8 groups takes waves w and
+  // w + 8, then three xor steps — 4 dependent merges instead of nwaves - 1
+  if (threadIdx.x < 64) {
+    const int w = threadIdx.x >> 3;
+    M = -INFINITY; L = 0.f; O = float4_{0.f, 0.f, 0.f, 0.f};
+    if (w < nwaves) {
       const float* e = red[w][dl];
       merge(e[4], e[5], float4_{e[0], e[1], e[2], e[3]});
     }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    store_bf16x4(p.out + (size_t)row * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, false);
+    if (w + 8 < nwaves) {
+      const float* e = red[w + 8][dl];
+      merge(e[4], e[5], float4_{e[0], e[1], e[2], e[3]});
+    }
+#pragma unroll
+    for (int x = 8; x < 64; x <<= 1) xmerge(x, w & (x >> 3));
+    if (w == 0) {
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      store_bf16x4(p.out + (size_t)row * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, false);
+    }
   }
 }
 }  // namespace

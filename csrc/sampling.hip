@@ -48,7 +48,20 @@ constexpr int W_KB = W_CNT + 4;          // [C] chunk's top histogram bin floor(
 constexpr int HB = 128;                  // histogram bins per chunk (the last one: everything lower)
 constexpr float BW = 16.f;               // bins per unit of z = logit / T
 constexpr int W_HIST = W_KB + C;         // [C][HB] chunk mass per bin, relative to the chunk max
-constexpr int W_ROW = W_HIST + C * HB;   // words per row; after the B rows: the rows-done ticket
+// top-k rows with k <= KMAX: every chunk publishes its own top-k tokens (ties at its k-th key
+// included up to LCAP), sorted by token id; the decider merges the C lists
+constexpr int KMAX = 64;
+constexpr int LCAP = 96;
+constexpr int W_TKN = W_HIST + C * HB;   // [C] list length | truncated << 16 (int)
+constexpr int W_TKK = W_TKN + C;         // [C] the chunk's k-th largest order key (int)
+constexpr int W_TKL = W_TKK + C;         // [C][LCAP] order keys (int)
+constexpr int W_TKI = W_TKL + C * LCAP;  // [C][LCAP] token ids (int)
+constexpr int W_ROW = W_TKI + C * LCAP;  // words per row; after the B rows: the rows-done ticket
+// LDS pool: the decider's histograms (hc, hm, hci, hmi) or, on top-k list rows, the chunk's
+// order keys (phase 1) / the merged lists (decider)
+constexpr int POOL_BYTES = NB * 4 * 3 + NB * 8;
+constexpr int POOLK = POOL_BYTES / 4;
+constexpr int NALLOW = NT;               // list path: at most this many allowed tokens (else the histogram path)
 
 RT_DEVICE uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -150,6 +163,60 @@ RT_DEVICE void chunk_range(int V, int c, int& lo, int& hi) {
   const int per = ((V + C - 1) / C + 7) & ~7;
   lo = min(V, c * per);
   hi = min(V, lo + per);
+}
+
+// order-preserving unsigned key of a float (larger value -> larger key; -inf > 0 = "no entry")
+RT_DEVICE uint32_t okey(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+RT_DEVICE float okey_value(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// The largest t with #{i < n : keys[i] >= t} >= need (the need-th largest key; need <= n), two
+// bits per step, down to bit lo (16 for bf16 values: their keys' low half carries no order).
+// Counts are wave ballots (a compare + a scalar popcount per key, no shuffles), one barrier per
+// step (scr: 2 x 3 x NWV ints, alternating so a step never overwrites what a slower wave reads).
+RT_DEVICE uint32_t kth_key(const uint32_t* keys, int n, int need, int lo, int* scr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t t = 0;
+  int par = 0;
+  for (int bit = 30; bit >= lo; bit -= 2, par ^= 1) {
+    const uint32_t c1 = t | (1u << bit), c2 = t | (2u << bit), c3 = t | (3u << bit);
+    int n1 = 0, n2 = 0, n3 = 0;
+    for (int i0 = 0; i0 < n; i0 += 8 * NT) {
+      uint32_t kk[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + (int)threadIdx.x + j * NT;
+        kk[j] = i < n ? keys[i] : 0u;     // 0: below every value's key
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        n1 += __popcll(__ballot(kk[j] >= c1));
+        n2 += __popcll(__ballot(kk[j] >= c2));
+        n3 += __popcll(__ballot(kk[j] >= c3));
+      }
+    }
+    int* sc = scr + par * 3 * NWV;
+    if (lane == 0) {
+      sc[wid] = n1;
+      sc[NWV + wid] = n2;
+      sc[2 * NWV + wid] = n3;
+    }
+    __syncthreads();
+    n1 = n2 = n3 = 0;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      n1 += sc[w];
+      n2 += sc[NWV + w];
+      n3 += sc[2 * NWV + w];
+    }
+    t = n3 >= need ? c3 : (n2 >= need ? c2 : (n1 >= need ? c1 : t));
+  }
+  __syncthreads();   // the caller may rewrite keys / scr
+  return t;
 }
 
 // First bin whose inclusive prefix of `a` reaches ta or of `bm` reaches tb (NT threads, NB/NT
@@ -347,12 +414,20 @@ struct SampleArgs {
 
 template <typename T, bool VEC>
 __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
-  __shared__ float hc[NB], hm[NB];
+  __shared__ __attribute__((aligned(16))) unsigned char pool[POOL_BYTES];
+  float* hc = reinterpret_cast<float*>(pool);
+  float* hm = hc + NB;
   // histogram accumulators: INTEGER LDS atomics (count, and mass in 32.32 fixed point) — LDS
   // float atomic adds serialize per lane on gfx950 (r03 probe: a 128K-token coarse pass took
   // 320 us on one workgroup), the integer ones do not
-  __shared__ unsigned hci[NB];
-  __shared__ unsigned long long hmi[NB];
+  unsigned* hci = reinterpret_cast<unsigned*>(hm + NB);
+  unsigned long long* hmi = reinterpret_cast<unsigned long long*>(hci + NB);
+  uint32_t* okeys = reinterpret_cast<uint32_t*>(pool);
+  __shared__ int s_cnt3[2 * 3 * NWV], s_ln, s_lt;
+  __shared__ uint32_t s_tk[LCAP];
+  __shared__ int s_ti[LCAP];
+  __shared__ uint32_t s_lk[LCAP];
+  __shared__ int s_li[LCAP];
   __shared__ float sv[NWV], red[2 * NWV + 2];
   __shared__ int si[NWV];
   __shared__ float s_max[C], s_gv[C], s_min[C];
@@ -416,6 +491,10 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   // without another pass over the row for all but the rows whose j* shares a bin with the cut
   const bool hist = temp > 0.f && p < 1.f && !use_k;
   const float sbin = sgrid > 0.f ? sgrid : invT * BW;
+  // top-k rows with a small k: chunk top-k lists (the decider needs no pass over the row)
+  const int per = ((V + C - 1) / C + 7) & ~7;
+  const bool lst = temp > 0.f && use_k && k <= KMAX && per <= POOLK && a.probe == 0;
+  constexpr int KLO = sizeof(T) == 2 ? 16 : 0;
 
   // ---- 1: chunk records ----
   ArgMax am{-INFINITY, 0x7fffffff}, gb{-INFINITY, 0x7fffffff};
@@ -425,6 +504,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
       am_merge(am, v, i);
       mn = fminf(mn, v);
       am_merge(gb, v * invT + gumbel(key, (uint32_t)i), i);
+      if (lst) okeys[i - lo] = okey(v);
     });
     gb = block_argmax(gb, sv, si);
     mn = -rt::block_max(-mn, red);
@@ -458,6 +538,66 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();   // every thread's histogram stores complete before thread 0's ticket
   }
+  if (lst) {
+    // this chunk's k-th largest key Kc; list = every token above it, then its ties up to LCAP,
+    // published sorted by token id (the atomic slot order is not deterministic)
+    const int n = hi - lo;
+    const int need = min(k, n);
+    uint32_t kc = 0;
+    if (need > 0) kc = kth_key(okeys, n, need, KLO, s_cnt3);
+    if (threadIdx.x == 0) s_ln = s_lt = 0;
+    __syncthreads();
+    if (need > 0) {   // one pass: keys above kc (fewer than need <= KMAX < LCAP) and ties apart
+      for (int i0 = 0; i0 < n; i0 += 8 * NT) {
+        uint32_t kk[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = i0 + (int)threadIdx.x + j * NT;
+          kk[j] = i < n ? okeys[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = i0 + (int)threadIdx.x + j * NT;
+          if (kk[j] > kc) {
+            const int sl = atomicAdd(&s_ln, 1);
+            s_lk[sl] = kk[j];
+            s_li[sl] = lo + i;
+          } else if (kk[j] == kc && i < n) {
+            const int sl = atomicAdd(&s_lt, 1);
+            if (sl < LCAP) {
+              s_tk[sl] = kk[j];
+              s_ti[sl] = lo + i;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int g = s_ln;
+      for (int q = threadIdx.x; q < min(s_lt, LCAP - g); q += NT) {
+        s_lk[g + q] = s_tk[q];
+        s_li[g + q] = s_ti[q];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) s_ln = g + s_lt;
+    }
+    __syncthreads();
+    const int len = min(s_ln, LCAP);
+    if ((int)threadIdx.x < len) {
+      const int mi = s_li[threadIdx.x];
+      int r = 0;
+      for (int j = 0; j < len; ++j) r += s_li[j] < mi;
+      __hip_atomic_store(&wi[W_TKL + c * LCAP + r], (int)s_lk[threadIdx.x], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&wi[W_TKI + c * LCAP + r], mi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&wi[W_TKN + c], len | (s_ln > LCAP ? 1 << 16 : 0), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&wi[W_TKK + c], (int)kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every thread's list stores complete before thread 0's ticket
+  }
   if (threadIdx.x == 0) {
     __hip_atomic_store(&w[W_MIN + c], mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&w[W_MAX + c], am.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -489,6 +629,33 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
 #pragma unroll
     for (int q = 0; q < C * HB / NT; ++q)
       hv[q] = __hip_atomic_load(&w[W_HIST + threadIdx.x + q * NT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // top-k list rows: the C lists (6 + 6 words per thread) in the same round trip
+  __shared__ int s_tkn[C], s_tkk[C], s_ccnt[C], s_fb;
+  uint32_t* lk = okeys;                                   // [C][LCAP] merged lists
+  int* li = reinterpret_cast<int*>(okeys + C * LCAP);
+  uint32_t* ak = okeys + 2 * C * LCAP;                    // [NALLOW] allowed tokens, id order
+  int* ai = reinterpret_cast<int*>(ak + NALLOW);
+  float* aw = reinterpret_cast<float*>(ai + NALLOW);
+  constexpr int LQ = C * LCAP / NT;
+  if (lst) {
+    int lkr[LQ], lir[LQ];
+    if (threadIdx.x < C) {
+      s_tkn[threadIdx.x] = __hip_atomic_load(&wi[W_TKN + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_tkk[threadIdx.x] = __hip_atomic_load(&wi[W_TKK + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+      lkr[q] = __hip_atomic_load(&wi[W_TKL + threadIdx.x + q * NT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lir[q] = __hip_atomic_load(&wi[W_TKI + threadIdx.x + q * NT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {   // entries past a chunk's length: key 0 (below every value's key)
+      const int e = threadIdx.x + q * NT, cc = e / LCAP;
+      lk[e] = e - cc * LCAP < (s_tkn[cc] & 0xffff) ? (uint32_t)lkr[q] : 0u;
+      li[e] = lir[q];
+    }
   }
   __syncthreads();
   ArgMax ra{-INFINITY, 0x7fffffff}, g{-INFINITY, 0x7fffffff};
@@ -615,6 +782,79 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
         if (cand < 0)
           cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, pz, vj, key, s_gv, s_gi, sv, si, red);
       }
+    }
+    if (lst) {
+      // top-k from the chunk lists: the union holds every chunk's top k, so its k-th largest key
+      // is the row's; every allowed token (key >= kg) is listed unless a chunk dropped ties AT kg
+      const uint32_t kg = kth_key(lk, C * LCAP, k, KLO, s_cnt3);
+      if (threadIdx.x == 0) s_fb = 0;
+      __syncthreads();
+      if (threadIdx.x < C && (s_tkn[threadIdx.x] >> 16) && (uint32_t)s_tkk[threadIdx.x] == kg) s_fb = 1;
+      __syncthreads();
+      if (!s_fb && !(p < 1.f)) {
+        ArgMax r{-INFINITY, 0x7fffffff};
+        for (int e = threadIdx.x; e < C * LCAP; e += NT) {
+          const uint32_t kk = lk[e];
+          if (kk >= kg) am_merge(r, (okey_value(kk) - mx) * invT + gumbel(key, (uint32_t)li[e]), li[e]);
+        }
+        r = block_argmax(r, sv, si);
+        cand = r.i != 0x7fffffff ? r.i : -1;
+      } else if (!s_fb) {
+        // top-p inside the top-k set: compact the allowed tokens in id order (lists are sorted by
+        // id, chunks in id order; each wave ranks 4 chunks with ballots), then the exact test —
+        // mass strictly above a token < p * allowed mass — and the Gumbel argmax over the nucleus
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        constexpr int CPW = C / NWV, RPC = (LCAP + 63) / 64;
+        int pos[CPW][RPC];
+#pragma unroll
+        for (int q = 0; q < CPW; ++q) {
+          const int cc = wid * CPW + q;
+          int run = 0;
+#pragma unroll
+          for (int r = 0; r < RPC; ++r) {
+            const int j = lane + 64 * r;
+            const bool al = j < LCAP && lk[cc * LCAP + j] >= kg;
+            const unsigned long long m = __ballot(al);
+            pos[q][r] = al ? run + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+            run += __popcll(m);
+          }
+          if (lane == 0) s_ccnt[cc] = run;
+        }
+        __syncthreads();
+        int tot = 0;
+        for (int j = 0; j < C; ++j) tot += s_ccnt[j];
+        if (tot <= NALLOW) {
+#pragma unroll
+          for (int q = 0; q < CPW; ++q) {
+            const int cc = wid * CPW + q;
+            int base = 0;
+            for (int j = 0; j < cc; ++j) base += s_ccnt[j];
+#pragma unroll
+            for (int r = 0; r < RPC; ++r) {
+              if (pos[q][r] >= 0) {
+                const int e = cc * LCAP + lane + 64 * r;
+                ak[base + pos[q][r]] = lk[e];
+                ai[base + pos[q][r]] = li[e];
+                aw[base + pos[q][r]] = __expf((okey_value(lk[e]) - mx) * invT);
+              }
+            }
+          }
+          __syncthreads();
+          const int t = threadIdx.x;
+          const float my_w = t < tot ? aw[t] : 0.f;
+          const float zsum = rt::block_sum(my_w, red);
+          ArgMax r{-INFINITY, 0x7fffffff};
+          if (t < tot) {
+            const uint32_t mk = ak[t];
+            float above = 0.f;
+            for (int j = 0; j < tot; ++j) above += ak[j] > mk ? aw[j] : 0.f;
+            if (above < p * zsum) am_merge(r, (okey_value(mk) - mx) * invT + gumbel(key, (uint32_t)ai[t]), ai[t]);
+          }
+          r = block_argmax(r, sv, si);
+          cand = r.i != 0x7fffffff ? r.i : -1;
+        }
+      }
+      __syncthreads();   // the histogram path below reuses the pool
     }
     if (accepted || cand >= 0 || a.probe == 1) {
       tok = accepted ? g.i : (cand >= 0 ? cand : ra.i);

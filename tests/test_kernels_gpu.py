@@ -331,6 +331,34 @@ def test_sample_rejection_paths_match_reference():
     assert hits >= total - 2, (hits, total)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_sample_topk_lists_match_reference(dtype):
+    """Top-k rows with k <= 64 (csrc/sampling.hip: every chunk publishes its own top k, the
+    decider merges the lists — no pass over the row), alone and with top-p inside the top-k set,
+    on bf16 (16-bit order keys) and fp32 logits; a tie-heavy row (quantised logits: chunks drop
+    ties at the cut, so the histogram path decides) and a near-flat row. Draw for draw against
+    the fp64 reference."""
+    B, V = 8, 128256
+    logits = bf(B, V, scale=2.0, seed=123).float()
+    logits[1] *= 0.05
+    logits[2] = torch.round(logits[2] * 2) / 2
+    logits = logits.to(dtype)
+    temp = torch.full((B,), 0.8, device=DEV)
+    top_k = torch.tensor([1, 5, 40, 64, 40, 64, 2, 17], dtype=torch.int32, device=DEV)
+    top_p = torch.tensor([1.0, 1.0, 1.0, 0.9, 0.5, 1.0, 0.7, 0.95], device=DEV)
+    ws = ops.sample_workspace(B, DEV)
+    hits = total = 0
+    for rep in range(6):
+        seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 7907 + rep
+        offs = torch.arange(B, dtype=torch.int64, device=DEV) + 333 * rep
+        got = ops.sample(logits, temp, top_p, top_k, seeds, offs, ws=ws).cpu()
+        exp = ref.sample(logits.cpu(), temp.cpu(), top_p.cpu(), top_k.cpu(), seeds.cpu(), offs.cpu())
+        hits += int((got == exp).sum())
+        total += B
+        assert torch.equal(got, ops.sample(logits, temp, top_p, top_k, seeds, offs, ws=ws).cpu())
+    assert hits >= total - 2, (hits, total)
+
+
 def test_sample_top_p_nucleus():
     V = 1000
     logits = torch.full((1, V), -10.0, device=DEV)

@@ -16,7 +16,7 @@ for V in (32000, 128256):
     s=torch.arange(B,device=DEV); o=torch.zeros(B,dtype=torch.int64,device=DEV)
     T=torch.full((B,),0.8,device=DEV); one=torch.ones(B,device=DEV); k0=torch.zeros(B,dtype=torch.int32,device=DEV)
     for name,(temp,p,k) in {'greedy':(T*0,one,k0),'unfilt':(T,one,k0),'topp.9':(T,one*0.9,k0),'topp.3':(T,one*0.3,k0),
-                            'topk40':(T,one,k0+40),'topk4000':(T,one,k0+4000)}.items():
+                            'topk40':(T,one,k0+40),'topk40p.9':(T,one*0.9,k0+40),'topk64':(T,one,k0+64),'topk4000':(T,one,k0+4000)}.items():
         print(V,B,name, round(t(lambda: ops.sample(lg,temp,p,k,s,o,out,ws=ws)),1))
 # per-row view of the B=3 top-p launches (fixed seeds: each row takes the same path every call)
 V = 128256
