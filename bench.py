@@ -397,6 +397,9 @@ def _run(args, failsafe) -> int:
                    "k9_us": getattr(getattr(engine.tp, "oneshot", None), "latency_us", None),
                    "k9_fused_gemm_ar": bool(getattr(getattr(engine.tp, "oneshot", None), "fused", False)),
                    "k9_fused_saving_us": getattr(getattr(engine.tp, "oneshot", None), "fused_saving_us", None),
+                   "k9_ll": getattr(getattr(engine.tp, "oneshot", None), "ll", None),
+                   "k9_flag_us": getattr(getattr(engine.tp, "oneshot", None), "flag_latency_us", None),
+                   "k9_ll_us": getattr(getattr(engine.tp, "oneshot", None), "ll_latency_us", None),
                    "k9_gather": bool(getattr(getattr(engine.tp, "oneshot", None), "gather_ok", False)),
                    "k9_gather_saving_us": getattr(getattr(engine.tp, "oneshot", None), "gather_saving_us", None),
                    "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,

@@ -63,6 +63,7 @@ int oneshot_handle_bytes();
 int oneshot_error(int id);
 int oneshot_clear_error(int id);
 int oneshot_set_poll_limit(int id, long long limit);
+int oneshot_set_ll(int id, int on);
 void oneshot_destroy(int id);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
@@ -626,6 +627,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("oneshot_error", [](int64_t id) { return oneshot_error((int)id); });
   m.def("oneshot_clear_error", [](int64_t id) { return oneshot_clear_error((int)id); });
   m.def("oneshot_set_poll_limit", [](int64_t id, int64_t limit) { return oneshot_set_poll_limit((int)id, limit); });
+  m.def("oneshot_set_ll", [](int64_t id, bool on) { return oneshot_set_ll((int)id, on ? 1 : 0); });
   m.def("oneshot_destroy", [](int64_t id) { oneshot_destroy((int)id); });
   m.def("decode_advance", &decode_advance, py::arg("out"), py::arg("ids"), py::arg("positions"), py::arg("ctx_lens"),
         py::arg("step"), py::arg("next"), py::arg("slots") = py::none(), py::arg("offsets") = py::none(),

@@ -17,6 +17,13 @@
 // the launch is hipGraph-capturable and replays with no host involvement.
 // Every flag wait is bounded: on expiry *err is set and the kernel proceeds (never a hang).
 //
+// LL form (oneshot_ar_ll_kernel, chosen per node by a timed probe, parallel/oneshot.py): every
+// 4-byte word of the slice travels with the call's epoch in ONE 8-byte store ((data, epoch)
+// pairs), so a receiver polls the data itself. The flag form pays, after its pushes, a system
+// fence (every remote store acknowledged: an xGMI round trip), then the flag's one-way trip,
+// then a local read of the data; the LL form pays the data's one-way trip only, for twice the
+// bytes on the link (a decode all-reduce is 24 KB: ~0.5 us more at ~50 GB/s per link).
+//
 // The same comm also serves the FUSED form (skinny_gemm_ar_kernel below, epilogue EPI_AR of
 // skinny_core.h): a row-parallel decode GEMM (o / down projection) exchanges each finished
 // 16-column tile itself — push, per-(peer, tile) flag, wait, rank-order sum — so the decode step
@@ -36,7 +43,7 @@ constexpr int MAXB = 64;   // workgroups per call (flags per (slot, source rank)
 constexpr long long FLAG_POLL_LIMIT = 1ll << 26;   // default bound (~seconds); tests lower it per comm
 constexpr int MAXT = 1024; // 16-column tiles per fused call (N <= 16384)
 constexpr int GCAP = 16 * 131072;   // all-gather output elements per slot (16 rows x a 128K vocab)
-constexpr int NHANDLES = 5;         // IPC handles per rank: data, flags, tile flags, gather data, gather flags
+constexpr int NHANDLES = 6;         // IPC handles per rank: data, flags, tile flags, gather data, gather flags, LL
 static_assert(MAXW == skinny::AR_MAXW, "rank limit shared with the fused epilogue");
 
 struct Peers {
@@ -115,6 +122,100 @@ __global__ void __launch_bounds__(256) oneshot_ar_kernel(uint16_t* __restrict__ 
     reinterpret_cast<vec*>(res != nullptr ? res : inout)[v] = o;
   }
   // 5. the last workgroup out advances the call counter (every workgroup has read it)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (uint32_t)nb - 1u) {
+      __hip_atomic_store(done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(epoch_ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+struct LLPeers {
+  uint64_t* ll[MAXW];      // rank p's LL buffer: [2 slots][world][cap / 2] (data word, epoch) pairs
+};
+
+__global__ void __launch_bounds__(256) oneshot_ar_ll_kernel(uint16_t* __restrict__ inout, int n, int rank, int world,
+                                                            int cap, LLPeers P, uint32_t* epoch_ctr,
+                                                            uint32_t* done_ctr, int* err, long long poll_limit,
+                                                            uint16_t* __restrict__ res) {
+  const uint32_t epoch = __hip_atomic_load(epoch_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int slot = (int)(epoch & 1u);
+  const int nb = gridDim.x, blk = blockIdx.x;
+  const int nvec = n >> 3;                              // 16-byte vectors (4 pairs each)
+  const int per = (nvec + nb - 1) / nb;
+  const int v0 = blk * per, v1 = min(nvec, v0 + per);
+  const size_t rstride = (size_t)cap / 2;               // pairs per (slot, source rank)
+  const uint64_t tag = (uint64_t)epoch << 32;
+  // 1. push: four 8-byte (word, epoch) stores per vector into every rank's buffer (own included)
+  for (int v = v0 + (int)threadIdx.x; v < v1; v += blockDim.x) {
+    const uint4 x = reinterpret_cast<const uint4*>(inout)[v];
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    for (int p = 0; p < world; ++p) {
+      uint64_t* dst = P.ll[p] + ((size_t)slot * world + rank) * rstride + 4 * (size_t)v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_store(dst + j, tag | w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // 2. receive: every rank's 4 pairs of the vector requested at once, re-polled until each
+  // carries this call's epoch (bounded), then summed in rank order (bit-identical on every rank)
+  const uint64_t* mine = P.ll[rank] + (size_t)slot * world * rstride;
+  for (int v = v0 + (int)threadIdx.x; v < v1; v += blockDim.x) {
+    uint64_t q[MAXW][4];
+#pragma unroll
+    for (int r = 0; r < MAXW; ++r)
+      if (r < world)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          q[r][j] = __hip_atomic_load(mine + (size_t)r * rstride + 4 * (size_t)v + j, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int r = 0; r < MAXW; ++r) {
+      if (r >= world) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        long long it = 0;
+        while ((uint32_t)(q[r][j] >> 32) != epoch) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++it > poll_limit) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          q[r][j] = __hip_atomic_load(mine + (size_t)r * rstride + 4 * (size_t)v + j, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < MAXW; ++r) {
+      if (r >= world) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t wj = (uint32_t)q[r][j];
+        acc[2 * j] += rt::bf2f((uint16_t)(wj & 0xffffu));
+        acc[2 * j + 1] += rt::bf2f((uint16_t)(wj >> 16));
+      }
+    }
+    if (res != nullptr) {
+      const uint4 rv = reinterpret_cast<const uint4*>(res)[v];
+      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] = rt::bf2f((uint16_t)(rw[j] & 0xffffu)) + rt::bf2f(rt::f2bf(acc[2 * j]));
+        acc[2 * j + 1] = rt::bf2f((uint16_t)(rw[j] >> 16)) + rt::bf2f(rt::f2bf(acc[2 * j + 1]));
+      }
+    }
+    uint4 o;
+    o.x = rt::pack2(acc[0], acc[1]);
+    o.y = rt::pack2(acc[2], acc[3]);
+    o.z = rt::pack2(acc[4], acc[5]);
+    o.w = rt::pack2(acc[6], acc[7]);
+    reinterpret_cast<uint4*>(res != nullptr ? res : inout)[v] = o;
+  }
+  // 3. the last workgroup out advances the call counter (every workgroup has read it)
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -206,6 +307,9 @@ struct Comm {
   uint32_t* ctr = nullptr;                // [epoch, done] (plain device memory, local only)
   int* err = nullptr;
   long long poll_limit = FLAG_POLL_LIMIT;
+  uint64_t* ll = nullptr;                 // own LL receive buffer
+  LLPeers llpeers{};
+  int use_ll = 0;                         // the all-reduce launch takes the LL form
   Peers peers{};
   std::vector<void*> opened;              // IPC mappings to close
 };
@@ -220,6 +324,7 @@ size_t data_bytes(const Comm& c) { return (size_t)2 * c.world * c.cap * sizeof(u
 size_t flag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXB * sizeof(uint32_t); }
 size_t tflag_bytes(const Comm& c) { return (size_t)2 * c.world * MAXT * sizeof(uint32_t); }
 size_t gdata_bytes() { return (size_t)2 * GCAP * sizeof(uint16_t); }
+size_t ll_bytes(const Comm& c) { return (size_t)2 * c.world * (c.cap / 2) * sizeof(uint64_t); }
 
 template <int NW, int U>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_ar_kernel(skinny::GemmArgs p) {
@@ -230,7 +335,7 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_ar_kernel(skinny::GemmArg
 }  // namespace
 
 // Allocates this rank's IPC buffers. Returns a comm id (>= 0) or a negative error; the
-// NHANDLES 64-byte IPC handles (data, flags, tile flags, gather data, gather flags) are written
+// NHANDLES 64-byte IPC handles (data, flags, tile flags, gather data, gather flags, LL) are written
 // to `handles` (64 * NHANDLES bytes).
 int oneshot_create(int world, int rank, int cap_elems, char* handles) {
   if (world < 2 || world > MAXW || rank < 0 || rank >= world || cap_elems < 8 || cap_elems % 8) return -1;
@@ -244,19 +349,20 @@ int oneshot_create(int world, int rank, int cap_elems, char* handles) {
       hipExtMallocWithFlags((void**)&c->tflags, tflag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void**)&c->gdata, gdata_bytes(), hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void**)&c->gflags, flag_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags((void**)&c->ll, ll_bytes(*c), hipDeviceMallocUncached) != hipSuccess ||
       hipMalloc((void**)&c->ctr, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc((void**)&c->err, sizeof(int)) != hipSuccess) {
     delete c;
     return -3;
   }
   if (hipMemset(c->flags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->tflags, 0, tflag_bytes(*c)) != hipSuccess ||
-      hipMemset(c->gflags, 0, flag_bytes(*c)) != hipSuccess ||
+      hipMemset(c->gflags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->ll, 0, ll_bytes(*c)) != hipSuccess ||
       hipMemset(c->ctr, 0, 2 * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(c->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     delete c;
     return -4;
   }
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
-  void* const bufs[NHANDLES] = {c->data, c->flags, c->tflags, c->gdata, c->gflags};
+  void* const bufs[NHANDLES] = {c->data, c->flags, c->tflags, c->gdata, c->gflags, c->ll};
   for (int i = 0; i < NHANDLES; ++i) {
     hipIpcMemHandle_t h;
     if (hipIpcGetMemHandle(&h, bufs[i]) != hipSuccess) {
@@ -275,7 +381,7 @@ int oneshot_open(int id, const char* all_handles) {
   Comm* c = get(id);
   if (c == nullptr) return -1;
   for (int p = 0; p < c->world; ++p) {
-    void* b[NHANDLES] = {c->data, c->flags, c->tflags, c->gdata, c->gflags};
+    void* b[NHANDLES] = {c->data, c->flags, c->tflags, c->gdata, c->gflags, c->ll};
     if (p != c->rank) {
       for (int i = 0; i < NHANDLES; ++i) {
         hipIpcMemHandle_t h;
@@ -289,6 +395,7 @@ int oneshot_open(int id, const char* all_handles) {
     c->peer_tflags[p] = (uint32_t*)b[2];
     c->gpeers.data[p] = (uint16_t*)b[3];
     c->gpeers.flags[p] = (uint32_t*)b[4];
+    c->llpeers.ll[p] = (uint64_t*)b[5];
   }
   return 0;
 }
@@ -310,8 +417,14 @@ int oneshot_allreduce(int id, void* inout, int n, void* res, hipStream_t stream)
     if (c->peers.data[p] == nullptr) return -3;   // oneshot_open not called
   int nb = n / 2048;                                // ~4 KB of slice per workgroup
   nb = nb < 1 ? 1 : (nb > MAXB ? MAXB : nb);
-  hipLaunchKernelGGL(oneshot_ar_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
-                     c->cap, c->peers, c->ctr, c->ctr + 1, c->err, c->poll_limit, (uint16_t*)res);
+  if (c->use_ll) {
+    if (c->llpeers.ll[c->rank] == nullptr) return -3;
+    hipLaunchKernelGGL(oneshot_ar_ll_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
+                       c->cap, c->llpeers, c->ctr, c->ctr + 1, c->err, c->poll_limit, (uint16_t*)res);
+  } else {
+    hipLaunchKernelGGL(oneshot_ar_kernel, dim3(nb), dim3(256), 0, stream, (uint16_t*)inout, n, c->rank, c->world,
+                       c->cap, c->peers, c->ctr, c->ctr + 1, c->err, c->poll_limit, (uint16_t*)res);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
@@ -334,7 +447,9 @@ int oneshot_gemm_ar(int id, void* out, const void* x, const void* Ws, int M, int
   for (int p = 0; p < c->world; ++p) {
     args.ar.data[p] = c->peers.data[p];
     args.ar.tflags[p] = c->peer_tflags[p];
+    args.ar.ll[p] = c->llpeers.ll[p];
   }
+  args.ar.use_ll = c->use_ll;
   args.ar.ctr = c->ctr;
   args.ar.err = c->err;
   args.ar.poll_limit = c->poll_limit;
@@ -392,6 +507,15 @@ int oneshot_set_poll_limit(int id, long long limit) {
   return 0;
 }
 
+// Protocol of the all-reduce launch and of the fused GEMM form: 1 = LL (data + epoch pairs),
+// 0 = push + fence + flag. (The all-gather keeps the flag form: its payload is 4x larger.)
+int oneshot_set_ll(int id, int on) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  c->use_ll = on ? 1 : 0;
+  return 0;
+}
+
 void oneshot_destroy(int id) {
   Comm* c = nullptr;
   {
@@ -408,6 +532,7 @@ void oneshot_destroy(int id) {
   (void)hipFree(c->tflags);
   (void)hipFree(c->gdata);
   (void)hipFree(c->gflags);
+  (void)hipFree(c->ll);
   (void)hipFree(c->ctr);
   (void)hipFree(c->err);
   delete c;

@@ -50,10 +50,12 @@ constexpr int AR_MAXW = 8;
 struct ArEpi {
   uint16_t* data[AR_MAXW];
   uint32_t* tflags[AR_MAXW];
+  uint64_t* ll[AR_MAXW];     // LL form: every rank's (data word, epoch) pair buffer
   uint32_t* ctr;
   int* err;
   long long poll_limit;
   int rank, world, cap, maxt;
+  int use_ll;                // 1: exchange in the LL form (oneshot_ar.hip header), 0: push + fence + flag
 };
 
 struct GemmArgs {
@@ -380,8 +382,63 @@ RT_DEVICE void ar_exchange(const GemmArgs& p, int tile, float v, int m, int n, b
   const uint16_t mine = rt::f2bf(v);
   if (live) stage[m * 16 + n] = mine;
   __syncthreads();
-  // 1. push: row m of the tile = 32 B = two 16-B stores per destination rank
   const int t = threadIdx.x;
+  if (ar.use_ll) {
+    // LL form: each 2-column word of the tile travels with the epoch in one 8-byte store; the
+    // receiver polls its rank's pairs directly (no fence, no tile flag)
+    const size_t rs = (size_t)ar.cap / 2;
+    const uint64_t tag = (uint64_t)epoch << 32;
+    for (int q = t; q < 8 * M * ar.world; q += blockDim.x) {
+      const int dst = q / (8 * M), rem = q - dst * 8 * M, row = rem >> 3, c2 = rem & 7;
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(stage + row * 16 + 2 * c2);
+      uint64_t* d = ar.ll[dst] + ((size_t)slot * ar.world + ar.rank) * rs + ((size_t)row * N + tile * 16) / 2 + c2;
+      __hip_atomic_store(d, tag | w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (live) {
+      const uint64_t* own = ar.ll[ar.rank] + (size_t)slot * ar.world * rs + ((size_t)m * N + tile * 16) / 2 + (n >> 1);
+      uint64_t q[AR_MAXW];
+#pragma unroll
+      for (int r = 0; r < AR_MAXW; ++r)
+        if (r < ar.world && r != ar.rank)
+          q[r] = __hip_atomic_load(own + (size_t)r * rs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      float acc = 0.f;
+#pragma unroll
+      for (int r = 0; r < AR_MAXW; ++r) {
+        if (r >= ar.world) continue;
+        if (r == ar.rank) {
+          acc += rt::bf2f(mine);
+          continue;
+        }
+        long long it = 0;
+        while ((uint32_t)(q[r] >> 32) != epoch) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++it > ar.poll_limit) {
+            __hip_atomic_store(ar.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          q[r] = __hip_atomic_load(own + (size_t)r * rs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        const uint32_t w = (uint32_t)q[r];
+        acc += rt::bf2f((uint16_t)((n & 1) ? (w >> 16) : (w & 0xffffu)));
+      }
+      if (p.res != nullptr) {
+        uint16_t* rp = p.res + (size_t)m * N + tile * 16 + n;
+        *rp = rt::f2bf(rt::bf2f(*rp) + rt::bf2f(rt::f2bf(acc)));
+      } else {
+        p.out[(size_t)m * p.ldo + tile * 16 + n] = rt::f2bf(acc);
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(ar.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1u) {
+        __hip_atomic_store(ar.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ar.ctr, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
+  // 1. push: row m of the tile = 32 B = two 16-B stores per destination rank
   if (t < 2 * M * ar.world) {
     const int dst = t / (2 * M), rem = t - dst * 2 * M, row = rem >> 1, half = rem & 1;
     const uint4 val = *reinterpret_cast<const uint4*>(stage + row * 16 + half * 8);

@@ -26,10 +26,13 @@ def test_oneshot_allreduce_ranks_on_one_gpu(world, fused_mode):
     assert len(recs) == 1, r.stdout[-2000:]
     ranks = recs[0]["ranks"]
     assert sorted(o["rank"] for o in ranks) == list(range(world))
-    # 6 eager sizes + 2 residual-form calls (+1 fused residual form when fused) + 15 graph replays
-    # + 3 gather replays
-    assert all(o["checks"] == 6 + 2 + int(o["fused_gemm_ar"]) + 15 + 3 and o["gather_ok"] is True
+    # (6 eager sizes + 2 residual-form calls + 1 fused check when fused) x both protocols (LL and
+    # push + fence + flag) + 15 graph replays + 3 gather replays
+    assert all(o["checks"] == 2 * (6 + 2 + int(o["fused_gemm_ar"])) + 15 + 3 and o["gather_ok"] is True
                for o in ranks), ranks
+    # the protocol choice: both forms passed the self-test and were timed; identical on every rank
+    assert len({(o["ll"], o["flag_latency_us"], o["ll_latency_us"]) for o in ranks}) == 1, ranks
+    assert all(o["flag_latency_us"] > 0 and o["ll_latency_us"] > 0 for o in ranks), ranks
     assert all(o.get("fused_residual_checked", False) == o["fused_gemm_ar"] for o in ranks), ranks
     # creation ran the exact self-tests: K9 values over both slots, then the fused GEMM + exchange
     # (EPI_AR) bit-identical to GEMM + K9 at three shard shapes

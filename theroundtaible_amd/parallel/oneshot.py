@@ -17,6 +17,10 @@ with GEMM + K9 on this node's links, and by default only when every rank owns it
 (:func:`fused_mode_env`) and when a timed probe on the node shows it beating GEMM + K9 (on one
 GPU shared by two rehearsal ranks it loses by ~46 µs: the two processes' spinning grids
 co-schedule badly); ``ROUNDTABLE_FUSED_AR=0`` keeps the separate launches.
+
+LL protocol (:func:`choose_protocol`): the standalone all-reduce can carry the call's epoch in
+every 8-byte store next to the data, so receivers poll the data itself — no system fence (an
+xGMI round trip) and no separate flag. Chosen per node by an exact self-test and a timed probe.
 """
 from __future__ import annotations
 
@@ -39,6 +43,14 @@ def fused_mode_env() -> str:
     the auto decision in rehearsals), ``1`` (forced, also on a shared GPU: the 2-rank numerics
     rehearsal), ``0`` (never)."""
     return os.environ.get("ROUNDTABLE_FUSED_AR", "auto")
+
+
+def ll_mode_env() -> str:
+    """``ROUNDTABLE_K9_LL``: protocol of the standalone all-reduce launch. ``auto`` (default): the
+    LL form (data + epoch in one 8-byte store, no fence) after its exact self-test, when the timed
+    probe on this node's links shows it faster than push + fence + flag; ``1``: LL after a passing
+    self-test; ``0``: push + fence + flag only."""
+    return os.environ.get("ROUNDTABLE_K9_LL", "auto")
 
 
 def _device_key() -> str:
@@ -67,6 +79,14 @@ class OneShotAllReduce:
         self.distinct_gpus = False                  # every rank of the group on its own device
         self.gather_ok = False                      # one-shot all-gather passed its self-test
         self.gather_saving_us: Optional[float] = None
+        self.ll = False                             # standalone all-reduce in the LL form
+        self.flag_latency_us: Optional[float] = None
+        self.ll_latency_us: Optional[float] = None
+
+    def set_ll(self, on: bool) -> None:
+        if self._nat.oneshot_set_ll(self.id, bool(on)) != 0:
+            raise RuntimeError("oneshot_set_ll failed")
+        self.ll = bool(on)
 
     def accepts_gemm(self, x: torch.Tensor, Ws: torch.Tensor) -> bool:
         """The fused row-parallel GEMM + all-reduce takes this decode shape."""
@@ -189,7 +209,8 @@ def try_create(group, rank: int, world: int, cap_elems: int = DEFAULT_CAP_ELEMS)
     if not all(verdicts):
         comm.close()
         return None
-    comm.latency_us = probe_latency(comm, group)
+    comm.latency_us = comm.flag_latency_us = probe_latency(comm, group)
+    choose_protocol(comm, group)
     passed = self_test_gather(comm)
     verdicts = [None] * world
     dist.all_gather_object(verdicts, passed, group=group)
@@ -223,6 +244,29 @@ def try_create(group, rank: int, world: int, cap_elems: int = DEFAULT_CAP_ELEMS)
 
 
 MIN_FUSED_SAVING_US = 0.5          # per call, at the o-projection shard shape
+MIN_LL_SAVING_US = 0.2             # per call, at the bench's all-reduce shape
+
+
+def choose_protocol(comm: OneShotAllReduce, group) -> None:
+    """Collective: the LL form replaces push + fence + flag for the standalone all-reduce when it
+    passes the same exact self-test on every rank and (``auto``) its group-max latency beats the
+    flag form's by ``MIN_LL_SAVING_US`` — identical numbers, so every rank takes the same
+    decision. The fused GEMM form and the gather keep the flag protocol."""
+    mode = ll_mode_env()
+    if mode == "0":
+        return
+    comm.set_ll(True)
+    passed = self_test(comm)
+    verdicts = [None] * comm.world
+    dist.all_gather_object(verdicts, passed, group=group)
+    if not all(verdicts):
+        comm.set_ll(False)
+        return
+    comm.ll_latency_us = probe_latency(comm, group)
+    use = mode == "1" or comm.ll_latency_us <= comm.flag_latency_us - MIN_LL_SAVING_US
+    comm.set_ll(use)
+    comm.latency_us = comm.ll_latency_us if use else comm.flag_latency_us
+
 SELF_TEST_POLL_LIMIT = 1 << 20      # ~1 s of flag polling: a dead link fails fast, not in minutes
 
 

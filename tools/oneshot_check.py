@@ -44,38 +44,52 @@ def main() -> int:
     torch.cuda.set_device(dev)
     backend = "nccl" if ndev >= world and os.environ.get("ROUNDTABLE_DIST_BACKEND") != "gloo" else "gloo"
     dist.init_process_group(backend, rank=rank, world_size=world)
+    from theroundtaible_amd import ops
     from theroundtaible_amd.parallel.oneshot import try_create
     ar = try_create(dist.group.WORLD, rank, world)
     assert ar is not None, "one-shot all-reduce could not be set up"
     out = {"rank": rank, "world": world, "backend": backend, "checks": 0, "self_test_latency_us": ar.latency_us,
-           "fused_gemm_ar": ar.fused, "fused_saving_us": ar.fused_saving_us}
-    for tag, n in enumerate([8, 1024, 4096, 8192, 3 * 8192, 16 * 8192]):
-        x = data(rank, n, tag, dev)
-        ar(x)
-        torch.cuda.synchronize()
-        err = (x.float().cpu() - expect(world, n, tag)).abs().max().item()
-        assert err <= 0.0625, f"n={n}: max err {err}"
-        out["checks"] += 1
-    # residual form (the tensor-parallel decode path): res = bf16(res + bf16(sum)), the input kept
-    for tag, n in ((40, 4096), (41, 3 * 4096)):
-        x = data(rank, n, tag, dev)
-        x0 = x.clone()
-        res = data(0, n, tag + 100, dev)          # the residual stream is identical on every rank
-        want = (data(0, n, tag + 100, "cpu").float() + expect(world, n, tag)).to(torch.bfloat16)
-        ar(x, res=res)
-        torch.cuda.synchronize()
-        assert torch.equal(res.cpu(), want) and torch.equal(x, x0), f"residual form n={n}"
-        out["checks"] += 1
-    if ar.fused:   # the fused GEMM + exchange with the residual add in its epilogue
-        from theroundtaible_amd.parallel.oneshot import _fused_case
-        xg, Ws = _fused_case(ar, 3, 4096, 512, 77)
-        base = data(0, 3 * 4096, 77, dev).view(3, 4096)
-        want = base.clone().add_(ar.gemm_ar(xg, Ws))
-        got = ar.gemm_ar(xg, Ws, res=base.clone())
-        torch.cuda.synchronize()
-        assert torch.equal(got, want), "fused residual form"
-        out["checks"] += 1
-        out["fused_residual_checked"] = True
+           "fused_gemm_ar": ar.fused, "fused_saving_us": ar.fused_saving_us, "ll": ar.ll,
+           "flag_latency_us": ar.flag_latency_us, "ll_latency_us": ar.ll_latency_us}
+
+    def eager_checks(base_tag: int) -> None:
+        for tag, n in enumerate([8, 1024, 4096, 8192, 3 * 8192, 16 * 8192]):
+            x = data(rank, n, base_tag + tag, dev)
+            ar(x)
+            torch.cuda.synchronize()
+            err = (x.float().cpu() - expect(world, n, base_tag + tag)).abs().max().item()
+            assert err <= 0.0625, f"n={n} ll={ar.ll}: max err {err}"
+            out["checks"] += 1
+        # residual form (the tensor-parallel decode path): res = bf16(res + bf16(sum)), input kept
+        for tag, n in ((40, 4096), (41, 3 * 4096)):
+            x = data(rank, n, base_tag + tag, dev)
+            x0 = x.clone()
+            res = data(0, n, base_tag + tag + 100, dev)   # the residual stream is identical on every rank
+            want = (data(0, n, base_tag + tag + 100, "cpu").float() + expect(world, n, base_tag + tag)).to(torch.bfloat16)
+            ar(x, res=res)
+            torch.cuda.synchronize()
+            assert torch.equal(res.cpu(), want) and torch.equal(x, x0), f"residual form n={n} ll={ar.ll}"
+            out["checks"] += 1
+        if ar.fused:   # the fused GEMM + exchange with the residual add in its epilogue
+            from theroundtaible_amd.parallel.oneshot import _fused_case
+            xg, Ws = _fused_case(ar, 3, 4096, 512, 77 + base_tag)
+            base = data(0, 3 * 4096, 77 + base_tag, dev).view(3, 4096)
+            want = base.clone().add_(ar.gemm_ar(xg, Ws))
+            sep = ops.skinny_gemm(xg, Ws, ops.PRO_PLAIN, ops.EPI_STORE)
+            ar(sep)                                   # GEMM + standalone K9 on the same inputs
+            got = ar.gemm_ar(xg, Ws, res=base.clone())
+            torch.cuda.synchronize()
+            assert torch.equal(got, want) and torch.equal(ar.gemm_ar(xg, Ws), sep), f"fused forms ll={ar.ll}"
+            out["checks"] += 1
+            out["fused_residual_checked"] = True
+
+    eager_checks(0)
+    # the protocol the node did NOT choose (LL vs push + fence + flag) runs the same checks, then
+    # the chosen one is restored — both forms are exercised on every run
+    chosen = ar.ll
+    ar.set_ll(not chosen)
+    eager_checks(1000)
+    ar.set_ll(chosen)
     # hipGraph: three calls captured, replayed; inputs refreshed in place before each replay
     n = 8192
     bufs = [torch.empty(n, dtype=torch.bfloat16, device=dev) for _ in range(3)]
@@ -123,20 +137,23 @@ def main() -> int:
             out["checks"] += 1
         assert ar.error() == 0, "a flag poll expired (gather)"
     if a.bench:
-        for n in (8192, 16 * 8192):
-            x = data(rank, n, 7, dev)
-            gg = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(gg, stream=s):
-                    for _ in range(20):
-                        ar(x)
-            dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(10):
-                gg.replay()
-            torch.cuda.synchronize()
-            out[f"oneshot_us_n{n}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+        for ll in (False, True):
+            ar.set_ll(ll)
+            for n in (3 * 4096, 8192, 16 * 8192):
+                x = data(rank, n, 7, dev)
+                gg = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(gg, stream=s):
+                        for _ in range(20):
+                            ar(x)
+                dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(10):
+                    gg.replay()
+                torch.cuda.synchronize()
+                out[f"oneshot_{'ll' if ll else 'flag'}_us_n{n}"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+        ar.set_ll(chosen)
         if ar.gather_ok:
             sl = data(rank, 3 * 16032, 8, dev).view(3, 16032)
             gg = torch.cuda.CUDAGraph()
