@@ -479,6 +479,10 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   const float sgrid = __hip_atomic_load(&w[W_SC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int k = a.top_k[b];
   const float p = a.top_p[b];
+  // the decider's step bookkeeping inputs come with the parameters (row b's decider is their
+  // only writer, after every ticket of the row): no dependent trip at the end of the launch
+  const int64_t pos_b = a.adv ? a.positions[b] : 0;
+  const int ctx_b = a.adv ? a.ctx_lens[b] : 0;
   // the deciders rewrite offsets / step / the grid scale: every read of them completes before
   // this workgroup's ticket (below), and the deciders write only after every ticket of their
   // row / launch (one wait for all the parameter loads)
@@ -998,28 +1002,33 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     const float sn = fminf((float)(HB - 2) / span, 1e6f / (fabsf(mx) + fabsf(rmin) + 1.f));
     __hip_atomic_store(&w[W_SC], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (threadIdx.x == 0) {
-    a.tok[b] = tok;
-    if (a.adv) {
-      if (st < a.max_steps) a.out[st * a.B + b] = tok;
-      a.ids[b] = tok;
-      const int64_t pn = a.positions[b] + 1;
-      a.positions[b] = pn;
-      a.ctx_lens[b] += 1;
-      if (a.slots != nullptr) {   // past the table (a turn's last step) the slot is never used
-        const int64_t bi = pn / a.BS;
-        const int64_t blk = bi < a.max_blocks ? a.block_tables[(size_t)b * a.max_blocks + bi] : 0;
-        a.slots[b] = blk * a.BS + pn % a.BS;
-        a.offsets[b] = pn + 1;
-      }
-    }
+  const int64_t pn = pos_b + 1;
+  int64_t blk = 0;
+  // the next K/V slot's block-table entry (thread 0) and the next step's embedding row (every
+  // lane, 16 B) are requested together: one round trip for both
+  if (a.adv && a.slots != nullptr && threadIdx.x == 0) {   // past the table the slot is never used
+    const int64_t bi = pn / a.BS;
+    if (bi < a.max_blocks) blk = a.block_tables[(size_t)b * a.max_blocks + bi];
   }
-  if (a.adv && a.res != nullptr) {   // next step's embedding row, 16 B per lane
+  if (a.adv && a.res != nullptr) {
     int64_t t = tok < 0 ? 0 : (tok >= a.vocab ? a.vocab - 1 : tok);
     const int row8 = a.H / 8;
     const uint4* src = reinterpret_cast<const uint4*>(a.embed) + (size_t)t * row8;
     uint4* dst = reinterpret_cast<uint4*>(a.res) + (size_t)b * row8;
     for (int i = threadIdx.x; i < row8; i += NT) dst[i] = src[i];
+  }
+  if (threadIdx.x == 0) {
+    a.tok[b] = tok;
+    if (a.adv) {
+      if (st < a.max_steps) a.out[st * a.B + b] = tok;
+      a.ids[b] = tok;
+      a.positions[b] = pn;
+      a.ctx_lens[b] = ctx_b + 1;
+      if (a.slots != nullptr) {
+        a.slots[b] = blk * a.BS + pn % a.BS;
+        a.offsets[b] = pn + 1;
+      }
+    }
   }
   if (a.adv && threadIdx.x == 0) {   // the last decider of the launch advances the step counter
     int* done = reinterpret_cast<int*>(a.ws) + (size_t)a.B * W_ROW;
