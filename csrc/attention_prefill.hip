@@ -230,7 +230,8 @@ __global__ void __launch_bounds__(256) prefill_kernel(
 int prefill32_rows(int G);
 int launch_prefill32(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv,
-                     int max_blocks, float scale, hipStream_t stream);
+                     int max_blocks, float scale, hipStream_t stream, int map_stride, const int* cmap, int n_split,
+                     float* part_o, float* part_ml);
 
 // D = 128 with G in {1, 2, 4, 8} runs the 32x32-MFMA kernel (attention_prefill32.hip) unless
 // ROUNDTABLE_PREFILL16=1; everything else this file's 16x16 kernel. The host tile map must use
@@ -254,7 +255,7 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
   if (Hq % Hkv || !(G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) return -1;
   if (use_prefill32(G, D))
     return launch_prefill32(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, tile_map, n_tiles, Hq, Hkv,
-                            max_blocks, scale, stream);
+                            max_blocks, scale, stream, 2, nullptr, 0, nullptr, nullptr);
   const int rows = prefill_rows_per_tile(G, D);
   dim3 grid(n_tiles, Hkv), block(256);
   const float sl2 = scale * LOG2E;
@@ -277,3 +278,20 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
 #undef RT_PF
   return 0;
 }
+
+// Key-split prefill (32x32 kernel only: D = 128, G in {1, 2, 4, 8}): items [n_items, 5] (sequence,
+// first row, first / end key tile, partial slot or -1), cmap [n_split, 4] (sequence, first row,
+// first slot, parts). For launches with fewer tiles than CUs (tensor-parallel shards: one or two
+// KV heads per rank), where whole tiles would leave most CUs idle.
+int launch_prefill_split(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                         const int* cu_q, const int* start_pos, const int* items, int n_items, const int* cmap,
+                         int n_split, float* part_o, float* part_ml, int Hq, int Hkv, int D, int max_blocks,
+                         float scale, hipStream_t stream) {
+  if (n_items == 0) return 0;
+  const int G = Hq / Hkv;
+  if (Hq % Hkv || !use_prefill32(G, D)) return -1;
+  return launch_prefill32(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, items, n_items, Hq, Hkv,
+                          max_blocks, scale, stream, 5, cmap, n_split, part_o, part_ml);
+}
+
+int prefill_split_supported(int G, int D) { return use_prefill32(G, D) ? 1 : 0; }

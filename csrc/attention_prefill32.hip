@@ -108,13 +108,14 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
     uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, const int* __restrict__ cu_q,
     const int* __restrict__ start_pos, const int* __restrict__ tile_map, int Hq, int Hkv, int max_blocks,
-    float scale_log2, int rows_per_tile) {
+    float scale_log2, int rows_per_tile, int map_stride, float* __restrict__ part_o, float* __restrict__ part_ml) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];   // 68 KiB: static (> 64 KiB)
   // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (id mod 8), so with
   // id = tile * Hkv + hk every workgroup of kv head hk lands on XCD hk (Hkv = 8): that head's
   // K/V (2 MiB at 4K tokens) stays in one XCD's 4 MiB L2 instead of streaming from MALL/HBM.
   const int tile = blockIdx.x / Hkv, hk = blockIdx.x - (blockIdx.x / Hkv) * Hkv;
-  const int s = tile_map[2 * tile], row0 = tile_map[2 * tile + 1];
+  const int* item = tile_map + (size_t)map_stride * tile;
+  const int s = item[0], row0 = item[1];
   const int q_begin = cu_q[s], q_end = cu_q[s + 1];
   const int sp = start_pos[s];
   const int tid = threadIdx.x;
@@ -125,7 +126,16 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
   const int wrow0 = row0 + 32 * (wid / G);
   const int tile_rows_end = min(row0 + rows_per_tile, q_end);
   const int kmax = sp + (tile_rows_end - q_begin);  // keys [0, kmax) for the whole workgroup
-  const int ntiles = (kmax + KT - 1) / KT;
+  // key split (map_stride 5: sequence, first row, first / end key tile, partial slot): this
+  // workgroup covers key tiles [tb, te) and leaves an unnormalised partial for the combine
+  // launch (part >= 0), or the whole range and writes the output itself (part < 0)
+  int tb = 0, te = (kmax + KT - 1) / KT, part = -1;
+  if (map_stride == 5) {
+    tb = item[2];
+    te = min(item[3], te);
+    part = item[4];
+  }
+  const int ntiles = max(0, te - tb);
   const int my_row = min(wrow0 + c, q_end - 1);
   const int my_pos = sp + (my_row - q_begin);
   // keys this wave can ever see (tiles past it are still loaded cooperatively, math skipped)
@@ -151,8 +161,9 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
   const size_t blk_stride = (size_t)Hkv * BS * D;
   const size_t head_off = (size_t)hk * BS * D;
   // one 64-key tile of the math: S^T = K Q^T, online softmax, O^T += V^T P^T
-  auto compute_tile = [&](int t, const unsigned char* kb, const unsigned char* vb) {
-      if (t * KT < wave_kmax) {
+  auto compute_tile = [&](int tl, const unsigned char* kb, const unsigned char* vb) {
+      const int t = tb + tl;   // absolute key tile
+      if (tl < ntiles && t * KT < wave_kmax) {
         // ---- S^T = K Q^T (two 32-key blocks) ----
         f16v sc[2];
 #pragma unroll
@@ -246,10 +257,10 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
     // register staging one tile ahead: tile t+1's loads fly during tile t's math
     Loader<NW> ld;
     if (ntiles > 0) {
-      nb.fetch(bt, 0, max_blocks, tid);
+      nb.fetch(bt, tb, max_blocks, tid);
       ld.load(k_cache, v_cache, nb, blk_stride, head_off, tid);
       ld.store(smem, smem + KBYTES, tid);
-      if (ntiles > 1) nb.fetch(bt, 1, max_blocks, tid);
+      if (ntiles > 1) nb.fetch(bt, tb + 1, max_blocks, tid);
     }
     // Q^T and tile 0 landed: without this explicit drain the waitcnt pass, merging the
     // ntiles == 0 path at the loop header, waits on qf inside the loop with vmcnt(n..0) —
@@ -260,7 +271,7 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
       const int buf = t & 1;
       if (t + 1 < ntiles) {
         ld.load(k_cache, v_cache, nb, blk_stride, head_off, tid);
-        if (t + 2 < ntiles) nb.fetch(bt, t + 2, max_blocks, tid);
+        if (t + 2 < ntiles) nb.fetch(bt, tb + t + 2, max_blocks, tid);
       }
       compute_tile(t, smem + buf * STAGE, smem + buf * STAGE + KBYTES);
       // buffer buf^1 held tile t-1, which every wave finished before the previous barrier
@@ -274,11 +285,11 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
     Loader<NW> la, lb;
     Blocks<NW> nb2;                       // second block-id set: fetched a step before its use
     const int last = ntiles > 0 ? ntiles - 1 : 0;
-    nb.fetch(bt, 0, max_blocks, tid);
+    nb.fetch(bt, tb, max_blocks, tid);
     la.load(k_cache, v_cache, nb, blk_stride, head_off, tid);
-    nb2.fetch(bt, min(1, last), max_blocks, tid);
+    nb2.fetch(bt, tb + min(1, last), max_blocks, tid);
     lb.load(k_cache, v_cache, nb2, blk_stride, head_off, tid);
-    nb.fetch(bt, min(2, last), max_blocks, tid);
+    nb.fetch(bt, tb + min(2, last), max_blocks, tid);
     la.store(smem, smem + KBYTES, tid);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
@@ -286,7 +297,7 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
     // step waits only for that (older) fetch, never for the K/V loads still in flight
     auto step = [&](int t, Loader<NW>& issue, const Loader<NW>& write, const Blocks<NW>& use, Blocks<NW>& fill) {
       const int buf = t & 1;
-      fill.fetch(bt, min(t + 3, last), max_blocks, tid);
+      fill.fetch(bt, tb + min(t + 3, last), max_blocks, tid);
       issue.load(k_cache, v_cache, use, blk_stride, head_off, tid);   // tile min(t+2, last)
       compute_tile(t, smem + buf * STAGE, smem + buf * STAGE + KBYTES);   // no-op for t >= ntiles
       // unconditional (past the end it fills a buffer nobody reads): a branch here leaves the
@@ -303,6 +314,21 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
   // ---- epilogue: lane (q = c, h) holds O^T[d = 32db + 8b + 4h + j][q], reg i = 4b + j ----
   lsum += __shfl_xor(lsum, 32, 64);
   const int row = wrow0 + c;
+  if (part >= 0) {
+    // partial of this wave's 32 columns over its key range: O^T unnormalised (relative to the
+    // running max m, log2 units), (m, l) per column; every column is written (the combine skips
+    // rows past the tile)
+    const size_t slot = (((size_t)part * Hkv + hk) * NW + wid) * 32 + c;
+    float* po = part_o + slot * D;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        *reinterpret_cast<rt::float4_*>(po + 32 * db + 8 * b + 4 * h) =
+            rt::float4_{o[db][4 * b], o[db][4 * b + 1], o[db][4 * b + 2], o[db][4 * b + 3]};
+    if (h == 0) *reinterpret_cast<float2*>(part_ml + 2 * slot) = make_float2(m, lsum);
+    return;
+  }
   if (row < q_end && row < row0 + rows_per_tile) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     uint16_t* orow = out + ((size_t)row * Hq + head) * D;
@@ -317,6 +343,62 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
       }
   }
 }
+// Combine of the key-split partials: one thread per (wave, column) of a split tile and 16 of its
+// 128 dims (grid.y = D / 16), every part's (m, l) and O slice requested before the merge of a
+// chunk; fixed part order (deterministic).
+template <int G, int NW>
+__global__ void __launch_bounds__(NW * 32) prefill32_combine_kernel(uint16_t* __restrict__ out,
+                                                                    const int* __restrict__ cmap,
+                                                                    const int* __restrict__ cu_q,
+                                                                    const float* __restrict__ part_o,
+                                                                    const float* __restrict__ part_ml, int Hq,
+                                                                    int Hkv, int rows_per_tile) {
+  const int st = blockIdx.x / Hkv, hk = blockIdx.x - (blockIdx.x / Hkv) * Hkv;
+  const int w = threadIdx.x >> 5, c = threadIdx.x & 31;
+  const int s = cmap[4 * st], row0 = cmap[4 * st + 1], p0 = cmap[4 * st + 2], np = cmap[4 * st + 3];
+  const int row = row0 + 32 * (w / G) + c;
+  if (row >= cu_q[s + 1] || row >= row0 + rows_per_tile) return;
+  const int head = hk * G + (w % G);
+  const int d0 = 16 * blockIdx.y;
+  constexpr int PC = 4;   // parts per chunk of loads
+  float M = -INFINITY, L = 0.f;
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int pb = 0; pb < np; pb += PC) {
+    float2 ml[PC];
+    rt::float4_ ov[PC][4];
+#pragma unroll
+    for (int j = 0; j < PC; ++j) {
+      const int p = p0 + min(pb + j, np - 1);
+      const size_t slot = (((size_t)p * Hkv + hk) * NW + w) * 32 + c;
+      ml[j] = *reinterpret_cast<const float2*>(part_ml + 2 * slot);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) ov[j][q4] = *reinterpret_cast<const rt::float4_*>(part_o + slot * 128 + d0 + 4 * q4);
+    }
+#pragma unroll
+    for (int j = 0; j < PC; ++j) {
+      if (pb + j >= np || !(ml[j].y > 0.f)) continue;
+      const float Mc = fmaxf(M, ml[j].x);
+      const float a = M == -INFINITY ? 0.f : exp2f(M - Mc), f = exp2f(ml[j].x - Mc);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[4 * q4 + i] = acc[4 * q4 + i] * a + f * ov[j][q4][i];
+      L = L * a + f * ml[j].y;
+      M = Mc;
+    }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  uint16_t* orow = out + ((size_t)row * Hq + head) * 128 + d0;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    uint2 pk;
+    pk.x = rt::pack2(acc[4 * q4] * inv, acc[4 * q4 + 1] * inv);
+    pk.y = rt::pack2(acc[4 * q4 + 2] * inv, acc[4 * q4 + 3] * inv);
+    *reinterpret_cast<uint2*>(orow + 4 * q4) = pk;
+  }
+}
 }  // namespace
 
 // rows of one work tile for group size G (D = 128); 0 = unsupported (use attention_prefill.hip)
@@ -325,12 +407,19 @@ int prefill32_rows(int G) {
   return 0;
 }
 
+// tile_map [n_tiles, map_stride]: map_stride 2 = (sequence, first row), every tile whole;
+// map_stride 5 = key-split work items (+ first / end key tile, partial slot or -1) whose partial
+// slots are merged by a second launch over cmap [n_split, 4] (sequence, first row, first slot,
+// parts); part_o >= parts * Hkv * 8 * 32 * 128 floats, part_ml >= parts * Hkv * 8 * 32 * 2.
 int launch_prefill32(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                      const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv,
-                     int max_blocks, float scale, hipStream_t stream) {
+                     int max_blocks, float scale, hipStream_t stream, int map_stride, const int* cmap, int n_split,
+                     float* part_o, float* part_ml) {
   const int G = Hq / Hkv;
   const int rows = prefill32_rows(G);
   if (rows == 0) return -1;
+  if (map_stride != 2 && map_stride != 5) return -2;
+  if (map_stride == 5 && n_split > 0 && (cmap == nullptr || part_o == nullptr || part_ml == nullptr)) return -3;
   const float sl2 = scale * LOG2E;
   dim3 grid(n_tiles * Hkv);
   static const int depth = [] {
@@ -340,10 +429,13 @@ int launch_prefill32(void* out, const void* q, const void* k_cache, const void* 
 #define RT_P32(GG, NWV)                                                                                          \
   if (depth == 1) hipLaunchKernelGGL((prefill32_kernel<GG, NWV, 1>), grid, dim3(64 * NWV), 0, stream, (uint16_t*)out, \
                      (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, \
-                     start_pos, tile_map, Hq, Hkv, max_blocks, sl2, rows);                                      \
+                     start_pos, tile_map, Hq, Hkv, max_blocks, sl2, rows, map_stride, part_o, part_ml);          \
   else hipLaunchKernelGGL((prefill32_kernel<GG, NWV, 2>), grid, dim3(64 * NWV), 0, stream, (uint16_t*)out,              \
                      (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, \
-                     start_pos, tile_map, Hq, Hkv, max_blocks, sl2, rows)
+                     start_pos, tile_map, Hq, Hkv, max_blocks, sl2, rows, map_stride, part_o, part_ml);          \
+  if (map_stride == 5 && n_split > 0)                                                                            \
+    hipLaunchKernelGGL((prefill32_combine_kernel<GG, NWV>), dim3(n_split * Hkv, D / 16), dim3(32 * NWV), 0, stream, \
+                       (uint16_t*)out, cmap, cu_q, (const float*)part_o, (const float*)part_ml, Hq, Hkv, rows)
   switch (G) {
     case 1: RT_P32(1, 8); break;
     case 2: RT_P32(2, 8); break;

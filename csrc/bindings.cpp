@@ -20,6 +20,11 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
                         hipStream_t stream, int defer_combine, int* deferred);
 int prefill_rows_per_tile(int G, int D);
+int launch_prefill_split(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                         const int* cu_q, const int* start_pos, const int* items, int n_items, const int* cmap,
+                         int n_split, float* part_o, float* part_ml, int Hq, int Hkv, int D, int max_blocks,
+                         float scale, hipStream_t stream);
+int prefill_split_supported(int G, int D);
 int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                    const int* cu_q, const int* start_pos, const int* tile_map, int n_tiles, int Hq, int Hkv, int D,
                    int max_blocks, float scale, hipStream_t stream);
@@ -216,6 +221,37 @@ void prefill_attention(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache
                                 tile_map.data_ptr<int>(), (int)tile_map.size(0), (int)Hq, (int)k_cache.size(1), (int)D,
                                 (int)block_tables.size(1), (float)scale, cur_stream());
   TORCH_CHECK(rc == 0, "prefill_attention: unsupported configuration (rc=", rc, ")");
+}
+
+void prefill_attention_split(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
+                             torch::Tensor block_tables, torch::Tensor cu_q, torch::Tensor start_pos,
+                             torch::Tensor items, torch::Tensor cmap, torch::Tensor part_o, torch::Tensor part_ml,
+                             int64_t n_parts, double scale) {
+  check_bf16(out, "out");
+  check_bf16(q, "q");
+  TORCH_CHECK(q.dim() == 3, "q must be [T, Hq, D]");
+  const int64_t Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
+  check_caches(k_cache, v_cache, Hkv, D);
+  TORCH_CHECK(k_cache.size(2) == 32, "prefill kernel requires kv block_size == 32");
+  TORCH_CHECK(prefill_split_supported((int)(Hq / Hkv), (int)D), "prefill_attention_split: needs D 128, G in {1,2,4,8}");
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_type(cu_q, torch::kInt32, "cu_q");
+  check_type(start_pos, torch::kInt32, "start_pos");
+  check_type(items, torch::kInt32, "items");
+  check_type(cmap, torch::kInt32, "cmap");
+  TORCH_CHECK(block_tables.size(0) == cu_q.numel() - 1 && start_pos.numel() == cu_q.numel() - 1, "varlen metadata");
+  TORCH_CHECK(items.dim() == 2 && items.size(1) == 5 && items.is_contiguous(), "items must be [n, 5]");
+  TORCH_CHECK(cmap.dim() == 2 && cmap.size(1) == 4 && cmap.is_contiguous(), "cmap must be [m, 4]");
+  TORCH_CHECK(part_o.scalar_type() == torch::kFloat32 && part_ml.scalar_type() == torch::kFloat32 &&
+                  part_o.is_contiguous() && part_ml.is_contiguous(), "partials must be contiguous fp32");
+  TORCH_CHECK(part_o.numel() >= n_parts * Hkv * 8 * 32 * D && part_ml.numel() >= n_parts * Hkv * 8 * 32 * 2,
+              "partial buffers too small");
+  const int rc = launch_prefill_split(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                      block_tables.data_ptr<int>(), cu_q.data_ptr<int>(), start_pos.data_ptr<int>(),
+                                      items.data_ptr<int>(), (int)items.size(0), cmap.data_ptr<int>(),
+                                      (int)cmap.size(0), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), (int)Hq,
+                                      (int)Hkv, (int)D, (int)block_tables.size(1), (float)scale, cur_stream());
+  TORCH_CHECK(rc == 0, "prefill_attention_split: unsupported configuration (rc=", rc, ")");
 }
 
 void silu_and_mul(torch::Tensor out, torch::Tensor x) {
@@ -652,6 +688,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("slot_stride") = 0, py::arg("defer_combine") = false);
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile, py::arg("G"), py::arg("D") = 128);
   m.def("prefill_attention", &prefill_attention);
+  m.def("prefill_attention_split", &prefill_attention_split);
+  m.def("prefill_split_supported", &prefill_split_supported, py::arg("G"), py::arg("D") = 128);
   m.def("silu_and_mul", &silu_and_mul);
   m.def("gelu_tanh", &gelu_tanh);
   m.def("sample", &sample);

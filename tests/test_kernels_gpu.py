@@ -255,6 +255,46 @@ def test_prefill_long_prefix():
     close(out, exp.to(DEV), 0.02, 0.02)
 
 
+@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (32, 8)])
+@pytest.mark.parametrize("min_chunk", [1, 3, 8])
+def test_prefill_key_split(hq, hkv, min_chunk):
+    """Key-split prefill (tensor-parallel shard head counts: few tiles x KV heads): work items
+    over key-tile ranges leave unnormalised partials merged by the combine launch
+    (attention_prefill32.hip); long tiles cut into 2..many parts, short ones whole, a fresh
+    sequence (causal diagonal inside a part) and delta chunks over long prefixes — vs the fp32
+    oracle and vs the whole-tile kernel."""
+    d = 128
+    specs = [(9000, 300), (0, 257), (2345, 129), (31, 1)]
+    S = len(specs)
+    nb_each = [(sp + n + 31) // 32 for sp, n in specs]
+    nb = sum(nb_each) + 2
+    kc, vc = make_cache(nb, hkv, d, seed=51)
+    perm = torch.randperm(nb, generator=torch.Generator().manual_seed(7)).tolist()
+    bt = torch.zeros(S, max(nb_each), dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(nb_each):
+        bt[s, :n] = torch.tensor(perm[i:i + n], dtype=torch.int32)
+        i += n
+    cu = [0]
+    for _, n in specs:
+        cu.append(cu[-1] + n)
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    st = torch.tensor([sp for sp, _ in specs], dtype=torch.int32)
+    q = bf(cu[-1], hq, d, seed=52)
+    scale = 1 / math.sqrt(d)
+    rows = ops.native().prefill_rows_per_tile(hq // hkv, d)
+    plan = ops.prefill_split_plan(cu_t, rows, st, hkv, num_cus=1 << 20, min_chunk_tiles=min_chunk)
+    assert plan is not None and plan[2] >= 2
+    split = (plan[0].to(DEV), plan[1].to(DEV), plan[2])
+    out = ops.prefill_attention(q, kc, vc, bt.to(DEV), cu_t.to(DEV), st.to(DEV), scale, split=split)
+    whole = ops.prefill_attention(q, kc, vc, bt.to(DEV), cu_t.to(DEV), st.to(DEV), scale)
+    exp = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt, cu_t, st, scale)
+    close(out, exp.to(DEV), 0.02, 0.02)
+    close(out, whole, 0.02, 0.02)
+    again = ops.prefill_attention(q, kc, vc, bt.to(DEV), cu_t.to(DEV), st.to(DEV), scale, split=split)
+    assert torch.equal(out, again)
+
+
 def test_sample_greedy_and_topk1():
     B, V = 5, 128256
     # fp32 logits: bf16 random rows contain exact ties at the max, where top-k=1 legitimately

@@ -133,3 +133,18 @@ def test_split_workspace_matches_native_layout():
         pytest.skip("native extension not built")
     assert ops.SPLIT_WS_INTS >= ops.native().split_workspace_ints(255)
     assert ops.split_workspace("cpu").numel() == ops.SPLIT_WS_INTS
+
+
+def test_prefill_split_plan_shapes():
+    """The planner splits only when whole tiles leave most CUs idle, and its parts tile each key
+    range exactly (host-only check of the plan the GPU test runs)."""
+    cu = torch.tensor([0, 1772], dtype=torch.int32)
+    st = torch.tensor([16000], dtype=torch.int32)
+    assert ops.prefill_split_plan(cu, 64, st, 8, num_cus=256) is None          # tp 1: 28 x 8 tiles
+    items, cmap, parts = ops.prefill_split_plan(cu, 64, st, 1, num_cus=256)    # tp 8: 28 tiles
+    assert items.shape[1] == 5 and cmap.shape[1] == 4 and parts == int(cmap[:, 3].sum())
+    assert len(items) >= 256                                                    # ~2 items per CU
+    for s, r, p0, n in cmap.tolist():
+        mine = sorted((tb, te) for s2, r2, tb, te, p in items.tolist() if (s2, r2) == (s, r))
+        assert mine[0][0] == 0 and all(a[1] == b[0] for a, b in zip(mine, mine[1:]))
+        assert sorted(p for s2, r2, tb, te, p in items.tolist() if (s2, r2) == (s, r)) == list(range(p0, p0 + n))

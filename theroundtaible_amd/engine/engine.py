@@ -57,6 +57,7 @@ class EngineConfig:
     kv_cache_fraction: float = 0.85
     max_kv_tokens: Optional[int] = None     # optional cap on resident tokens
     prefill_chunk: int = 8192               # tokens per prefill forward (summed over sequences)
+    prefill_key_split: bool = True          # split long prefill tiles' key ranges when tiles x KV heads < CUs / 2
     use_graphs: bool = True
     sync_every: int = 32                    # decode steps between host token readbacks
     max_batch: int = 16
@@ -456,6 +457,14 @@ class Engine:
                 rows = ops.native().prefill_rows_per_tile(self.model.n_heads // self.model.n_kv_heads,
                                                           self.cfg.head_dim)
                 meta.tile_map = ops.prefill_tile_map(cu_t, rows, torch.tensor(starts)).to(dev, non_blocking=True)
+                # few tiles x KV heads (a tensor-parallel shard) leave most CUs idle: cut the long
+                # tiles' key ranges into partials merged by a second launch (attention_prefill32.hip)
+                G = self.model.n_heads // self.model.n_kv_heads
+                if self.ecfg.prefill_key_split and ops.native().prefill_split_supported(G, self.cfg.head_dim):
+                    plan = ops.prefill_split_plan(cu_t, rows, torch.tensor(starts), self.model.n_kv_heads)
+                    if plan is not None:
+                        meta.prefill_split = (plan[0].to(dev, non_blocking=True), plan[1].to(dev, non_blocking=True),
+                                              plan[2])
             with trace.range("prefill"):
                 logits = self.model.forward(torch.tensor(tok, dtype=torch.int64).to(dev, non_blocking=True),
                                             torch.tensor(pos, dtype=torch.int64).to(dev, non_blocking=True),

@@ -38,6 +38,7 @@ class AttnMeta:
     cu_q: Optional[torch.Tensor] = None         # prefill: [S+1] int32
     start_pos: Optional[torch.Tensor] = None    # prefill: [S] int32
     tile_map: Optional[torch.Tensor] = None     # prefill: [n_tiles, 2] int32
+    prefill_split: Optional[tuple] = None       # prefill: ops.prefill_split_plan (items, cmap, parts) on device
     last_rows: Optional[torch.Tensor] = None    # prefill: rows whose logits are needed
     groups: Optional[torch.Tensor] = None       # decode: [B, 3] shared-prefix groups (ops.decode_groups)
     local_logits: bool = False                  # TP decode: return this rank's vocab shard (C3 greedy argmax)
@@ -71,7 +72,7 @@ class LlamaModel:
             return ops.paged_attention_decode(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale,
                                               meta.num_splits, meta.workspace, groups=meta.groups)
         return ops.prefill_attention(q, kc, vc, meta.block_tables, meta.cu_q, meta.start_pos, self.scale,
-                                     meta.tile_map)
+                                     meta.tile_map, split=meta.prefill_split)
 
     def fused_decode_ok(self, ids: torch.Tensor) -> bool:
         cfg = self.cfg

@@ -222,15 +222,73 @@ def prefill_tile_map(cu_q: torch.Tensor, rows_per_tile: int, start_pos=None) -> 
     return torch.tensor([(s, r) for _, s, r in items], dtype=torch.int32).reshape(-1, 2)
 
 
+PREFILL_KT = 64          # keys per tile of the 32x32 prefill kernel (attention_prefill32.hip)
+
+
+def prefill_split_plan(cu_q: torch.Tensor, rows_per_tile: int, start_pos, n_kv_heads: int,
+                       num_cus: Optional[int] = None, min_chunk_tiles: int = 8):
+    """Key-split work list for the varlen prefill kernel when its whole tiles would leave CUs idle
+    (tensor-parallel shards: one or two KV heads per rank give ``tiles x Hkv`` << CUs, e.g. 28
+    workgroups for a 1.8K-token prefill at tp 8). Returns None when the tiles alone fill half the
+    chip; else ``(items [n, 5], cmap [m, 4], parts)``: items = (sequence, first row, first / end
+    key tile of 64 keys, partial slot or -1), heaviest first; a tile longer than the chunk is cut
+    into equal key ranges whose partial slots are consecutive and merged by the combine launch
+    (cmap = sequence, first row, first slot, parts). Chunk = the tiles' total key work spread over
+    ~2 workgroups per CU, at least ``min_chunk_tiles`` key tiles (partials cost a write + read
+    of 128 floats per query row and head each)."""
+    cq = cu_q.tolist()
+    sp = start_pos.tolist() if start_pos is not None else [0] * (len(cq) - 1)
+    tiles = []
+    for s in range(len(cq) - 1):
+        for r in range(cq[s], cq[s + 1], rows_per_tile):
+            last_key = sp[s] + min(r + rows_per_tile, cq[s + 1]) - cq[s]
+            tiles.append((s, r, (last_key + PREFILL_KT - 1) // PREFILL_KT))
+    num_cus = device_cus() if num_cus is None else num_cus
+    hkv = max(1, n_kv_heads)
+    if not tiles or len(tiles) * hkv >= num_cus // 2:
+        return None
+    target = max(1, (2 * num_cus) // hkv)
+    total = sum(t[2] for t in tiles)
+    chunk = max(min_chunk_tiles, -(-total // target))
+    items, cmap, p = [], [], 0
+    for s, r, nkt in tiles:
+        if nkt <= chunk:
+            items.append((nkt, (s, r, 0, nkt, -1)))
+            continue
+        n = -(-nkt // chunk)
+        per = -(-nkt // n)
+        cmap.append((s, r, p, n))
+        for j in range(n):
+            tb = j * per
+            te = min(nkt, tb + per)
+            items.append((te - tb, (s, r, tb, te, p + j)))
+        p += n
+    if not cmap:
+        return None
+    items.sort(key=lambda x: -x[0])
+    return (torch.tensor([it for _, it in items], dtype=torch.int32).reshape(-1, 5),
+            torch.tensor(cmap, dtype=torch.int32).reshape(-1, 4), p)
+
+
 def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                       cu_q: torch.Tensor, start_pos: torch.Tensor, scale: float,
-                      tile_map: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      tile_map: Optional[torch.Tensor] = None, split=None) -> torch.Tensor:
+    """``split``: a device-resident :func:`prefill_split_plan` ``(items, cmap, parts)`` — the
+    key-split launch + its combine; ``tile_map`` otherwise (whole tiles)."""
     if _use_native(q):
         nat = native()
+        out = torch.empty_like(q)
+        if split is not None:
+            items, cmap, parts = split
+            hkv, D = k_cache.shape[1], q.shape[2]
+            part_o = torch.empty(parts * hkv * 8 * 32 * D, dtype=torch.float32, device=q.device)
+            part_ml = torch.empty(parts * hkv * 8 * 32 * 2, dtype=torch.float32, device=q.device)
+            nat.prefill_attention_split(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, items, cmap,
+                                        part_o, part_ml, parts, scale)
+            return out
         rows = nat.prefill_rows_per_tile(q.shape[1] // k_cache.shape[1], q.shape[2])
         if tile_map is None:
             tile_map = prefill_tile_map(cu_q.cpu(), rows, start_pos.cpu()).to(q.device)
-        out = torch.empty_like(q)
         nat.prefill_attention(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, tile_map, scale)
         return out
     return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q.cpu(), start_pos.cpu(), scale)
