@@ -141,17 +141,19 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
 
   const int b = bh / Hkv, hk = bh - (bh / Hkv) * Hkv;
   const int G = Hq / Hkv;
-  int b0 = b, n = 1, sh = 0;
-  if (P.groups != nullptr) {
-    b0 = P.groups[3 * b];
-    n = P.groups[3 * b + 1];
-    sh = P.groups[3 * b + 2];
-    if (n < 1 || n * G > GM || b0 < 0 || b < b0 || b - b0 >= n || sh < 0) {  // malformed: run alone
-      b0 = b;
-      n = 1;
-      sh = 0;
-    }
-  }
+  // the sequence's length and its group record are requested together, before any test on
+  // either (a short-circuit test made the compiler wait for one load before issuing the next:
+  // two extra dependent trips ahead of the K/V stream)
+  // branch-free: without groups the three record loads read ctx_lens[b] (valid, ignored)
+  const bool grouped = P.groups != nullptr;
+  const int* gp = grouped ? P.groups + 3 * b : ctx_lens + b;
+  const int go = grouped ? 1 : 0;
+  const int ctx = ctx_lens[b];
+  const int g0 = gp[0], g1 = gp[go], g2 = gp[2 * go];
+  const bool bad = !grouped | (g1 < 1) | (g1 * G > GM) | (g0 < 0) | (b < g0) | (b - g0 >= g1) | (g2 < 0);
+  const int b0 = bad ? b : g0;   // no / malformed group record: run alone
+  const int n = bad ? 1 : g1;
+  const int sh = bad ? 0 : g2;
   const int mi = b - b0, ncol = n * G;
   const int nslots = n * num_splits, slot = mi * num_splits + split;
   const int stride = P.slot_stride > 0 ? P.slot_stride : num_splits;
@@ -159,7 +161,6 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
   const int r = lane & 15, g = lane >> 4;
   const int rseq = r / G, rhead = r - (r / G) * G;  // column r -> (member, head within the kv group)
 
-  const int ctx = ctx_lens[b];
   if (P.probe == 1) {          // launch + metadata round trip only
     if (ctx == -12345) out[0] = 0;
     return false;
