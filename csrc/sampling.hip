@@ -143,19 +143,83 @@ RT_DEVICE void am_merge(ArgMax& a, float v, int i) {
     a.i = i;
   }
 }
+// Wave reductions on DPP lane permutes (VALU, a few cycles each) instead of ds_bpermute shuffles
+// (an LDS round trip each): xor 1 and xor 2 as quad permutes, then the half-row and row mirrors
+// pair the quads and the 8-lane halves (every lane of a 16-lane row then holds the row's
+// result), and the four rows are read out with readlane (wave-uniform result). Fixed pairing
+// order: deterministic.
+constexpr int DPP_QUAD_1032 = 0xB1, DPP_QUAD_2301 = 0x4E, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_MIRROR = 0x140;
+template <int CTRL>
+RT_DEVICE float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+RT_DEVICE int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+RT_DEVICE float rl(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+RT_DEVICE float wave_sum_dpp(float v) {
+  v += dpp_f<DPP_QUAD_1032>(v);
+  v += dpp_f<DPP_QUAD_2301>(v);
+  v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_f<DPP_ROW_MIRROR>(v);
+  return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
+}
+RT_DEVICE float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f<DPP_QUAD_1032>(v));
+  v = fmaxf(v, dpp_f<DPP_QUAD_2301>(v));
+  v = fmaxf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v));
+  v = fmaxf(v, dpp_f<DPP_ROW_MIRROR>(v));
+  return fmaxf(fmaxf(rl(v, 0), rl(v, 16)), fmaxf(rl(v, 32), rl(v, 48)));
+}
+RT_DEVICE ArgMax wave_argmax_dpp(ArgMax a) {
+  am_merge(a, dpp_f<DPP_QUAD_1032>(a.v), dpp_i<DPP_QUAD_1032>(a.i));
+  am_merge(a, dpp_f<DPP_QUAD_2301>(a.v), dpp_i<DPP_QUAD_2301>(a.i));
+  am_merge(a, dpp_f<DPP_ROW_HALF_MIRROR>(a.v), dpp_i<DPP_ROW_HALF_MIRROR>(a.i));
+  am_merge(a, dpp_f<DPP_ROW_MIRROR>(a.v), dpp_i<DPP_ROW_MIRROR>(a.i));
+  ArgMax r{rl(a.v, 0), __builtin_amdgcn_readlane(a.i, 0)};
+#pragma unroll
+  for (int q = 16; q < 64; q += 16) am_merge(r, rl(a.v, q), __builtin_amdgcn_readlane(a.i, q));
+  return r;
+}
+// block reductions: one value per wave through LDS, then every thread folds the NWV values in
+// wave order (no second shuffle level)
+RT_DEVICE float block_sum_dpp(float v, float* scr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_sum_dpp(v);
+  __syncthreads();
+  if (lane == 0) scr[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) t += scr[w];
+  return t;
+}
+RT_DEVICE float block_max_dpp(float v, float* scr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_max_dpp(v);
+  __syncthreads();
+  if (lane == 0) scr[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) t = fmaxf(t, scr[w]);
+  return t;
+}
 RT_DEVICE ArgMax block_argmax(ArgMax a, float* sv, int* si) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) am_merge(a, __shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64));
+  a = wave_argmax_dpp(a);
   __syncthreads();
   if (lane == 0) {
     sv[wid] = a.v;
     si[wid] = a.i;
   }
   __syncthreads();
-  ArgMax b{lane < NWV ? sv[lane] : -INFINITY, lane < NWV ? si[lane] : 0x7fffffff};
+  ArgMax b{sv[0], si[0]};
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) am_merge(b, __shfl_xor(b.v, o, 64), __shfl_xor(b.i, o, 64));
+  for (int w = 1; w < NWV; ++w) am_merge(b, sv[w], si[w]);
   return b;
 }
 
@@ -324,7 +388,7 @@ RT_DEVICE int nucleus_by_candidates(const T* row, int V, float mx, float invT, f
   float v_in = INFINITY, v_out = vj;   // known: values >= v_in are inside, <= v_out outside
 #pragma unroll
   for (int k = 0; k < NC; ++k) {
-    const float m = rt::block_sum(acc[k], red);
+    const float m = block_sum_dpp(acc[k], red);
     const bool ok = cv[k] != INFINITY && m < pz;
     if (ok) {
       if (kstar < 0) kstar = k;
@@ -375,7 +439,7 @@ RT_DEVICE int nucleus_by_candidates(const T* row, int V, float mx, float invT, f
     });
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      const float m = rt::block_sum(acc[k], red);
+      const float m = block_sum_dpp(acc[k], red);
       if (k < nu && m < pz) am_merge(best, s_us[k], s_ui[k]);
     }
   }
@@ -511,7 +575,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
       if (lst) okeys[i - lo] = okey(v);
     });
     gb = block_argmax(gb, sv, si);
-    mn = -rt::block_max(-mn, red);
+    mn = -block_max_dpp(-mn, red);
   } else {
     for_chunk([&](int i, float v) { am_merge(am, v, i); });
   }
@@ -699,9 +763,9 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
           mid_m += kb >= kj ? m : 0.f;
         }
       }
-      lo_m = rt::block_sum(lo_m, red);
-      mid_m = rt::block_sum(mid_m, red);
-      tot_m = rt::block_sum(tot_m, red);
+      lo_m = block_sum_dpp(lo_m, red);
+      mid_m = block_sum_dpp(mid_m, red);
+      tot_m = block_sum_dpp(tot_m, red);
       float pz = p * tot_m;
       bool decided = lo_m + mid_m < pz || lo_m >= pz;
       accepted = lo_m + mid_m < pz;
@@ -712,8 +776,8 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
           total += e;
           above += v > vj ? e : 0.f;
         });
-        above = rt::block_sum(above, red);
-        total = rt::block_sum(total, red);
+        above = block_sum_dpp(above, red);
+        total = block_sum_dpp(total, red);
         pz = p * total;
         accepted = above < pz;
       }
@@ -846,7 +910,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
           __syncthreads();
           const int t = threadIdx.x;
           const float my_w = t < tot ? aw[t] : 0.f;
-          const float zsum = rt::block_sum(my_w, red);
+          const float zsum = block_sum_dpp(my_w, red);
           ArgMax r{-INFINITY, 0x7fffffff};
           if (t < tot) {
             const uint32_t mk = ak[t];
@@ -894,7 +958,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
       }
       float tm = 0.f;
       for (int i = threadIdx.x; i < NB; i += NT) tm += hm[i];
-      tm = rt::block_sum(tm, red);
+      tm = block_sum_dpp(tm, red);
       const float tk = use_k ? (float)k : 3.0e38f;
       int bk = NB;
       float pre_c = 0.f, zk_mass = tm;
