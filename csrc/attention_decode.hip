@@ -184,13 +184,26 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   } else if (args.ext_combine) {
     // slots per row: every split of every member of the largest group (groups: n * G <= 16)
     const int nmax = groups != nullptr ? min(slot_stride, (16 / G) * num_splits) : num_splits;
-    const int nsl = min(128, (nmax + 7) / 8 * 8);          // slot-lanes (x 8 dim-lanes)
-    const int spl = (nmax + nsl - 1) / nsl;                 // slots per lane per chunk: 1 or 2
+    // slot-lanes (x 8 dim-lanes) per workgroup, capped at 32 (RT_COMBINE_NSL): fewer, wider lanes
+    // (8 slots each for a tp 8 table's 256-slot bound) beat 128 lanes x 2 — 4 waves to dispatch
+    // and merge instead of 16; tp 8 grouped attention + combine 12.4 -> 11.6 us
+    // (profiles/r04/combine_lanes_ab.md)
+    static const int nsl_cap = [] {
+      const char* e = getenv("RT_COMBINE_NSL");
+      const int v = e ? atoi(e) : 32;
+      return (v >= 8 && v <= 128 && v % 8 == 0) ? v : 32;
+    }();
+    int nsl = min(nsl_cap, (nmax + 7) / 8 * 8);
+    int spl = (nmax + nsl - 1) / nsl;                       // slots per lane per chunk
+    spl = spl <= 1 ? 1 : (spl <= 2 ? 2 : (spl <= 4 ? 4 : 8));
+    if ((nmax + spl - 1) / spl < nsl) nsl = ((nmax + spl - 1) / spl + 7) / 8 * 8;
     const dim3 cgrid(B * Hq, D / 32), cblock(8 * nsl);
 #define RT_CB(DV)                                                                                   \
   do {                                                                                              \
     if (spl <= 1) hipLaunchKernelGGL((decode_combine_kernel<DV, 1>), cgrid, cblock, 0, stream, args); \
-    else hipLaunchKernelGGL((decode_combine_kernel<DV, 2>), cgrid, cblock, 0, stream, args);          \
+    else if (spl <= 2) hipLaunchKernelGGL((decode_combine_kernel<DV, 2>), cgrid, cblock, 0, stream, args); \
+    else if (spl <= 4) hipLaunchKernelGGL((decode_combine_kernel<DV, 4>), cgrid, cblock, 0, stream, args); \
+    else hipLaunchKernelGGL((decode_combine_kernel<DV, 8>), cgrid, cblock, 0, stream, args);          \
   } while (0)
     if (D == 128) RT_CB(128);
     else RT_CB(64);
