@@ -67,6 +67,11 @@ def parse():
     p.add_argument("--simulate-tp", type=int, default=0,
                    help="COST MODEL ONLY: one process runs rank 0's shard of a tp=N engine, collectives replaced "
                         "by local no-ops (the output is labelled simulated)")
+    p.add_argument("--sim-k9-us", type=float, default=5.0,
+                   help="--simulate-tp: device-side stand-in latency of each all-reduce (a spin kernel holding the "
+                        "K9 launch's CUs, inside the captured graph); 0 = collectives free (round-4 compute-only records)")
+    p.add_argument("--sim-gather-us", type=float, default=9.5,
+                   help="--simulate-tp: the same for the vocab-parallel logits gather (0 = free)")
     p.add_argument("--knights-per-table", type=int, default=3)
     p.add_argument("--new-tokens", type=int, default=512, help="decode tokens per knight turn")
     p.add_argument("--temperature", type=float, default=0.7)
@@ -257,7 +262,9 @@ def _run(args, failsafe) -> int:
     tp = None
     if sim > 1:
         from theroundtaible_amd.parallel.tp import SimulatedTP
-        tp = SimulatedTP(sim)
+        tp = SimulatedTP(sim, comm_us=args.sim_k9_us or None, gather_us=args.sim_gather_us or None)
+        if tp.comm_us or tp.gather_us:
+            tp._spin_launch_us()      # calibrate the stand-in's launch cost before any capture
     elif T > 1:
         import torch.distributed as dist
         from theroundtaible_amd.parallel.tp import TPInfo
@@ -341,6 +348,12 @@ def _run(args, failsafe) -> int:
                 eng_ms[e.round] = agg(eng_ms.get(e.round, 0.0), float(e.metrics.get("turn_ms", 0.0)))
                 pre_ms[e.round] = agg(pre_ms.get(e.round, 0.0), float(e.metrics.get("prefill_ms", 0.0)))
                 dec_ms[e.round] = agg(dec_ms.get(e.round, 0.0), float(e.metrics.get("decode_ms", 0.0)))
+    ctx = []     # each timed turn's context at its end (prompt + reply tokens) per knight
+    for o in orchs:
+        for e in o.all_rounds:
+            if e.round in timed:
+                ctx.append(int(e.metrics.get("prompt_tokens", 0)) + int(e.metrics.get("decode_tokens", 0))
+                           + int(e.metrics.get("forced_tokens", 0)))
     for o in orchs:
         for e in o.all_rounds:
             if e.round in timed:
@@ -366,10 +379,15 @@ def _run(args, failsafe) -> int:
         metric = f"aggregate knight tokens/sec (one {kpt}-knight discuss, {args.round_mode} rounds)"
     else:
         metric = f"aggregate knight tokens/sec ({kpt}-knight discuss tables, {args.round_mode} rounds)"
-    if sim:
+    if sim and args.sim_k9_us:
+        metric = (f"SIMULATED rank 0 of tp{sim}: shard compute + device-simulated collectives (all-reduce "
+                  f"{args.sim_k9_us:g} us, gather {args.sim_gather_us:g} us per call) — " + metric)
+    elif sim:
         metric = f"SIMULATED rank-0 compute of tp{sim} (no communication; cost model input) — " + metric
     if sim:
-        parallelism = f"simulated tp{sim} (rank 0 shard, collectives elided)"
+        parallelism = (f"simulated tp{sim} (rank 0 shard, collectives "
+                       + (f"simulated on device: {args.sim_k9_us:g} us all-reduce, {args.sim_gather_us:g} us gather)"
+                          if args.sim_k9_us else "elided)"))
     elif T == 1:
         parallelism = (f"knight-placement x{N} (tables {args.placement} over GPUs), C1 all-gather"
                        if N > 1 else "single GPU")
@@ -387,12 +405,20 @@ def _run(args, failsafe) -> int:
         "config": {"model": args.model + (f" ({args.layers} layers, rehearsal)" if args.layers else ""),
                    "knights_per_table": kpt, "tables": n_tables, "knights": kpt * n_tables,
                    "knights_per_gpu": args.knights_per_gpu, "new_tokens_per_turn": args.new_tokens,
-                   "global_batch": kpt * n_tables, "seq_len": args.new_tokens,
+                   # seq_len = the longest context a knight's decode attends over in the timed
+                   # rounds (prompt + reply); the decode length per turn is new_tokens_per_turn
+                   "global_batch": kpt * n_tables, "seq_len": max(ctx, default=0),
+                   "context_tokens_per_knight_mean": round(sum(ctx) / len(ctx)) if ctx else 0,
+                   "context_tokens_per_knight_max": max(ctx, default=0),
                    "round_mode": args.round_mode, "prompt_layout": args.layout,
                    "placement": args.placement, "tp": sim or T,
                    "parallelism": parallelism},
         "detail": {"world": cl.world, "backend": cl.backend, "c1_ranks": cl.world if cl.distributed else 1,
                    "simulated_tp": sim or None,
+                   "sim_comm": ({"all_reduce_us": args.sim_k9_us, "gather_us": args.sim_gather_us,
+                                 "spin_launch_us": round(tp._launch_us, 2) if getattr(tp, "_launch_us", None) else None,
+                                 "calls_per_rank": getattr(tp, "sim_comm_calls", 0)}
+                                if sim and args.sim_k9_us else None),
                    "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),
                    "k9_us": getattr(getattr(engine.tp, "oneshot", None), "latency_us", None),
                    "k9_fused_gemm_ar": bool(getattr(getattr(engine.tp, "oneshot", None), "fused", False)),
@@ -402,6 +428,7 @@ def _run(args, failsafe) -> int:
                    "k9_ll_us": getattr(getattr(engine.tp, "oneshot", None), "ll_latency_us", None),
                    "k9_gather": bool(getattr(getattr(engine.tp, "oneshot", None), "gather_ok", False)),
                    "k9_gather_saving_us": getattr(getattr(engine.tp, "oneshot", None), "gather_saving_us", None),
+                   "k9_resyncs": engine.stats.get("k9_resyncs", 0),
                    "failed_turns": len(failures), "transcript_sha": transcript_sha, "decode_tokens": dec, "prefill_tokens": pre, "reused_kv_tokens": reused,
                    "exchange_ms_per_round": round(exch, 3), "c1_skipped_batches": getattr(pool, "c1_skipped", 0),
                    "c1_device_assembled": pool.exchange.device_path if pool.exchange is not None else 0,

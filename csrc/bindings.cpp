@@ -69,6 +69,9 @@ int oneshot_error(int id);
 int oneshot_clear_error(int id);
 int oneshot_set_poll_limit(int id, long long limit);
 int oneshot_set_ll(int id, int on);
+long long oneshot_epoch(int id);
+int oneshot_resync(int id, long long epoch);
+int sim_comm_spin(long long ticks, int nb, hipStream_t stream);
 void oneshot_destroy(int id);
 int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int K, int rope_rows, int D, int swiglu,
                           hipStream_t stream);
@@ -664,6 +667,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("oneshot_clear_error", [](int64_t id) { return oneshot_clear_error((int)id); });
   m.def("oneshot_set_poll_limit", [](int64_t id, int64_t limit) { return oneshot_set_poll_limit((int)id, limit); });
   m.def("oneshot_set_ll", [](int64_t id, bool on) { return oneshot_set_ll((int)id, on ? 1 : 0); });
+  m.def("sim_comm_spin", [](int64_t ticks, int64_t nb) {
+    const int rc = sim_comm_spin((long long)ticks, (int)nb, cur_stream());
+    TORCH_CHECK(rc == 0, "sim_comm_spin failed (rc=", rc, ")");
+  });
+  m.def("oneshot_epoch", [](int64_t id) { return (int64_t)oneshot_epoch((int)id); });
+  m.def("oneshot_resync", [](int64_t id, int64_t epoch) { return oneshot_resync((int)id, (long long)epoch); });
   m.def("oneshot_destroy", [](int64_t id) { oneshot_destroy((int)id); });
   m.def("decode_advance", &decode_advance, py::arg("out"), py::arg("ids"), py::arg("positions"), py::arg("ctx_lens"),
         py::arg("step"), py::arg("next"), py::arg("slots") = py::none(), py::arg("offsets") = py::none(),

@@ -499,6 +499,52 @@ int oneshot_clear_error(int id) {
   return hipMemset(c->err, 0, sizeof(int)) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -2;
 }
 
+// This rank's device call counter (the epoch of its last completed call). Host read, synchronous.
+long long oneshot_epoch(int id) {
+  Comm* c = get(id);
+  if (c == nullptr) return -1;
+  uint32_t e = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&e, c->ctr, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return -2;
+  return (long long)e;
+}
+
+// Re-arm this rank's side of the comm at an epoch the group agreed on (parallel/oneshot.py
+// resync: every rank quiesced and past a group barrier, then this, then a second barrier): the call
+// counter becomes `epoch`, the done counter and the expiry flag 0, and every receive buffer this
+// rank owns — flags, tile flags, gather flags, LL (word, epoch) pairs — is zeroed, so no stale tag
+// of a call some rank issued alone can match a future epoch. Local memory only.
+int oneshot_resync(int id, long long epoch) {
+  Comm* c = get(id);
+  if (c == nullptr || epoch < 0 || epoch > 0xffffffffll) return -1;
+  const uint32_t ctr[2] = {(uint32_t)epoch, 0u};
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemset(c->flags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->tflags, 0, tflag_bytes(*c)) != hipSuccess ||
+      hipMemset(c->gflags, 0, flag_bytes(*c)) != hipSuccess || hipMemset(c->ll, 0, ll_bytes(*c)) != hipSuccess ||
+      hipMemcpy(c->ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->err, 0, sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return -3;
+  return 0;
+}
+
+// ---- device-side stand-in for a collective (bench.py --simulate-tp, parallel/tp.py SimulatedTP) ----
+// One process computes rank 0's shard of a tp = N engine; every collective becomes this kernel: `nb`
+// workgroups (the K9 launch's own count for the message) each hold their CU for `ticks` of the
+// 100 MHz s_memrealtime clock, then exit — the step pays the collective's latency INSIDE the captured
+// graph, on the stream, occupying the CUs a real K9 call occupies, so a schedule that overlaps
+// communication with other work (a second stream) can be measured on one GPU.
+__global__ void __launch_bounds__(64) sim_comm_spin_kernel(long long ticks) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+int sim_comm_spin(long long ticks, int nb, hipStream_t stream) {
+  if (nb < 1 || nb > 1024 || ticks < 0) return -1;
+  hipLaunchKernelGGL(sim_comm_spin_kernel, dim3(nb), dim3(64), 0, stream, ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
 // Flag-wait bound in poll iterations (fault-injection tests force an expiry with a tiny bound).
 int oneshot_set_poll_limit(int id, long long limit) {
   Comm* c = get(id);

@@ -229,13 +229,16 @@ RT_DEVICE void chunk_range(int V, int c, int& lo, int& hi) {
   hi = min(V, lo + per);
 }
 
-// order-preserving unsigned key of a float (larger value -> larger key; -inf > 0 = "no entry")
-RT_DEVICE uint32_t okey(float v) {
+// order-preserving unsigned key of a float (larger value -> larger key; -inf > 0 = "no entry").
+// lo = 16 for bf16 rows: the key's low half carries no order and is cleared, so equal values have
+// equal keys whatever their sign (a negative value's ~u would otherwise set the low half to 0xFFFF
+// and every tie at a threshold t with a clear low half would compare ABOVE t)
+RT_DEVICE uint32_t okey(float v, int lo) {
   const uint32_t u = __float_as_uint(v);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) & ~((1u << lo) - 1u);
 }
-RT_DEVICE float okey_value(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+RT_DEVICE float okey_value(uint32_t k, int lo) {
+  return __uint_as_float(((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k) & ~((1u << lo) - 1u));
 }
 
 // The largest t with #{i < n : keys[i] >= t} >= need (the need-th largest key; need <= n), two
@@ -572,7 +575,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
       am_merge(am, v, i);
       mn = fminf(mn, v);
       am_merge(gb, v * invT + gumbel(key, (uint32_t)i), i);
-      if (lst) okeys[i - lo] = okey(v);
+      if (lst) okeys[i - lo] = okey(v, KLO);
     });
     gb = block_argmax(gb, sv, si);
     mn = -block_max_dpp(-mn, red);
@@ -626,10 +629,12 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int i = i0 + (int)threadIdx.x + j * NT;
-          if (kk[j] > kc) {
+          if (kk[j] > kc) {   // fewer than need <= KMAX < LCAP such keys; bounded all the same
             const int sl = atomicAdd(&s_ln, 1);
-            s_lk[sl] = kk[j];
-            s_li[sl] = lo + i;
+            if (sl < LCAP) {
+              s_lk[sl] = kk[j];
+              s_li[sl] = lo + i;
+            }
           } else if (kk[j] == kc && i < n) {
             const int sl = atomicAdd(&s_lt, 1);
             if (sl < LCAP) {
@@ -863,7 +868,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
         ArgMax r{-INFINITY, 0x7fffffff};
         for (int e = threadIdx.x; e < C * LCAP; e += NT) {
           const uint32_t kk = lk[e];
-          if (kk >= kg) am_merge(r, (okey_value(kk) - mx) * invT + gumbel(key, (uint32_t)li[e]), li[e]);
+          if (kk >= kg) am_merge(r, (okey_value(kk, KLO) - mx) * invT + gumbel(key, (uint32_t)li[e]), li[e]);
         }
         r = block_argmax(r, sv, si);
         cand = r.i != 0x7fffffff ? r.i : -1;
@@ -903,7 +908,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
                 const int e = cc * LCAP + lane + 64 * r;
                 ak[base + pos[q][r]] = lk[e];
                 ai[base + pos[q][r]] = li[e];
-                aw[base + pos[q][r]] = __expf((okey_value(lk[e]) - mx) * invT);
+                aw[base + pos[q][r]] = __expf((okey_value(lk[e], KLO) - mx) * invT);
               }
             }
           }
@@ -916,7 +921,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
             const uint32_t mk = ak[t];
             float above = 0.f;
             for (int j = 0; j < tot; ++j) above += ak[j] > mk ? aw[j] : 0.f;
-            if (above < p * zsum) am_merge(r, (okey_value(mk) - mx) * invT + gumbel(key, (uint32_t)ai[t]), ai[t]);
+            if (above < p * zsum) am_merge(r, (okey_value(mk, KLO) - mx) * invT + gumbel(key, (uint32_t)ai[t]), ai[t]);
           }
           r = block_argmax(r, sv, si);
           cand = r.i != 0x7fffffff ? r.i : -1;

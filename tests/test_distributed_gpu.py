@@ -233,3 +233,27 @@ def test_fused_ar_four_ranks_on_one_gpu_is_contained():
     # agreed device-wait failure: the expiring rank names K9, its peers "a peer rank's device
     # wait expired" (Engine.device_flag_errors)
     assert all("K9" in e or "device wait expired" in e for e in errs), errs
+
+
+def test_k9_epoch_desync_fails_one_turn_then_resyncs_on_shared_gpu():
+    """VERDICT r4 #3 / advisor r4: the K9 call counter is device-local, so one extra call on ONE
+    rank (injected: ``0:k9-extra@0``) leaves the group's epochs apart — every later call would pair
+    with the wrong peer call and the last one waits for an epoch the peer never writes. That turn
+    must fail on every rank (agreed expiry), the group must re-agree its counters
+    (OneShotAllReduce.resync: group max, buffers zeroed), and the NEXT turns must succeed with no
+    flag error: round 1 (warm-up) fails for the table's 3 knights, timed rounds 2-3 decode fully."""
+    env_old = {k: os.environ.get(k) for k in ("ROUNDTABLE_ENGINE_FAULTS", "ROUNDTABLE_K9_POLL_LIMIT")}
+    os.environ["ROUNDTABLE_ENGINE_FAULTS"] = "0:k9-extra@0"
+    os.environ["ROUNDTABLE_K9_POLL_LIMIT"] = "300000"
+    try:
+        out = _bench()
+    finally:
+        for k, v in env_old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    d = out["detail"]
+    assert d["k9_oneshot"], out["_log"]
+    assert d["failed_turns"] == 3 and d["k9_resyncs"] >= 1, out["_log"]
+    assert d["decode_tokens"] == 3 * 16 * 2, out["_log"]

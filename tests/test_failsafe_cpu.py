@@ -61,40 +61,81 @@ def test_bench_raise_on_rank_zero_mid_run():
     assert out["failed_stage"] == "round 3" and out["failed_rank"] == 0
 
 
-def _capture_worker(rank, world, port, q):
+class _FakeK9:
+    """Stand-in for the K9 comm: a host call counter; resync() is the real agreement shape (group
+    MAX over the TP group, then a second all-reduce as the barrier)."""
+
+    def __init__(self, group, calls):
+        self.group, self.calls, self.resyncs = group, calls, 0
+
+    def resync(self):
+        t = torch.tensor([float(self.calls)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self.calls = int(t.item())
+        dist.all_reduce(torch.zeros(1, dtype=torch.float64), group=self.group)
+        self.resyncs += 1
+        return True
+
+
+def _capture_worker(rank, world, port, q, where):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from theroundtaible_amd.engine import graphs
         from theroundtaible_amd.engine.engine import Engine
         from theroundtaible_amd.engine import EngineConfig
         from theroundtaible_amd.parallel.tp import TPInfo
-        # the agreement logic alone: an engine shell whose capture fails on rank 1 only
+
+        class CountingTP(TPInfo):
+            agreements = 0
+
+            def any_rank(self, flag):
+                CountingTP.agreements += 1
+                return super().any_rank(flag)
+
+        # the agreement logic alone: an engine shell whose graph set-up fails on rank 1 only,
+        # either allocating the graph's buffers or inside the capture (whose eager warm-up runs
+        # issue K9 calls: rank 0 has issued 4 of them, rank 1 only 1)
         e = object.__new__(Engine)
         e.on_gpu = True
         e.ecfg = EngineConfig(device="cpu")
-        e.tp = TPInfo(size=world, rank=rank, group=dist.group.WORLD)
-        e.graphs = {"stale": object()}
+        e.tp = CountingTP(size=world, rank=rank, group=dist.group.WORLD)
+        e.tp.oneshot = _FakeK9(dist.group.WORLD, 10)
+        e.graphs = {(0, 8, False, False): "cached graph"}
         e.stats = {}
+        e._graph_key = lambda B, grouped, dist_greedy: (B, 8, grouped, dist_greedy)
 
-        def graph_for(B, max_ctx, grouped=False, dist_greedy=False):
-            if rank == 1:
-                raise RuntimeError("operation not permitted when stream is capturing")
-            return "graph"
+        class FakeGraph:
+            def __init__(self, engine, bucket, splits, grouped=False, dist_greedy=False, capture=True):
+                if where == "alloc" and rank == 1:
+                    raise RuntimeError("HIP out of memory allocating the graph's buffers")
 
-        e._graph_for = graph_for
+            def capture(self):
+                e.tp.oneshot.calls += 1 if rank == 1 else 4
+                if where == "capture" and rank == 1:
+                    raise RuntimeError("operation not permitted when stream is capturing")
+
+        graphs.DecodeGraph = FakeGraph
+        cached = e._agreed_graph(0, 100, False, False)
+        n_cached = CountingTP.agreements
         got = e._agreed_graph(3, 100, True, False)
-        q.put((rank, got, e.ecfg.use_graphs, len(e.graphs), e.stats.get("capture_fallbacks")))
+        q.put((rank, cached, n_cached, got, e.ecfg.use_graphs, len(e.graphs), e.stats.get("capture_fallbacks"),
+               e.tp.oneshot.calls, e.tp.oneshot.resyncs))
     finally:
         dist.destroy_process_group()
 
 
-def test_capture_fallback_is_agreed_by_the_group():
-    """A capture that fails on ONE rank of a TP group sends every rank to eager decode (the ranks
-    that captured drop their graphs): no rank replays K9 calls its peers never issue."""
+@pytest.mark.parametrize("where", ["alloc", "capture"])
+def test_capture_fallback_is_agreed_by_the_group(where):
+    """A graph set-up that fails on ONE rank of a TP group sends every rank to eager decode (the
+    ranks that captured drop their graphs): no rank replays K9 calls its peers never issue. A
+    failure inside the capture (after the warm-up's K9 calls) also re-agrees the ranks' K9 call
+    counters (advisor r4: the counters drifted apart and every later call waited out its bound);
+    a buffer failure is agreed before any call is issued. A cached graph costs no agreement."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_capture_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_capture_worker, args=(r, 2, port, q, where)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in range(2)))
@@ -102,8 +143,13 @@ def test_capture_fallback_is_agreed_by_the_group():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank in (0, 1):
-        got, use_graphs, n_graphs, fallbacks = res[rank]
+        cached, n_cached, got, use_graphs, n_graphs, fallbacks, calls, resyncs = res[rank]
+        assert cached == "cached graph" and n_cached == 0, res[rank]
         assert got is None and use_graphs is False and n_graphs == 0 and fallbacks == 1, (rank, res[rank])
+        if where == "capture":
+            assert resyncs == 1 and calls == 14, res[rank]      # both ranks at the group max
+        else:
+            assert resyncs == 0 and calls == 10, res[rank]      # no call was issued
 
 
 def _pool_worker(rank, world, port, q):
@@ -216,3 +262,36 @@ def test_config5_topology_two_tp_groups(nproc, tp):
     assert all((c > 0) == (r in lead) for r, c in enumerate(contrib)), contrib
     assert d["decode_tokens"] == one["detail"]["decode_tokens"]
     assert d["transcript_sha"] == one["detail"]["transcript_sha"]
+
+
+def test_discuss_tp2_knight_skipped_when_a_rank_stalls(tmp_path):
+    """containment outside the bench. A plain ``roundtable discuss`` whose Groot
+    knight is tensor-parallel over 2 ranks; rank 1 stalls for 20 s on entering round 1's turn
+    (before any collective of it). Every rank of Groot's group takes the SAME decision at the
+    turn-start rendezvous (launcher store, knights/distributed.py): the turn is skipped with a
+    timeout error after the 6-s turn timeout on rank 0 (the reference skips a failed knight and the
+    round goes on, /root/reference/src/orchestrator.ts:521-535), the late rank joins that decision
+    instead of entering collectives its peer abandoned, Klein (tp 1) speaks, and round 2 runs
+    with both knights."""
+    from test_distributed_cpu import _tp_project
+    _tp_project(tmp_path, {"Groot": {"tp": 2}, "Klein": {}})
+    cfg_path = tmp_path / ".roundtable" / "config.json"
+    cfg = json.loads(cfg_path.read_text())
+    cfg["rules"].update(max_rounds=2, timeout_per_turn_seconds=6)
+    cfg_path.write_text(json.dumps(cfg))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               ROUNDTABLE_BENCH_FAULT="1:turn 1:sleep20")
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-m", "theroundtaible_amd", "discuss", "TP onderwerp", "--no-read-codebase",
+                        "--choice", "4"], capture_output=True, text=True, timeout=400, env=env, cwd=str(tmp_path))
+    took = time.monotonic() - t0
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    sessions = os.listdir(tmp_path / ".roundtable" / "sessions")
+    disc = (tmp_path / ".roundtable" / "sessions" / sessions[0] / "discussion.md").read_text()
+    assert "Round 1 — Klein" in disc and "Round 1 — Groot" not in disc, disc[:2000]
+    assert "Round 2 — Groot" in disc and "Round 2 — Klein" in disc, disc[:2000]
+    assert "did not reach the turn within 6 s" in r.stdout + r.stderr, r.stdout[-2000:]
+    # timestamped stage transitions name where each rank is
+    assert "stage 'turn 1'" in r.stderr and "stage 'turn 2'" in r.stderr
+    assert took < 200, took

@@ -379,13 +379,20 @@ def test_sample_topk_lists_match_reference(dtype):
     ties at the cut, so the histogram path decides) and a near-flat row. Draw for draw against
     the fp64 reference."""
     B, V = 8, 128256
+    B = 11
     logits = bf(B, V, scale=2.0, seed=123).float()
     logits[1] *= 0.05
     logits[2] = torch.round(logits[2] * 2) / 2
+    # rows whose whole top k is NEGATIVE (log-prob-like inputs), with many exact ties at the
+    # chunks' k-th value: a negative value's order key must compare EQUAL to a tie at the cut,
+    # not above it (advisor r4: the 'above' list then overflowed its LDS slots)
+    logits[8] = torch.round(logits[8] * 4) / 4 - 20.0
+    logits[9] = torch.round(logits[9]) - 9.0
+    logits[10] = torch.round(logits[10] * 8) / 8 - 3.0
     logits = logits.to(dtype)
     temp = torch.full((B,), 0.8, device=DEV)
-    top_k = torch.tensor([1, 5, 40, 64, 40, 64, 2, 17], dtype=torch.int32, device=DEV)
-    top_p = torch.tensor([1.0, 1.0, 1.0, 0.9, 0.5, 1.0, 0.7, 0.95], device=DEV)
+    top_k = torch.tensor([1, 5, 40, 64, 40, 64, 2, 17, 40, 64, 9], dtype=torch.int32, device=DEV)
+    top_p = torch.tensor([1.0, 1.0, 1.0, 0.9, 0.5, 1.0, 0.7, 0.95, 1.0, 0.9, 1.0], device=DEV)
     ws = ops.sample_workspace(B, DEV)
     hits = total = 0
     for rep in range(6):

@@ -31,11 +31,33 @@ def spmd_cluster(config=None):
     if _CLUSTER is None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         from .parallel.cluster import init_cluster
         cpu = False
+        timeout = 1800
         if config is not None:
-            from .parallel.launch import ranks_needed
+            from .parallel.launch import collective_timeout_s, ranks_needed
             cpu = ranks_needed(config)[2]
-        _CLUSTER = init_cluster(prefer_gpu=not cpu)
+            timeout = collective_timeout_s(config)
+        _CLUSTER = init_cluster(prefer_gpu=not cpu, timeout_s=timeout)
+        _start_guard(_CLUSTER, config)
     return _CLUSTER
+
+
+def _start_guard(cl, config) -> None:
+    """Containment for SPMD commands (utils/failsafe.py, as in bench.py): engine loading, K9
+    set-up, graph capture and every turn batch run under time limits on every rank; a rank that
+    raises or stalls past its limit ends the whole command with one message naming the stage and
+    rank (exit code 2), instead of its peers waiting in a collective. Turn batches carry their own
+    limit (knights/distributed.py: the turn timeout per knight group, plus margin)."""
+    if cl is None or not cl.distributed:
+        return
+    from .utils import failsafe
+    t = float(getattr(getattr(config, "rules", None), "timeout_per_turn_seconds", 120) or 120)
+
+    def report(rec: dict) -> None:
+        sys.stderr.write(f"roundtable: rank {rec.get('failed_rank')} failed at stage {rec.get('failed_stage')!r}: "
+                         f"{rec.get('error')}\n")
+
+    failsafe.RunGuard(cl.rank, cl.world, report, default_s=float("inf"), exit_code=2,
+                      limits={"engine_load": 900.0, "k9_create": 900.0, "capture": t + 120.0}).start()
 
 
 def make_backends(config, ui: UI, args, only_knight: Optional[str] = None):
@@ -75,7 +97,8 @@ def ask(ui: UI, question: str, default: str = "") -> str:
         except (EOFError, OSError):
             line = None
     if _CLUSTER is not None and _CLUSTER.distributed:
-        line = _CLUSTER.broadcast_object(line, src=0)   # every rank takes the King's answer
+        # every rank takes the King's answer (a person: no containment timeout on this wait)
+        line = _CLUSTER.broadcast_object(line, src=0, wait=True)
     if not line:
         return default
     return line.strip() or default
@@ -793,6 +816,11 @@ def main(argv: Optional[List[str]] = None) -> int:
             import traceback
             traceback.print_exc()
         return get_exit_code(e)
+    finally:
+        from .utils import failsafe
+        g = failsafe.guard()
+        if g is not None:
+            g.finish()
 
 
 if __name__ == "__main__":

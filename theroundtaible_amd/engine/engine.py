@@ -156,9 +156,13 @@ class Engine:
                       "speculative_tokens": 0, "speculative_kept": 0}
         self._calls = 0
         self.faults = dict(ecfg.faults)
+        # "<call>:<kind>[@<tp rank>]": a fault restricted to one rank of a tensor-parallel group
+        # (e.g. "0:k9-extra@0" desynchronises the group's K9 call counters)
         for item in filter(None, os.environ.get("ROUNDTABLE_ENGINE_FAULTS", "").split(",")):
             k, _, v = item.partition(":")
-            self.faults[int(k)] = v.strip()
+            v, _, only = v.strip().partition("@")
+            if not only or int(only) == self.tp.rank:
+                self.faults[int(k)] = v
         self.debug_checks = ecfg.debug_checks or os.environ.get("ROUNDTABLE_DEBUG_CHECKS") == "1"
 
     # ---- memory ----------------------------------------------------------------------------
@@ -506,7 +510,11 @@ class Engine:
             # a bounded device-side wait expired: this turn's tokens are wrong. Fail the turn,
             # drop its KV (the knight re-prefills next turn) AND every shared-prefix sequence the
             # call prefilled — its all-reduces may have summed stale data, and sync_shared would
-            # hand that KV to every member of the table by LCP. The engine itself stays usable.
+            # hand that KV to every member of the table by LCP. The engine itself stays usable:
+            # an expiry the group agreed on (check_device_flags) may mean the ranks' K9 call
+            # counters diverged, so the group re-agrees them before the next turn
+            if getattr(e, "agreed", False):
+                self._resync_k9()
             lru = self.__dict__.get("_shared_lru", {})
             for t in turns:
                 self.release(t.seq_key)
@@ -547,6 +555,9 @@ class Engine:
         for key in list(self.kv.seqs):
             self.kv.free_seq(key)
         self.graphs.clear()
+        # the failed work may have left the ranks' K9 call counters apart (calls one rank issued
+        # alone): the recovered group starts from one agreed epoch
+        self._resync_k9()
         self.healthy = True
         return True
 
@@ -565,6 +576,11 @@ class Engine:
             raise RuntimeError(f"HIP error: injected unrecoverable device fault at call {call}")
         if f == "flag":             # a bounded device-side wait expired (K9 / persistent kernel)
             raise DeviceFlagError("engine", f"injected poll expiry at call {call}", kind="device")
+        if f == "k9-extra":         # one K9 call on THIS rank alone: the group's call counters diverge
+            os_ = self.tp.oneshot
+            if os_ is not None:
+                os_(torch.zeros(os_.world * 64, dtype=torch.bfloat16, device=self.device))
+            return
         raise AdapterError("engine", f"injected failure at call {call}", kind="unknown")
 
     def check_paging(self, block_tables: torch.Tensor, slots: Sequence[int]) -> None:
@@ -717,8 +733,30 @@ class Engine:
     def check_device_flags(self) -> None:
         msgs = self.device_flag_errors()
         if self.tp.any_rank(bool(msgs)):     # every rank of a TP knight fails the turn together
-            raise DeviceFlagError("engine", "; ".join(msgs) or "a peer rank's device wait expired",
+            err = DeviceFlagError("engine", "; ".join(msgs) or "a peer rank's device wait expired",
                                   kind="device")
+            err.agreed = True
+            raise err
+
+    def _resync_k9(self) -> None:
+        """Collective over the TP group (every rank calls it at the same point): re-agree the K9
+        call counter (:meth:`OneShotAllReduce.resync`). If any rank cannot, the group drops K9
+        together — RCCL / host collectives from then on, and (a gloo rehearsal group, whose
+        captured step needs K9) eager decode; captured graphs referencing the comm are dropped."""
+        os_ = self.tp.oneshot
+        if self.tp.size == 1 or os_ is None or not self.on_gpu:
+            return
+        self.stats["k9_resyncs"] = self.stats.get("k9_resyncs", 0) + 1
+        if os_.resync():
+            return
+        import warnings
+        warnings.warn("K9 one-shot comm could not be re-armed on every rank: the group falls back to "
+                      "process-group collectives")
+        os_.close()
+        self.tp.oneshot = None
+        self.graphs.clear()
+        if self.tp.backend() != "nccl":
+            self.ecfg.use_graphs = False
 
     # ---- continuous batching (serve.py): admit / step in chunks / retire ----------------------------
     def _on_stream(self):
@@ -921,13 +959,27 @@ class Engine:
                 out[b].append(int(x))
             lens = [l + 1 for l in lens]
             if step % self.ecfg.sync_every == 0:
-                if time.perf_counter() > deadline:
+                if self.past_deadline(deadline, step // self.ecfg.sync_every):
                     self._unwind(seqs)
                     raise EngineTimeout("engine", "turn exceeded timeout_per_turn_seconds")
                 done = [d or _finished(o, t.params, eos, self.tokenizer) for d, o, t in zip(done, out, turns)]
                 if all(done):
                     break
         return out
+
+    DEADLINE_AGREE_EVERY = 8   # tensor-parallel groups agree on the turn deadline every 8th check
+
+    def past_deadline(self, deadline: float, check: int) -> bool:
+        """The decode loop's wall-clock check (every chunk). A tensor-parallel group must stop at
+        the SAME step on every rank — one rank leaving the loop alone would leave its peers'
+        remaining K9 calls unanswered — so its ranks decide together, every
+        ``DEADLINE_AGREE_EVERY``-th check (one small collective per ~256 steps; the turn may
+        overrun its limit by that many steps)."""
+        if self.tp.size == 1:
+            return time.perf_counter() > deadline
+        if check % self.DEADLINE_AGREE_EVERY:
+            return False
+        return self.tp.any_rank(time.perf_counter() > deadline)
 
     def _unwind(self, seqs):
         # the knights' tokens were not extended; drop the blocks pre-allocated for generation
@@ -950,40 +1002,61 @@ class Engine:
 
     def _agreed_graph(self, B: int, max_ctx: int, grouped: bool, dist_greedy: bool):
         """The captured decode step, or None (eager). A capture that fails on ANY rank of a
-        tensor-parallel group sends EVERY rank to eager decode (one agreement round): a rank
-        replaying a graph whose K9 calls no peer issues would wait out each poll bound."""
+        tensor-parallel group sends EVERY rank to eager decode: a rank replaying a graph whose K9
+        calls no peer issues would wait out each poll bound. The group agrees twice, only when the
+        graph is not cached (cache keys are the same on every rank, so all ranks miss together and
+        a cached replay costs no host round trip): after the graph's buffers are allocated (where
+        an out-of-memory rank fails, before any K9 call) and after the capture itself, whose eager
+        warm-up runs issue K9 calls — a rank failing in there leaves the counters apart, so the
+        fallback re-agrees them (:meth:`_resync_k9`)."""
         if not (self.on_gpu and self.ecfg.use_graphs):
             return None
-        runner, err = None, None
+        key = self._graph_key(B, grouped, dist_greedy)
+        g = self.graphs.get(key)
+        if g is not None:
+            return g
+        from .graphs import DecodeGraph
+        g, err = None, None
         try:
             with failsafe.stage("capture"):
-                runner = self._graph_for(B, max_ctx, grouped=grouped, dist_greedy=dist_greedy)
-        except RuntimeError as e:   # e.g. a collective that refuses stream capture
+                g = DecodeGraph(self, key[0], key[1], grouped=grouped, dist_greedy=dist_greedy, capture=False)
+        except RuntimeError as e:   # out of memory for the graph's static buffers
             err = e
-        if self.tp.size > 1:
-            failed = self.tp.any_rank(err is not None)
-        else:
-            if err is not None:
-                raise err
-            failed = False
+        failed = self.tp.any_rank(err is not None) if self.tp.size > 1 else err is not None
+        calls_issued = False
+        if not failed:
+            try:
+                with failsafe.stage("capture"):
+                    calls_issued = True
+                    g.capture()
+            except RuntimeError as e:   # e.g. a collective that refuses stream capture
+                err = e
+            failed = self.tp.any_rank(err is not None) if self.tp.size > 1 else err is not None
         if failed:
+            if self.tp.size == 1:
+                raise err
             import warnings
             warnings.warn(f"hipGraph capture failed on a rank of the tp={self.tp.size} group "
                           f"({err if err is not None else 'peer rank'}); every rank decodes eagerly")
             self.ecfg.use_graphs = False
             self.graphs.clear()
             self.stats["capture_fallbacks"] = self.stats.get("capture_fallbacks", 0) + 1
+            if calls_issued:
+                self._resync_k9()
             return None
-        return runner
+        self.graphs[key] = g
+        return g
+
+    def _graph_key(self, B: int, grouped: bool, dist_greedy: bool) -> Tuple[int, int, bool, bool]:
+        bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
+        return (bucket, ops.decode_splits(bucket, self.model.n_kv_heads, grouped=grouped), grouped, dist_greedy)
 
     def _graph_for(self, B: int, max_ctx: int, grouped: bool = False, dist_greedy: bool = False) -> "DecodeGraph":
         from .graphs import DecodeGraph
-        bucket = next((b for b in BATCH_BUCKETS if b >= B), B)
-        splits = ops.decode_splits(bucket, self.model.n_kv_heads, grouped=grouped)
-        key = (bucket, splits, grouped, dist_greedy)
+        key = self._graph_key(B, grouped, dist_greedy)
         g = self.graphs.get(key)
         if g is None:
-            g = DecodeGraph(self, bucket, splits, grouped=grouped, dist_greedy=dist_greedy)
+            g = DecodeGraph(self, key[0], key[1], grouped=grouped, dist_greedy=dist_greedy)
             self.graphs[key] = g
         return g
 

@@ -54,7 +54,8 @@ def no_gc_during_capture():
 
 
 class DecodeGraph:
-    def __init__(self, engine, bucket: int, splits: int, grouped: bool = False, dist_greedy: bool = False):
+    def __init__(self, engine, bucket: int, splits: int, grouped: bool = False, dist_greedy: bool = False,
+                 capture: bool = True):
         self.engine = engine
         self.B = bucket
         self.splits = splits
@@ -93,6 +94,10 @@ class DecodeGraph:
         self.sample_ws = ops.sample_workspace(B, dev)      # self-re-arming K6 tickets
         self.graph = None
         self._host_out: List[torch.Tensor] = []
+        if capture:     # (Engine._agreed_graph agrees on the buffers first, then captures)
+            self._capture()
+
+    def capture(self) -> None:
         self._capture()
 
     def _fused(self) -> bool:
@@ -240,7 +245,7 @@ class DecodeGraph:
             if i % chunk == 0:
                 if engine.debug_checks:
                     self.check_guard()
-                if time.perf_counter() > deadline:
+                if engine.past_deadline(deadline, i // chunk):
                     engine._sync()
                     raise EngineTimeout("engine", "turn exceeded timeout_per_turn_seconds")
                 if need_tokens:

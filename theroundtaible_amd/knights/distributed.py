@@ -22,19 +22,26 @@ from typing import Dict, List, Optional, Sequence, Tuple, Union  # noqa: F401
 from ..errors import AdapterError
 from ..parallel.cluster import Cluster
 from ..parallel.exchange import TokenExchange, exchange_token_ids
-from ..utils import trace
+from ..utils import failsafe, trace
 from .base import KnightBackend, TurnRequest, TurnResult
 
 
 class DistributedPool:
     def __init__(self, cluster: Cluster, placement: Dict[str, List[int]], local: Dict[str, KnightBackend],
-                 tokenizer=None, max_reply_tokens: int = 4096):
+                 tokenizer=None, max_reply_tokens: int = 4096, turn_rendezvous: bool = False):
         """``placement``: knight name -> ranks hosting it (first = leader). ``local``: name -> backend here.
-        ``max_reply_tokens``: width of the static C1 buffers (longer replies take the shape-agreeing path)."""
+        ``max_reply_tokens``: width of the static C1 buffers (longer replies take the shape-agreeing path).
+        ``turn_rendezvous``: every tensor-parallel group agrees, through the launcher's key-value store
+        and within the turn timeout, that ALL its ranks reached a turn before any of them enters its
+        collectives (``roundtable discuss`` & co.; see :meth:`_rendezvous`)."""
         self.cluster = cluster
         self.placement = placement
         self.local = local
         self.tokenizer = tokenizer
+        self.turn_rendezvous = turn_rendezvous and cluster.distributed
+        self._rv_count: Dict[tuple, int] = {}
+        self._calls = 0
+        self.rendezvous_skips = 0
         self.exchange_ms: List[float] = []
         self.exchange: Optional[TokenExchange] = None
         self.events: List[str] = []     # C1 ordering record (c1_start / speculate / c1_wait)
@@ -93,9 +100,39 @@ class DistributedPool:
         if len(self.events) > 4096:
             del self.events[:1024], self.event_ns[:1024]
 
+    def _rendezvous(self, ranks: tuple, wait_s: float) -> bool:
+        """Turn-start agreement of one tensor-parallel group, outside its process groups (the
+        launcher's TCP key-value store): each rank counts itself in, and the FIRST rank to see
+        either every rank arrived ("go") or its wait expire ("skip") fixes the decision with one
+        compare-and-set; every rank — a late one included — takes that decision. A rank that
+        stalls before a turn (a hung host call, a slow previous step) thus makes the whole group
+        skip the turn with a timeout error within ``wait_s``, instead of its peers blocking inside
+        the turn's first collective for the process-group timeout, and a late rank never enters
+        collectives its peers have abandoned (reference: a failed turn is skipped and the round
+        continues, /root/reference/src/orchestrator.ts:521-535)."""
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+        n = self._rv_count[ranks] = self._rv_count.get(ranks, 0) + 1
+        key = f"rt/turn/{'-'.join(map(str, ranks))}/{n}"
+        store.add(key + "/n", 1)
+        deadline = time.monotonic() + wait_s
+        while True:
+            if store.check([key + "/d"]):
+                dec = store.get(key + "/d")
+                break
+            if store.add(key + "/n", 0) >= len(ranks):
+                dec = store.compare_set(key + "/d", "", "go")
+                break
+            if time.monotonic() > deadline:
+                dec = store.compare_set(key + "/d", "", "skip")
+                break
+            time.sleep(0.002)
+        return dec == b"go"
+
     def execute_round(self, pairs: Sequence[Tuple["RemoteKnight", TurnRequest]],
                       timeout_s: float) -> List[Union[TurnResult, BaseException]]:
         rank = self.cluster.rank
+        self._calls += 1
         mine_idx = [i for i, (k, _) in enumerate(pairs) if rank in self.placement[k.knight_name]]
         local_res: Dict[int, Union[TurnResult, BaseException]] = {}
         # group local work by underlying backend group (one batched decode per engine)
@@ -103,11 +140,32 @@ class DistributedPool:
         for i in mine_idx:
             b = self.local[pairs[i][0].knight_name]
             groups.setdefault(b.group_key(), []).append(i)
-        for idxs in groups.values():
-            first = self.local[pairs[idxs[0]][0].knight_name]
-            outs = first.execute_group([(self.local[pairs[i][0].knight_name], pairs[i][1]) for i in idxs], timeout_s)
-            for i, o in zip(idxs, outs):
-                local_res[i] = o
+        # tensor-parallel groups first, in one global order (their placements sorted), so a
+        # group's k-th place bounds when its ranks can all arrive: k turns of at most timeout_s
+        # each; single-rank engines after them
+        tp_order = sorted({tuple(self.placement[k.knight_name]) for k, _ in pairs
+                           if len(self.placement[k.knight_name]) > 1})
+
+        def place(idxs):
+            pl = tuple(self.placement[pairs[idxs[0]][0].knight_name])
+            return tp_order.index(pl) if pl in tp_order else len(tp_order)
+
+        budget = (len(tp_order) + 1) * timeout_s + 30.0
+        with failsafe.stage(f"turn {self._calls}", limit_s=budget if self.turn_rendezvous else None):
+            for idxs in sorted(groups.values(), key=place):
+                first = self.local[pairs[idxs[0]][0].knight_name]
+                ranks = tuple(self.placement[pairs[idxs[0]][0].knight_name])
+                if self.turn_rendezvous and len(ranks) > 1 and not self._rendezvous(ranks, (place(idxs) + 1) * timeout_s):
+                    self.rendezvous_skips += 1
+                    for i in idxs:
+                        local_res[i] = AdapterError(pairs[i][0].name, f"a rank of its tensor-parallel group {list(ranks)} "
+                                                    f"did not reach the turn within {timeout_s:.0f} s; turn skipped "
+                                                    "on every rank of the group", kind="timeout")
+                    continue
+                outs = first.execute_group([(self.local[pairs[i][0].knight_name], pairs[i][1]) for i in idxs],
+                                           timeout_s)
+                for i, o in zip(idxs, outs):
+                    local_res[i] = o
         if len(mine_idx) == len(pairs) and all(len(self.placement[k.knight_name]) == self.cluster.world
                                                for k, _ in pairs):
             # every knight of the batch spans EVERY rank (one tensor-parallel group: the strong-

@@ -28,6 +28,7 @@ from ..parallel.cluster import Cluster
 from ..parallel.tp import TPInfo
 from ..types import RoundtableConfig
 from ..utils.local_detect import resolve_model
+from ..utils import failsafe
 from ..utils.ui import NULL_UI, UI
 from .distributed import DistributedPool, RemoteKnight
 from .engine_backend import EngineBackend
@@ -92,7 +93,8 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
                                 model_overrides=overrides)
             if not ecfg.device.startswith("cuda"):
                 ecfg.dtype = "fp32"
-            engines[ekey] = (Engine(ecfg, tp), threading.Lock())
+            with failsafe.stage("engine_load"):
+                engines[ekey] = (Engine(ecfg, tp), threading.Lock())
         engine, lock = engines[ekey]
         tokenizer = tokenizer or engine.tokenizer
         params = SamplingParams(temperature=float(st.get("temperature", 0.7)), top_p=float(st.get("top_p", 0.95)),
@@ -109,6 +111,9 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         st = engine_settings(config, config.knights[0].adapter)
         model, overrides = resolve_model(st["model"], str(st.get("weights", "random:0")), st.get("model_overrides"))
         tokenizer = get_tokenizer(get_config(model, **overrides).vocab, str(st.get("weights", "random:0")))
-    pool = DistributedPool(cluster, placement, local, tokenizer)
+    # every tensor-parallel group agrees at each turn start that all its ranks arrived (within the
+    # turn timeout) before entering its collectives: a stalled rank skips the knight's turn on
+    # every rank instead of hanging the table
+    pool = DistributedPool(cluster, placement, local, tokenizer, turn_rendezvous=True)
     backends = {aid: RemoteKnight(pool, aid, display_name(aid, config), aid) for aid in placement}
     return backends, pool

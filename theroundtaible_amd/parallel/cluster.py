@@ -25,6 +25,10 @@ class Cluster:
     device: str = "cpu"      # this rank's device: cuda:LOCAL_RANK (or shared round-robin in rehearsal mode)
     backend: str = "none"
     cpu_group: Optional[object] = None
+    # gloo group with a very long timeout for waits on a PERSON or an idle client (the King's
+    # answer, a server's next request): the data and control collectives keep the short,
+    # containment-sized timeout of init_cluster
+    wait_group: Optional[object] = None
 
     @property
     def is_leader(self) -> bool:
@@ -35,11 +39,13 @@ class Cluster:
         return self.world > 1
 
     # ---- control plane (gloo) -------------------------------------------------------------
-    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+    def broadcast_object(self, obj: Any, src: int = 0, wait: bool = False) -> Any:
+        """``wait``: over :attr:`wait_group` (no containment timeout: rank ``src`` may be waiting
+        on a human or an HTTP client)."""
         if not self.distributed:
             return obj
         box = [obj]
-        dist.broadcast_object_list(box, src=src, group=self.cpu_group)
+        dist.broadcast_object_list(box, src=src, group=self.wait_group if wait else self.cpu_group)
         return box[0]
 
     def all_gather_object(self, obj: Any) -> List[Any]:
@@ -74,8 +80,14 @@ class Cluster:
 _CLUSTER: Optional[Cluster] = None
 
 
+WAIT_TIMEOUT_S = 7 * 24 * 3600
+
+
 def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
-    """Initialize from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); single process otherwise."""
+    """Initialize from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); single process otherwise.
+    ``timeout_s``: every collective of the world / control groups (and, by default, of TP groups
+    created later) fails after it — the commands size it from the turn timeout
+    (parallel/launch.py collective_timeout_s), so a stalled rank surfaces within minutes."""
     global _CLUSTER
     if _CLUSTER is not None:
         return _CLUSTER
@@ -103,7 +115,9 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
             kw["device_id"] = torch.device(device)
         dist.init_process_group(**kw)
         c.backend = backend
-        c.cpu_group = dist.new_group(backend="gloo") if backend == "nccl" else dist.group.WORLD
+        td = datetime.timedelta(seconds=timeout_s)
+        c.cpu_group = dist.new_group(backend="gloo", timeout=td) if backend == "nccl" else dist.group.WORLD
+        c.wait_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=WAIT_TIMEOUT_S))
     _CLUSTER = c
     return c
 

@@ -111,3 +111,26 @@ def launch_ranks(n: int, argv: List[str], cpu: bool, why: str, quiet: bool = Fal
     if not quiet:
         print(f"  Launching {n} ranks ({why})", file=sys.stderr, flush=True)
     return subprocess.run(cmd, env=env).returncode
+
+
+def collective_timeout_s(config: RoundtableConfig, world: Optional[int] = None) -> int:
+    """Process-group timeout of an SPMD command (containment outside the bench).
+    A rank waits in a collective at most while the ranks it waits for run their turns: the turn
+    timeout (``rules.timeout_per_turn_seconds``, 120 s by default) times the most knight groups one
+    rank runs one after another, plus a minute of margin — 180 s for the usual one group per rank,
+    instead of torch's 30-minute default. Waits on a person (the King) use the cluster's
+    long-timeout wait group instead."""
+    t = float(getattr(config.rules, "timeout_per_turn_seconds", 120) or 120)
+    world = world or int(os.environ.get("WORLD_SIZE", "1"))
+    per_rank = 1
+    try:
+        from ..knights.spmd import plan_placement
+        pl = plan_placement(config, max(1, world))
+        counts: dict = {}
+        for ranks in {tuple(r) for r in pl.values()}:
+            for r in ranks:
+                counts[r] = counts.get(r, 0) + 1
+        per_rank = max(counts.values(), default=1)
+    except Exception:  # noqa: BLE001 - a bad placement is reported by the backend factory
+        pass
+    return int(max(120.0, per_rank * t + 60.0))

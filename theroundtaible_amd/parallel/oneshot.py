@@ -18,9 +18,15 @@ with GEMM + K9 on this node's links, and by default only when every rank owns it
 GPU shared by two rehearsal ranks it loses by ~46 µs: the two processes' spinning grids
 co-schedule badly); ``ROUNDTABLE_FUSED_AR=0`` keeps the separate launches.
 
-LL protocol (:func:`choose_protocol`): the standalone all-reduce can carry the call's epoch in
-every 8-byte store next to the data, so receivers poll the data itself — no system fence (an
-xGMI round trip) and no separate flag. Chosen per node by an exact self-test and a timed probe.
+LL protocol (:func:`choose_protocol`): the all-reduce (standalone launch AND the fused EPI_AR
+epilogue) can carry the call's epoch in every 8-byte store next to the data, so receivers poll the
+data itself — no system fence (an xGMI round trip) and no separate flag. Chosen per node by an
+exact self-test and a timed probe; the gather keeps flags.
+
+Epoch agreement (:meth:`OneShotAllReduce.resync`): the call counter is device-local, so ranks that
+issued different numbers of calls (one rank's capture warm-up failed part-way, an abandoned turn)
+would wait on epochs their peers never write. The engine re-agrees it (group MAX, buffers zeroed)
+whenever the group recovers, falls back from a failed capture, or fails a turn on an expired wait.
 """
 from __future__ import annotations
 
@@ -82,6 +88,42 @@ class OneShotAllReduce:
         self.ll = False                             # standalone all-reduce in the LL form
         self.flag_latency_us: Optional[float] = None
         self.ll_latency_us: Optional[float] = None
+
+    group = None                                    # the TP process group (set by try_create)
+    resyncs = 0
+
+    def epoch(self) -> int:
+        """This rank's device call counter (host read; synchronises the device)."""
+        e = int(self._nat.oneshot_epoch(self.id))
+        if e < 0:
+            raise RuntimeError(f"oneshot_epoch failed (rc={e})")
+        return e
+
+    def resync(self) -> bool:
+        """Collective over the TP group: re-agree the call counter after ranks may have issued
+        different numbers of K9 calls (a capture warm-up that failed part-way on one rank, a turn
+        abandoned mid-decode, an injected extra call). Every rank quiesces its device, the group
+        takes the MAX of the ranks' epochs (one all-reduce, which is also the first barrier), each
+        rank sets its counter to it and zeroes every receive buffer it owns (flags, tile flags,
+        gather flags, LL pairs: no stale tag can match a future epoch), and a second all-reduce —
+        the barrier before any rank's next call can push into a peer's buffer — agrees that every
+        rank succeeded. Returns False (on every rank) if any rank failed: the caller drops K9."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rc = 0
+        try:
+            torch.cuda.synchronize(dev)
+            e = self.epoch()
+        except Exception:  # noqa: BLE001 - a dead device: the group drops K9 together
+            e, rc = 0, 1
+        E = int(_group_max(torch.tensor([float(e)], dtype=torch.float64), self.group, dev))
+        if rc == 0:
+            try:
+                rc = 0 if int(self._nat.oneshot_resync(self.id, E)) == 0 else 1
+            except Exception:  # noqa: BLE001
+                rc = 1
+        ok = _group_max(torch.tensor([float(rc)], dtype=torch.float64), self.group, dev) == 0
+        self.resyncs += 1
+        return ok
 
     def set_ll(self, on: bool) -> None:
         if self._nat.oneshot_set_ll(self.id, bool(on)) != 0:
@@ -200,6 +242,7 @@ def try_create(group, rank: int, world: int, cap_elems: int = DEFAULT_CAP_ELEMS)
             nat.oneshot_destroy(comm_id)
         return None
     comm = OneShotAllReduce(nat, comm_id, rank, world, cap_elems)
+    comm.group = group
     # a mapping that opened is not yet a mapping that works: prove the push / flag protocol on
     # THIS node's links (both slots, every rank's values) before any decode depends on it, and
     # agree on the verdict — a single failing rank sends the whole group to RCCL
@@ -240,6 +283,9 @@ def try_create(group, rank: int, world: int, cap_elems: int = DEFAULT_CAP_ELEMS)
         # the one-shot gather replaces an RCCL all-gather: keep whichever this node runs faster
         comm.gather_saving_us = probe_gather_saving(comm, group)
         comm.gather_ok = comm.gather_saving_us > 0.0
+    lim = os.environ.get("ROUNDTABLE_K9_POLL_LIMIT")
+    if lim:          # tests: a short flag-wait bound so an injected desync expires in ms, not s
+        comm.set_poll_limit(int(lim))
     return comm
 
 
@@ -251,7 +297,9 @@ def choose_protocol(comm: OneShotAllReduce, group) -> None:
     """Collective: the LL form replaces push + fence + flag for the standalone all-reduce when it
     passes the same exact self-test on every rank and (``auto``) its group-max latency beats the
     flag form's by ``MIN_LL_SAVING_US`` — identical numbers, so every rank takes the same
-    decision. The fused GEMM form and the gather keep the flag protocol."""
+    decision. The fused GEMM form (EPI_AR epilogue) follows the same choice — ``oneshot_gemm_ar``
+    passes the comm's protocol to the epilogue, and the fused self-test / saving probe run after
+    this, on the chosen form; only the one-shot gather keeps the flag protocol."""
     mode = ll_mode_env()
     if mode == "0":
         return

@@ -165,13 +165,20 @@ class TPInfo:
 class SimulatedTP(TPInfo):
     """Cost-model stand-in (``bench.py --simulate-tp N``, tools/tp_cost.py): ONE process computes
     rank 0's shard of a tp=N knight — the exact per-rank GEMM / attention / sampler shapes, in
-    the captured decode graph — while every collective is replaced by a local op of the same
-    output shape and no communication: all-reduce is the identity, the vocab all-gather tiles the
-    local shard N times (the copy a gather would write). The communication time is added by the
-    cost model from measured collective latencies. Never used for a real multi-GPU run."""
+    the captured decode graph — with every collective replaced by a local op of the same output
+    shape. ``comm_us`` set (bench default: K9 5 µs per all-reduce, 9.5 µs per logits gather):
+    each collective ALSO launches a device kernel that holds as many CUs as the real K9 launch
+    for that long (csrc/oneshot_ar.hip ``sim_comm_spin``), so the simulated step pays its
+    communication inside the graph, on the stream, as a node would — and a schedule that hides it
+    (:func:`~theroundtaible_amd.models.llama.LlamaModel.forward_decode_fused_tp_mb`) can be
+    measured on one GPU. ``comm_us=None``: collectives are free (round-4 compute-only records).
+    Never used for a real multi-GPU run."""
 
-    def __init__(self, size: int):
+    def __init__(self, size: int, comm_us: Optional[float] = None, gather_us: Optional[float] = None):
         super().__init__(size=size, rank=0, group=None)
+        self.comm_us = comm_us
+        self.gather_us = gather_us if gather_us is not None else comm_us
+        self._launch_us: Optional[float] = None
 
     def backend(self) -> str:
         return "nccl"            # keep hipGraph capture on, as on a real RCCL group
@@ -179,18 +186,62 @@ class SimulatedTP(TPInfo):
     def setup_oneshot(self) -> None:
         self.oneshot = None
 
+    def _spin_launch_us(self) -> float:
+        """What a zero-length spin node costs inside a captured graph, back to back (subtracted,
+        so a simulated collective costs ``comm_us`` per call in the captured step, node overhead
+        included)."""
+        if self._launch_us is None:
+            from .. import ops
+            nat = ops.native()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(8):
+                    nat.sim_comm_spin(0, 6)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(100):
+                    nat.sim_comm_spin(0, 6)
+            g.replay()
+            torch.cuda.synchronize()
+            best = float("inf")
+            for _ in range(5):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                g.replay()
+                b.record()
+                torch.cuda.synchronize()
+                best = min(best, a.elapsed_time(b) * 1e3 / 100)
+            self._launch_us = best
+        return self._launch_us
+
+    def _spin(self, us: Optional[float], numel: int) -> None:
+        if not us:
+            return
+        from .. import ops
+        nb = max(1, min(64, numel // 2048))       # the K9 launch's workgroup count for this message
+        ticks = int(max(0.0, us - self._spin_launch_us()) * 100)   # s_memrealtime: 100 MHz
+        ops.native().sim_comm_spin(ticks, nb)
+        self.sim_comm_calls = getattr(self, "sim_comm_calls", 0) + 1
+
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         self.sim_all_reduces = getattr(self, "sim_all_reduces", 0) + 1
+        if x.is_cuda:
+            self._spin(self.comm_us, x.numel())
         return x
 
     def row_parallel(self, x: torch.Tensor, Ws: torch.Tensor, res: Optional[torch.Tensor] = None,
                      **gemm_kw) -> torch.Tensor:
-        """The shard GEMM with the (no-op) all-reduce elided; the residual add stays (RESID
-        epilogue: the work the fused K9 epilogue does besides communicating)."""
+        """The shard GEMM, the residual add kept (RESID epilogue: the work K9's residual form does
+        besides communicating), then the simulated all-reduce."""
         from .. import ops
         if res is not None:
             self.sim_all_reduces = getattr(self, "sim_all_reduces", 0) + 1
-            return ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, **gemm_kw)
+            out = ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, **gemm_kw)
+            self._spin(self.comm_us, res.numel())
+            return out
         return self.all_reduce(ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_STORE, **gemm_kw))
 
     def any_rank(self, flag: bool) -> bool:
@@ -204,7 +255,10 @@ class SimulatedTP(TPInfo):
         return local[:, :lim].float().argmax(dim=1)
 
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
-        return x.repeat(1, self.size)
+        out = x.repeat(1, self.size)
+        if x.is_cuda:
+            self._spin(self.gather_us, out.numel())
+        return out
 
 
 def shard_rows(w: torch.Tensor, tp: TPInfo) -> torch.Tensor:

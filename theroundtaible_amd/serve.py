@@ -37,6 +37,7 @@ import itertools
 import json
 import os
 import queue
+import sys
 import threading
 import time
 import uuid
@@ -46,6 +47,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from .engine import Engine, EngineConfig, SamplingParams, Turn
 from .engine.engine import cut_at_stop
+from .utils import failsafe
 
 ROLE_TAGS = {"system": "Systeem", "user": "Gebruiker", "assistant": "Assistent"}
 
@@ -241,8 +243,9 @@ class MirroredEngine:
     the followers run the same call with the same arguments, so the TP collectives inside
     match. Everything else (tokenizer, stats, capacity, health) reads the local engine."""
 
-    def __init__(self, engine: Engine, cluster):
+    def __init__(self, engine: Engine, cluster, op_limit_s: Optional[float] = None):
         self._engine, self._cluster = engine, cluster
+        self._op_limit_s = op_limit_s
         self._lock = threading.Lock()    # one announced operation at a time, in issue order
         self.diverged: Optional[str] = None   # set when a follower's outcome differed from ours
 
@@ -256,10 +259,14 @@ class MirroredEngine:
         engine refuses every later operation instead of entering collectives no peer will join."""
         if self.diverged is not None:
             raise RuntimeError(f"tensor-parallel group stopped: {self.diverged}")
-        self._cluster.broadcast_object(op)
+        # announced over the wait group (a follower idles in that broadcast between requests);
+        # the operation and the outcome gather run on the containment-timeout groups and under a
+        # stage limit, so a follower that stalls mid-operation ends the server with a message
+        self._cluster.broadcast_object(op, wait=True)
         res, err = None, None
         try:
-            res = fn()
+            with failsafe.stage(f"serve {op[0]}", limit_s=self._op_limit_s):
+                res = fn()
         except Exception as e:  # noqa: BLE001 - re-raised after the agreement round
             err = e
         outs = self._cluster.all_gather_object(_outcome(err))
@@ -287,7 +294,7 @@ class MirroredEngine:
     def stop_followers(self) -> None:
         with self._lock:
             if self.diverged is None:
-                self._cluster.broadcast_object(("stop",))
+                self._cluster.broadcast_object(("stop",), wait=True)
 
 
 def _outcome(err: Optional[BaseException]) -> tuple:
@@ -295,26 +302,27 @@ def _outcome(err: Optional[BaseException]) -> tuple:
     return ("ok",) if err is None else ("err", type(err).__name__)
 
 
-def serve_follower(engine: Engine, cluster) -> int:
+def serve_follower(engine: Engine, cluster, op_limit_s: Optional[float] = None) -> int:
     """Ranks 1..N-1 of ``serve --tp N``: run rank 0's engine operations in its order until it
     announces ``stop``. Returns the number of operations executed. After each operation the
     ranks gather their outcomes (MirroredEngine._run): rank 0 reports a request's error; if
     any rank's outcome differs, every rank leaves the loop (the group has diverged)."""
     n = 0
     while True:
-        op = cluster.broadcast_object(None)
+        op = cluster.broadcast_object(None, wait=True)     # idle between requests: no timeout
         kind = op[0]
         if kind == "stop":
             return n
         err = None
         try:
-            if kind == "start":
-                engine.start_turns(op[1])
-            elif kind == "decode":
-                seqs = [engine.kv.seqs[k] for k in op[1]]
-                engine.continue_decode(seqs, op[2], op[3], op[4])
-            elif kind == "release":
-                engine.release(op[1])
+            with failsafe.stage(f"serve {kind}", limit_s=op_limit_s):
+                if kind == "start":
+                    engine.start_turns(op[1])
+                elif kind == "decode":
+                    seqs = [engine.kv.seqs[k] for k in op[1]]
+                    engine.continue_decode(seqs, op[2], op[3], op[4])
+                elif kind == "release":
+                    engine.release(op[1])
         except Exception as e:  # noqa: BLE001 - rank 0 reports the request's error
             err = e
         outs = cluster.all_gather_object(_outcome(err))
@@ -564,7 +572,7 @@ class RoundtableServer:
 def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", dtype: str = "bf16",
                  host: str = "127.0.0.1", port: int = 8000, max_batch: int = 16, max_tokens: int = 512,
                  use_graphs: bool = True, num_blocks: Optional[int] = None,
-                 tp: int = 1) -> Optional[RoundtableServer]:
+                 tp: int = 1, op_limit_s: float = 660.0) -> Optional[RoundtableServer]:
     """The server (rank 0), or — on a follower rank of a ``tp > 1`` launch — None after that
     rank has served rank 0's operations until shutdown."""
     # a checkpoint directory defines the architecture: preset + shape overrides from config.json
@@ -575,9 +583,18 @@ def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", 
         import torch.distributed as dist
         from .parallel.cluster import init_cluster
         from .parallel.tp import TPInfo
-        cluster = init_cluster(prefer_gpu=device != "cpu")
+        # containment: collectives fail after the request timeout + a minute, and
+        # every engine operation runs under a stage limit (a stalled rank ends the server with a
+        # message naming it, utils/failsafe.py); idle waits for the next request use the
+        # cluster's long-timeout wait group
+        cluster = init_cluster(prefer_gpu=device != "cpu", timeout_s=int(op_limit_s + 60))
         if cluster.world != tp:
             raise ValueError(f"serve --tp {tp} needs {tp} ranks, {cluster.world} joined")
+        failsafe.RunGuard(cluster.rank, cluster.world,
+                          lambda rec: sys.stderr.write(f"roundtable serve: rank {rec.get('failed_rank')} failed at "
+                                                       f"stage {rec.get('failed_stage')!r}: {rec.get('error')}\n"),
+                          default_s=float("inf"), exit_code=2,
+                          limits={"engine_load": 900.0, "k9_create": 900.0, "capture": op_limit_s}).start()
         tpi = TPInfo(size=tp, rank=cluster.rank, group=dist.group.WORLD)
         if device != "cpu":
             device = cluster.device
@@ -587,9 +604,10 @@ def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", 
         ecfg.dtype = "fp32" if dtype == "bf16" else dtype
         ecfg.use_graphs = False
     if tpi is not None:
-        engine = Engine(ecfg, tpi)
+        with failsafe.stage("engine_load"):
+            engine = Engine(ecfg, tpi)
         if cluster.rank != 0:
-            serve_follower(engine, cluster)
+            serve_follower(engine, cluster, op_limit_s)
             return None
-        return RoundtableServer(MirroredEngine(engine, cluster), model, host, port, max_batch, max_tokens)
+        return RoundtableServer(MirroredEngine(engine, cluster, op_limit_s), model, host, port, max_batch, max_tokens)
     return RoundtableServer(Engine(ecfg), model, host, port, max_batch, max_tokens)

@@ -13,8 +13,11 @@ prints nothing. This module gives every rank a named *stage* and a guard thread:
   printed as ONE JSON line naming the failed stage and rank, and the process exits non-zero
   without waiting for the collective its peers may be stuck in.
 
-Fault injection for tests: ``ROUNDTABLE_BENCH_FAULT="<rank>:<stage>:raise|stall"`` (comma
-separated) raises or blocks on entry to that stage on that rank only.
+Fault injection for tests: ``ROUNDTABLE_BENCH_FAULT="<rank>:<stage>:raise|stall|sleep<s>"`` (comma
+separated) raises, blocks, or pauses for <s> seconds on entry to that stage on that rank only.
+
+Stages are tracked per thread (engines capture from their own threads) and every transition is
+logged with a timestamp on stderr while a guard runs (or ``ROUNDTABLE_STAGE_LOG=1``).
 """
 from __future__ import annotations
 
@@ -29,8 +32,12 @@ import time
 from typing import Callable, Dict, Optional
 
 _lock = threading.Lock()
-_stage = "start"
-_stage_t0 = time.monotonic()
+# stage stack per thread: engines capture from their own threads (orchestrator.execute_plan), so
+# a process-global stage saved / restored by overlapping sub-stages could restore a stale value;
+# each thread keeps its own stack and the guard checks every thread's innermost stage
+_stacks: Dict[int, list] = {}
+_main = threading.main_thread().ident
+_t_start = time.monotonic()
 _guard: Optional["RunGuard"] = None
 
 
@@ -39,26 +46,62 @@ class FaultInjected(Exception):
 
 
 def current_stage() -> str:
-    return _stage
+    """The calling thread's innermost stage (else the main thread's, else ``start``)."""
+    with _lock:
+        st = _stacks.get(threading.get_ident()) or _stacks.get(_main)
+        return st[-1][0] if st else "start"
+
+
+def active_stages() -> list:
+    """(name, entered at, own limit or None) of every thread's innermost stage."""
+    with _lock:
+        return [st[-1] for st in _stacks.values() if st]
+
+
+def _log(name: str) -> None:
+    if _guard is not None or os.environ.get("ROUNDTABLE_STAGE_LOG") == "1":
+        # timestamped stage transitions on stderr: a run the launcher (or a silence watchdog)
+        # kills still names the stage it was in
+        rank = os.environ.get("RANK", "0")
+        sys.stderr.write(f"[rank {rank} +{time.monotonic() - _t_start:8.2f}s] stage {name!r}\n")
+        sys.stderr.flush()
 
 
 def set_stage(name: str) -> str:
-    """Enter stage ``name`` (returns the previous one); applies injected faults for it."""
-    global _stage, _stage_t0
+    """Enter stage ``name`` on the calling thread (replacing its innermost stage; returns the
+    previous one); applies injected faults for it."""
+    tid = threading.get_ident()
     with _lock:
-        prev, _stage, _stage_t0 = _stage, name, time.monotonic()
+        st = _stacks.setdefault(tid, [])
+        prev = st[-1][0] if st else "start"
+        if st:
+            st[-1] = (name, time.monotonic(), None)
+        else:
+            st.append((name, time.monotonic(), None))
+    _log(name)
     _maybe_fault(name)
     return prev
 
 
 @contextlib.contextmanager
-def stage(name: str):
-    """A sub-stage (e.g. ``capture`` inside ``round 1``): the enclosing stage resumes after it."""
-    prev = set_stage(name)
+def stage(name: str, limit_s: Optional[float] = None):
+    """A sub-stage (e.g. ``capture`` inside ``round 1``) of the calling thread: its enclosing
+    stage resumes after it, with its own clock as it was. ``limit_s``: this stage's own time limit
+    (else the guard's limit for its name)."""
+    tid = threading.get_ident()
+    with _lock:
+        _stacks.setdefault(tid, []).append((name, time.monotonic(), limit_s))
+    _log(name)
     try:
+        _maybe_fault(name)
         yield
     finally:
-        set_stage(prev)
+        with _lock:
+            st = _stacks.get(tid)
+            if st:
+                st.pop()
+            if not st and tid != _main:
+                _stacks.pop(tid, None)
 
 
 def _maybe_fault(name: str) -> None:
@@ -75,6 +118,8 @@ def _maybe_fault(name: str) -> None:
         if parts[2] == "stall":
             while True:            # a stuck rank: only the guard (or the launcher) ends it
                 time.sleep(1.0)
+        if parts[2].startswith("sleep"):   # a rank that stalls for a while, then carries on
+            time.sleep(float(parts[2][5:]))
 
 
 def run_dir() -> str:
@@ -89,8 +134,10 @@ class RunGuard:
     ``default_s`` otherwise. ``report(payload)`` prints rank 0's JSON line (called once)."""
 
     def __init__(self, rank: int, world: int, report: Callable[[dict], None], default_s: float = 300.0,
-                 limits: Optional[Dict[str, float]] = None, poll_s: float = 0.25, ack_wait_s: float = 15.0):
+                 limits: Optional[Dict[str, float]] = None, poll_s: float = 0.25, ack_wait_s: float = 15.0,
+                 exit_code: int = 3):
         self.rank, self.world, self.report = rank, world, report
+        self.exit_code = exit_code
         self.ack_wait_s = ack_wait_s
         self.default_s, self.limits, self.poll_s = default_s, dict(limits or {}), poll_s
         self.dir = run_dir()
@@ -118,9 +165,15 @@ class RunGuard:
     def _loop(self) -> None:
         while not self._done:
             time.sleep(self.poll_s)
-            name, t0 = _stage, _stage_t0
-            lim = self.limit_for(name)
-            if time.monotonic() - t0 > lim:
+            now = time.monotonic()
+            # every thread's innermost stage against its own limit; the most overdue one is named
+            over = []
+            for name, t0, own in active_stages():
+                lim = own if own is not None else self.limit_for(name)
+                if now - t0 > lim:
+                    over.append((now - t0 - lim, name, lim))
+            if over:
+                _, name, lim = max(over)
                 self.fail(name, f"stalled: stage {name!r} exceeded {lim:.0f} s on rank {self.rank}")
             if self.rank == 0:
                 peer = self._peer_failure()
@@ -164,7 +217,7 @@ class RunGuard:
         deadline = time.monotonic() + self.ack_wait_s
         while time.monotonic() < deadline and not os.path.exists(os.path.join(self.dir, "reported")):
             time.sleep(0.05)
-        os._exit(3)
+        os._exit(self.exit_code)
 
     def _report_and_exit(self, rec: dict) -> None:
         with self._rlock:
@@ -187,14 +240,15 @@ class RunGuard:
                         open(os.path.join(self.dir, "reported"), "w").close()
                     except OSError:
                         pass
-        os._exit(3)
+        os._exit(self.exit_code)
 
     def _on_term(self, signum, frame) -> None:  # noqa: ARG002 - signal handler signature
         """The launcher is tearing the run down (a peer exited): report what the peers filed."""
         recs = self._records()
         self._report_and_exit(recs[0] if recs else
-                              {"failed_stage": _stage, "failed_rank": None,
-                               "error": f"terminated by the launcher (signal {signum}) during stage {_stage!r}"})
+                              {"failed_stage": current_stage(), "failed_rank": None,
+                               "error": f"terminated by the launcher (signal {signum}) during stage "
+                                        f"{current_stage()!r}"})
 
     def finish(self) -> None:
         """Normal end: stop the guard (rank 0 removes the run directory)."""
