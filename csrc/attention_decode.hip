@@ -8,10 +8,10 @@
 namespace {
 using namespace attn;
 
-template <int D, int GM, int W = NW>
+template <int D, int GM, int W = NW, bool PP = true>
 __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
   __shared__ AttnSmem<D, GM, W> sm;
-  attn_item<D, false, GM, W>(p, blockIdx.x, blockIdx.y, sm);
+  attn_item<D, false, GM, W, PP>(p, blockIdx.x, blockIdx.y, sm);
 }
 
 // Split-KV combine as its own launch, for launches with many partial slots per query row
@@ -167,17 +167,25 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   args.ext_combine = (ext_min > 0 && num_splits >= ext_min && probe == 0) ? 1 : 0;
   const int G = Hq / Hkv;
   // a group's n*G columns need the 16-column LDS merge buffers
-#define RT_PD(DV)                                                                                  \
-  do {                                                                                             \
-    if (groups != nullptr) hipLaunchKernelGGL((paged_decode_kernel<DV, 16>), grid, block, 0, stream, args); \
-    else if (G <= 4) hipLaunchKernelGGL((paged_decode_kernel<DV, 4>), grid, block, 0, stream, args);   \
-    else if (G <= 8) hipLaunchKernelGGL((paged_decode_kernel<DV, 8>), grid, block, 0, stream, args); \
-    else hipLaunchKernelGGL((paged_decode_kernel<DV, 16>), grid, block, 0, stream, args);         \
+  // K/V loop form (attn_core.h PP): the copy-free ping-pong wins where a workgroup streams many
+  // tiles (Llama-3-8B tp 1, 8 KV heads: 3 knights x 22K shared keys 29.6 -> 28.7 us, 40K 41.1 ->
+  // 40.8 us) and loses ~0.3 us on the short ranges of 1-2 KV-head shards (tp 4 / 8), which keep the
+  // copy loop (profiles/r05/attn_pingpong_ab.md). RT_ATTN_PP=0 / 1 pins it (A/B).
+  static const int pp_env = getenv("RT_ATTN_PP") ? atoi(getenv("RT_ATTN_PP")) : -1;
+  const bool pp = pp_env >= 0 ? pp_env != 0 : Hkv >= 4;
+#define RT_PD2(DV, PPV)                                                                                       \
+  do {                                                                                                        \
+    if (groups != nullptr) hipLaunchKernelGGL((paged_decode_kernel<DV, 16, NW, PPV>), grid, block, 0, stream, args); \
+    else if (G <= 4) hipLaunchKernelGGL((paged_decode_kernel<DV, 4, NW, PPV>), grid, block, 0, stream, args);   \
+    else if (G <= 8) hipLaunchKernelGGL((paged_decode_kernel<DV, 8, NW, PPV>), grid, block, 0, stream, args); \
+    else hipLaunchKernelGGL((paged_decode_kernel<DV, 16, NW, PPV>), grid, block, 0, stream, args);         \
   } while (0)
+#define RT_PD(DV) do { if (pp) RT_PD2(DV, true); else RT_PD2(DV, false); } while (0)
   if (D == 128) RT_PD(128);
   else if (D == 64) RT_PD(64);
   else return -2;
 #undef RT_PD
+#undef RT_PD2
   if (args.ext_combine && defer_combine && D == 128) {
     // the caller runs the combine inside the next launch (combine_o.hip: combine + o-projection)
     if (deferred != nullptr) *deferred = 1;

@@ -121,7 +121,8 @@ RT_DEVICE void store_bf16x4(uint16_t* dst, float a, float b_, float c, float d, 
 // output rows (no split, or the last-arriving split that combined them).
 // W = waves per workgroup (8; 16 for grouped launches: twice the K/V in flight per CU and
 // enough threads to combine a whole group's slots in one round trip).
-template <int D, bool SC1, int GM = 16, int W = NW>
+// PP: ping-pong K/V tiles (two in flight per wave); false = the round-4 cur/nxt copy loop (A/B)
+template <int D, bool SC1, int GM = 16, int W = NW, bool PP = true>
 RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W>& S) {
   uint16_t* __restrict__ out = P.out;
   const uint16_t* __restrict__ q = P.q;
@@ -203,31 +204,22 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
     return v < nsh ? block_tables[(size_t)b0 * max_blocks + sh_b + v]
                    : block_tables[(size_t)b * max_blocks + pr_b + (v - nsh)];
   };
-  Tile<D> cur, nxt;
   int v = wid;
-  // Block ids of this wave's tiles (v = wid + W*j) are fetched one per lane up front, in
-  // flight with Q, and read out with readlane: no dependent scalar load inside the loop (refilled
-  // every 64 tiles, i.e. only past ~164K keys at 10 splits). B=3, ctx 1500: 12.2 -> 11.2 us.
+  // Block ids of this wave's tiles (v = wid + W*j) are fetched one per lane (at j = 0, in flight
+  // with Q, and refilled every 64 tiles, i.e. only past ~164K keys at 10 splits) and read out
+  // with readlane: no dependent scalar load inside the loop. B=3, ctx 1500: 12.2 -> 11.2 us.
   int blk_lane = 0;
-  {
-    const int tt = v + W * lane;
-    if (tt < nv) blk_lane = bt_entry(tt);
-  }
-  if (v < nv) {
-    const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, 0) * blk_stride + (size_t)hk * BS * D;
-    load_tile<D, SC1>(cur, k_cache + base, v_cache + base, r, g);
-  }
-  for (int j = 1; v < nv; v += W, ++j) {
-    const int vn = v + W;
-    if (vn < nv) {  // keep the next tile's loads in flight during this tile's math
-      if ((j & 63) == 0) {
-        const int tt = vn + W * lane;
-        blk_lane = tt < nv ? bt_entry(tt) : 0;
-      }
-      const size_t base =
-          (size_t)__builtin_amdgcn_readlane(blk_lane, j & 63) * blk_stride + (size_t)hk * BS * D;
-      load_tile<D, SC1>(nxt, k_cache + base, v_cache + base, r, g);
+  // tile vn = wid + W*j into t (j: the wave's tile index, uniform)
+  auto fetch = [&](Tile<D>& t, int vn, int j) {
+    if ((j & 63) == 0) {
+      const int tt = vn + W * lane;
+      blk_lane = tt < nv ? bt_entry(tt) : 0;
     }
+    const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, j & 63) * blk_stride + (size_t)hk * BS * D;
+    load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g);
+  };
+  // one 32-key tile: S^T = K Q^T, online softmax down each column, O += P V
+  auto step = [&](const Tile<D>& cur, int v) {
     // ---- S^T = K Q^T ----
     float4_ s[2];
 #pragma unroll
@@ -285,7 +277,51 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       oacc[e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pa),
                                                         __builtin_bit_cast(bf16x8, cur.v[e]), o, 0, 0, 0);
     }
-    cur = nxt;
+  };
+  if constexpr (PP) {
+    // Ping-pong over two named tiles, no `cur = nxt` copy, and the prefetch UNCONDITIONAL: with
+    // the copy (and with a prefetch skipped past the range end) the compiler's wait counts had to
+    // hold on every path, so each iteration waited for the NEXT tile's loads (vmcnt 15..0 before
+    // the MFMAs) and a wave had one tile in flight — a full memory latency per tile. Here tile
+    // j+1's 16 loads are always issued before tile j's math, which then waits with vmcnt(16):
+    // two tiles (32 KB) in flight per wave. Past the end the prefetch re-reads the tile being
+    // computed (an L2 hit, once per wave).
+    auto prefetch = [&](Tile<D>& t, int vn, int j) {
+      const bool past = vn >= nv;
+      const int jj = past ? j - 1 : j;
+      if (!past && (j & 63) == 0) {
+        const int tt = vn + W * lane;
+        blk_lane = tt < nv ? bt_entry(tt) : 0;
+      }
+      const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, jj & 63) * blk_stride + (size_t)hk * BS * D;
+      load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g);
+    };
+    Tile<D> ta, tb;
+    if (v < nv) {
+      fetch(ta, v, 0);
+      int j = 1;
+      while (true) {
+        prefetch(tb, v + W, j);
+        step(ta, v);
+        v += W;
+        ++j;
+        if (v >= nv) break;
+        prefetch(ta, v + W, j);
+        step(tb, v);
+        v += W;
+        ++j;
+        if (v >= nv) break;
+      }
+    }
+  } else {
+    Tile<D> cur, nxt;
+    if (v < nv) fetch(cur, v, 0);
+    for (int j = 1; v < nv; v += W, ++j) {
+      const int vn = v + W;
+      if (vn < nv) fetch(nxt, vn, j);  // keep the next tile's loads in flight during this tile's math
+      step(cur, v);
+      cur = nxt;
+    }
   }
   if (P.probe == 2) {          // + block ids, Q, every K/V tile and the math
     if (m == 12345.f && lsum == 1.f) out[0] = (uint16_t)oacc[0][0];
