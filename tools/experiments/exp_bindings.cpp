@@ -14,6 +14,8 @@ int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, 
                         int I, int Hq, int Hkv, int head_dim, int BS, int max_blocks, int num_splits, float eps,
                         float scale, hipStream_t stream);
 int decode_layer_grid();
+int launch_fused_mlp(void* res, void* g, const void* wgu, const void* wd, int* ws, int S, int* sync, int* err, int M,
+                     int H, int I, float eps, int grid, hipStream_t stream);
 int launch_ring_gemm(void* out, const void* x, const void* Ws, int M, int N, int K, int grid, int variant,
                      hipStream_t stream);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
@@ -146,6 +148,24 @@ PYBIND11_MODULE(_exp, m) {
         py::arg("part_ml"), py::arg("split_counters"), py::arg("sync"), py::arg("err"), py::arg("Hq"),
         py::arg("Hkv"), py::arg("num_splits"), py::arg("eps"), py::arg("scale"), py::arg("stamps") = py::none());
   m.def("decode_layer_grid", &decode_layer_grid);
+  m.def("fused_mlp", [](torch::Tensor res, torch::Tensor g, torch::Tensor wgu, torch::Tensor wd, torch::Tensor ws,
+                        int64_t S, torch::Tensor sync, torch::Tensor err, double eps, int64_t grid) {
+    check_bf16(res, "res");
+    check_bf16(g, "g");
+    check_bf16(wgu, "wgu");
+    check_bf16(wd, "wd");
+    check_type(ws, torch::kInt32, "ws");
+    check_type(sync, torch::kInt32, "sync");
+    check_type(err, torch::kInt32, "err");
+    const int64_t M = res.size(0), H = res.size(1), I = g.size(1);
+    TORCH_CHECK(g.size(0) == M && wgu.numel() == 2 * I * H && wd.numel() == H * I && sync.numel() >= 2 &&
+                    grid > 0 && grid <= decode_layer_grid(),
+                "fused_mlp: shapes / grid (must not exceed the CU count: every workgroup resident)");
+    const int rc = launch_fused_mlp(res.data_ptr(), g.data_ptr(), wgu.data_ptr(), wd.data_ptr(), ws.data_ptr<int>(),
+                                    (int)S, sync.data_ptr<int>(), err.data_ptr<int>(), (int)M, (int)H, (int)I,
+                                    (float)eps, (int)grid, cur_stream());
+    TORCH_CHECK(rc == 0, "fused_mlp: unsupported configuration (rc=", rc, ")");
+  });
   m.def("ring_gemm_exp", &ring_gemm_exp, py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("grid") = 0,
         py::arg("variant") = 0);
   m.def("prefetch", &prefetch, py::arg("t"), py::arg("nwg"), py::arg("sink"));

@@ -1,0 +1,121 @@
+// EXPERIMENT (launch folding redone fairly at shard shapes): the decode MLP
+// of a tensor-parallel shard — gate_up (+RMSNorm, SwiGLU) then down (+residual) — as ONE
+// persistent launch over ALL CUs, each phase laid out exactly as the product's separate launch:
+//   phase 1: gate_up split-K (the product's tile/part mapping, S from splitk_parts: Llama-3-8B tp 8
+//            = 112 tiles x 2 parts on 224 CUs; tp 4 = 224 whole tiles), the last arriver of a
+//            tile combines its parts in index order and writes g write-through (sc1);
+//   phase 2: down + residual, one 16-column tile per workgroup (256 tiles), its first weight
+//            stage issued BEFORE the wait on phase 1 (weights never depend on activations).
+// The phase hand-off is the persistent-kernel protocol of decode_layer.hip (drain + one arrival
+// atomic per work item, a bounded sc1 poll, a workgroup barrier). Round 4's persistent LAYER
+// ran gate_up on 112 CUs without split-K; this one gives both phases the whole chip, so the A/B
+// against the two product launches isolates the kernel-boundary vs in-launch hand-off cost.
+#include "skinny_core.h"
+
+namespace {
+using rt::short8;
+using namespace skinny;
+
+constexpr int NWM = 8;        // waves per workgroup (the product's split-K gate_up config)
+constexpr int UM = 2;         // k-steps per wave per pipeline stage
+constexpr int SPLIT_CTRS = 256;
+constexpr long long POLL_LIMIT = 1ll << 25;
+
+struct MlpArgs {
+  GemmArgs gu, dn;
+  int* ws;            // split workspace (product layout: SPLIT_CTRS counters, then part buffers)
+  int S;              // gate_up parts per tile (1 = whole tiles)
+  int n_gu, n_dn;     // tiles per phase
+  int* sync;          // [2] counters, zero at launch (re-armed by the last workgroup out)
+  int* err;
+};
+
+union MlpSmem {
+  GemmSmem<2, NWM> g2;
+  GemmSmem<1, NWM> g1;
+};
+
+RT_DEVICE void arrive(int* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+RT_DEVICE void wait_for(const int* cnt, int target, int* err) {
+  if (threadIdx.x == 0) {
+    long long it = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > POLL_LIMIT) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(NWM * 64) fused_mlp_kernel(MlpArgs P) {
+  __shared__ MlpSmem sm;
+  const int G = gridDim.x, w = blockIdx.x;
+  const int T = P.n_gu, S = P.S, items = T * S;
+  for (int b = w; b < items; b += G) {
+    if (S > 1) {
+      int tile, part;
+      if ((T & 7) == 0) {   // the product's placement: a tile's parts on one XCD
+        const int j = b >> 3;
+        tile = (j / S) * 8 + (b & 7);
+        part = j % S;
+      } else {
+        tile = b / S;
+        part = b % S;
+      }
+      const SplitX sx{reinterpret_cast<float*>(P.ws + SPLIT_CTRS) + (size_t)tile * S * SPLIT_STRIDE, P.ws + tile, part,
+                      S};
+      Stage<PRO_NORM, EPI_SWIGLU, UM> st;
+      gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, true>(P.gu, tile, sm.g2, st, false, false, &sx);
+    } else {
+      Stage<PRO_NORM, EPI_SWIGLU, UM> st;
+      gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, true>(P.gu, b, sm.g2, st, false, false);
+    }
+    arrive(P.sync);
+  }
+  {
+    Stage<PRO_PLAIN, EPI_RESID, UM> st;
+    if (w < P.n_dn) gemm_prefetch<PRO_PLAIN, EPI_RESID, NWM, UM>(P.dn, w, st);
+    wait_for(P.sync, items, P.err);
+    for (int t = w; t < P.n_dn; t += G) gemm_tile<PRO_PLAIN, EPI_RESID, NWM, UM, true>(P.dn, t, sm.g1, st, t == w, false);
+  }
+  // the last workgroup out re-arms the counters (every workgroup is past its wait)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(P.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == G - 1) {
+      __hip_atomic_store(P.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(P.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+}  // namespace
+
+// res [M, H] (in/out residual), g [M, I] scratch, wgu = shuffle_weight([gate; up] [2I, H], gamma, swiglu),
+// wd = shuffle_weight(W_down [H, I]); ws = the product split workspace; S = gate_up parts (1 = none).
+int launch_fused_mlp(void* res, void* g, const void* wgu, const void* wd, int* ws, int S, int* sync, int* err, int M,
+                     int H, int I, float eps, int grid, hipStream_t stream) {
+  if (M < 1 || M > 16 || H % 32 || I % 32 || S < 1 || grid < 1) return -1;
+  const RopeEpi none{};
+  MlpArgs P;
+  P.gu = GemmArgs{(uint16_t*)g, (const uint16_t*)res, (const short8*)wgu, nullptr, M, I, H, I, eps, none, nullptr,
+                  nullptr};
+  P.dn = GemmArgs{nullptr, (const uint16_t*)g, (const short8*)wd, (uint16_t*)res, M, H, I, 0, eps, none, nullptr,
+                  nullptr};
+  P.ws = ws;
+  P.S = S;
+  P.n_gu = I / 16;
+  P.n_dn = H / 16;
+  P.sync = sync;
+  P.err = err;
+  hipLaunchKernelGGL(fused_mlp_kernel, dim3(grid), dim3(NWM * 64), 0, stream, P);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
