@@ -284,7 +284,7 @@ constexpr int ALDS_BATCH = 8;   // 16-B loads per lane in flight while staging o
 // Rows are spread over the waves (row m on wave m % NW); within a row the 64 lanes take 16-B
 // units, ALDS_BATCH per lane per round trip (clamped re-reads at the tail are L2 hits, never
 // stored twice).
-template <int PRO, int NW>
+template <int PRO, int NW, bool SC1A = false>
 RT_DEVICE void stage_a(const GemmArgs& p, int s_lo, int nsteps, const ALds& L, uint16_t* __restrict__ xo) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int K = p.K, kb = s_lo * 32, n8 = (nsteps - s_lo) * 4;
@@ -298,7 +298,10 @@ RT_DEVICE void stage_a(const GemmArgs& p, int s_lo, int nsteps, const ALds& L, u
 #pragma unroll
       for (int j = 0; j < ALDS_BATCH; ++j) {
         const int u = min(u0 + 64 * j + lane, n8 - 1);
-        a[j] = *reinterpret_cast<const short8*>(xr + 8 * u);
+        if constexpr (SC1A)   // rows written earlier in this launch (persistent phases)
+          a[j] = __builtin_bit_cast(short8, rt::sc1_load4(rt::buf_rsrc(p.x), (int)((xr - p.x) + 8 * u) * 2));
+        else
+          a[j] = *reinterpret_cast<const short8*>(xr + 8 * u);
         if constexpr (PRO == PRO_NORM_ADD) b[j] = *reinterpret_cast<const short8*>(x2r + 8 * u);
       }
 #pragma unroll
@@ -490,11 +493,15 @@ RT_DEVICE void ar_exchange(const GemmArgs& p, int tile, float v, int m, int n, b
 
 // One 16-column tile. `st0` may hold this tile's prefetched stage-0 weights (prefetched=true).
 // `publish_xo`: this workgroup writes the NORM_ADD sum to p.xo.
-template <int PRO, int EPI, int NW, int U, bool SC1, bool ALDS = false>
+// AC (persistent kernels): coherence of the ACTIVATION loads apart from the stores — -1 = as SC1,
+// 0 = plain (the activation came from an earlier launch), 1 = sc1 (produced in this launch). With
+// ALDS, AC = 1 stages the rows with sc1 loads once, then reads LDS.
+template <int PRO, int EPI, int NW, int U, bool SC1, bool ALDS = false, int AC = -1>
 RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>& sm, Stage<PRO, EPI, U>& st0,
                          bool prefetched,
                          bool publish_xo, const SplitX* sx = nullptr, const ALds* al = nullptr) {
-  static_assert(!(ALDS && SC1), "the LDS-staged A operand is for standalone launches");
+  constexpr bool SC1A = AC < 0 ? SC1 : AC != 0;
+  static_assert(!(ALDS && SC1 && AC < 0), "an LDS-staged A operand in a persistent launch needs an explicit AC");
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int M = p.M, N = p.N, K = p.K;
@@ -505,11 +512,11 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   const int nsteps = sx != nullptr ? (int)((long)ksteps * (sx->idx + 1) / sx->n) : ksteps;
   const bool row_ok = r < M;
   const size_t lane_elem = (size_t)(row_ok ? r : 0) * K + 8 * g;
-  const XSrc xr = make_xsrc<SC1>(p.x, lane_elem);
-  const XSrc xr2 = make_xsrc<SC1>(PRO == PRO_NORM_ADD ? p.x2 : p.x, lane_elem);
+  const XSrc xr = make_xsrc<SC1A>(p.x, lane_elem);
+  const XSrc xr2 = make_xsrc<SC1A>(PRO == PRO_NORM_ADD ? p.x2 : p.x, lane_elem);
   uint16_t* xo_r =
       (PRO == PRO_NORM_ADD && publish_xo && row_ok && p.xo != nullptr) ? p.xo + (size_t)r * K + 8 * g : nullptr;
-  const XSrc xo_s = make_xsrc<SC1>(PRO == PRO_NORM_ADD && p.xo != nullptr ? p.xo : p.x, lane_elem);
+  const XSrc xo_s = make_xsrc<SC1A>(PRO == PRO_NORM_ADD && p.xo != nullptr ? p.xo : p.x, lane_elem);
   WStride sstride;
   const short8* wt = tile_base<EPI>(p, tile, sstride);
   const short8* wt2 = nullptr;
@@ -527,12 +534,12 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   const uint16_t* arow = nullptr;
   if constexpr (ALDS) {
     // stage-0 weights are in flight; stage A once (its loads overlap theirs), then the k-loop
-    stage_a<PRO, NW>(p, s_lo, nsteps, *al,
+    stage_a<PRO, NW, SC1A>(p, s_lo, nsteps, *al,
                      (PRO == PRO_NORM_ADD && publish_xo && p.xo != nullptr) ? p.xo : nullptr);
     __syncthreads();
     arow = al->a + (size_t)(row_ok ? r : 0) * al->astride + 8 * g - 32 * s_lo;
   } else {
-    issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, w0, nsteps);
+    issue_a<PRO, EPI, NW, U, SC1A>(st0, xr, xr2, row_ok, w0, nsteps);
   }
   // Epilogue operands that do not depend on the GEMM are loaded NOW, so their round trips hide
   // under the k-loop instead of following the last MFMA: the residual element (RESID) and the
@@ -564,13 +571,13 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
     for (; j + 1 < nst; j += 2) {
       const int s = w0 + SPAN * j;
       issue_w<PRO, EPI, NW, U>(st1, wt, wt2, s + SPAN, nsteps, lane, sstride);
-      issue_a<PRO, EPI, NW, U, SC1>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
-      consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
+      issue_a<PRO, EPI, NW, U, SC1A>(st1, xr, xr2, row_ok, s + SPAN, nsteps);
+      consume<PRO, EPI, NW, U, SC1A>(st0, acc, acc2, ssq, s, nsteps, xo_r, xo_s);
       issue_w<PRO, EPI, NW, U>(st0, wt, wt2, s + 2 * SPAN, nsteps, lane, sstride);
-      issue_a<PRO, EPI, NW, U, SC1>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
-      consume<PRO, EPI, NW, U, SC1>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
+      issue_a<PRO, EPI, NW, U, SC1A>(st0, xr, xr2, row_ok, s + 2 * SPAN, nsteps);
+      consume<PRO, EPI, NW, U, SC1A>(st1, acc, acc2, ssq, s + SPAN, nsteps, xo_r, xo_s);
     }
-    if (j < nst) consume<PRO, EPI, NW, U, SC1>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps, xo_r, xo_s);
+    if (j < nst) consume<PRO, EPI, NW, U, SC1A>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps, xo_r, xo_s);
   }
 
   // C layout: acc[i] = C[m = 4g + i][n = r]

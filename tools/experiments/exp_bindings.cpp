@@ -15,7 +15,7 @@ int launch_decode_layer(void* res, void* q, void* a, void* g, const void* wqkv, 
                         float scale, hipStream_t stream);
 int decode_layer_grid();
 int launch_fused_mlp(void* res, void* g, const void* wgu, const void* wd, int* ws, int S, int* sync, int* err, int M,
-                     int H, int I, float eps, int grid, hipStream_t stream);
+                     int H, int I, float eps, int grid, int phases, hipStream_t stream);
 int launch_ring_gemm(void* out, const void* x, const void* Ws, int M, int N, int K, int grid, int variant,
                      hipStream_t stream);
 int launch_prefetch(const void* p, int64_t nbytes, int nwg, uint32_t* sink, hipStream_t stream);
@@ -149,7 +149,7 @@ PYBIND11_MODULE(_exp, m) {
         py::arg("Hkv"), py::arg("num_splits"), py::arg("eps"), py::arg("scale"), py::arg("stamps") = py::none());
   m.def("decode_layer_grid", &decode_layer_grid);
   m.def("fused_mlp", [](torch::Tensor res, torch::Tensor g, torch::Tensor wgu, torch::Tensor wd, torch::Tensor ws,
-                        int64_t S, torch::Tensor sync, torch::Tensor err, double eps, int64_t grid) {
+                        int64_t S, torch::Tensor sync, torch::Tensor err, double eps, int64_t grid, int64_t phases) {
     check_bf16(res, "res");
     check_bf16(g, "g");
     check_bf16(wgu, "wgu");
@@ -163,7 +163,7 @@ PYBIND11_MODULE(_exp, m) {
                 "fused_mlp: shapes / grid (must not exceed the CU count: every workgroup resident)");
     const int rc = launch_fused_mlp(res.data_ptr(), g.data_ptr(), wgu.data_ptr(), wd.data_ptr(), ws.data_ptr<int>(),
                                     (int)S, sync.data_ptr<int>(), err.data_ptr<int>(), (int)M, (int)H, (int)I,
-                                    (float)eps, (int)grid, cur_stream());
+                                    (float)eps, (int)grid, (int)phases, cur_stream());
     TORCH_CHECK(rc == 0, "fused_mlp: unsupported configuration (rc=", rc, ")");
   });
   m.def("ring_gemm_exp", &ring_gemm_exp, py::arg("out"), py::arg("x"), py::arg("Ws"), py::arg("grid") = 0,

@@ -28,6 +28,7 @@ struct MlpArgs {
   int n_gu, n_dn;     // tiles per phase
   int* sync;          // [2] counters, zero at launch (re-armed by the last workgroup out)
   int* err;
+  int phases;         // diagnosis: 3 = both (the experiment), 1 = gate_up only, 2 = down only; +4 plain phase-1 stores
 };
 
 union MlpSmem {
@@ -55,10 +56,14 @@ RT_DEVICE void wait_for(const int* cnt, int target, int* err) {
   __syncthreads();
 }
 
+// ST1: phase-1 stores write-through (needed: phase 2 reads g from every XCD); false = diagnosis only
+template <bool ST1>
 __global__ void __launch_bounds__(NWM * 64) fused_mlp_kernel(MlpArgs P) {
   __shared__ MlpSmem sm;
+  extern __shared__ float alds_dyn[];          // phase 2: [16] row sums, then the staged g rows
+  const ALds al{reinterpret_cast<uint16_t*>(alds_dyn + 16), alds_dyn, P.dn.K + 8};
   const int G = gridDim.x, w = blockIdx.x;
-  const int T = P.n_gu, S = P.S, items = T * S;
+  const int T = P.n_gu, S = P.S, items = (P.phases & 1) ? T * S : 0;
   for (int b = w; b < items; b += G) {
     if (S > 1) {
       int tile, part;
@@ -72,19 +77,23 @@ __global__ void __launch_bounds__(NWM * 64) fused_mlp_kernel(MlpArgs P) {
       }
       const SplitX sx{reinterpret_cast<float*>(P.ws + SPLIT_CTRS) + (size_t)tile * S * SPLIT_STRIDE, P.ws + tile, part,
                       S};
-      Stage<PRO_NORM, EPI_SWIGLU, UM> st;
-      gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, true>(P.gu, tile, sm.g2, st, false, false, &sx);
+      Stage<PRO_NORM, EPI_SWIGLU, UM> st;   // res came from an earlier launch: plain A loads
+      gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, ST1, false, 0>(P.gu, tile, sm.g2, st, false, false, &sx);
     } else {
       Stage<PRO_NORM, EPI_SWIGLU, UM> st;
-      gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, true>(P.gu, b, sm.g2, st, false, false);
+      gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, ST1, false, 0>(P.gu, b, sm.g2, st, false, false);
     }
     arrive(P.sync);
   }
   {
     Stage<PRO_PLAIN, EPI_RESID, UM> st;
-    if (w < P.n_dn) gemm_prefetch<PRO_PLAIN, EPI_RESID, NWM, UM>(P.dn, w, st);
+    const int ndn = (P.phases & 2) ? P.n_dn : 0;
+    if (w < ndn) gemm_prefetch<PRO_PLAIN, EPI_RESID, NWM, UM>(P.dn, w, st);
     wait_for(P.sync, items, P.err);
-    for (int t = w; t < P.n_dn; t += G) gemm_tile<PRO_PLAIN, EPI_RESID, NWM, UM, true>(P.dn, t, sm.g1, st, t == w, false);
+    // g was written in this launch: staged ONCE per tile into LDS with sc1 loads (ALDS), not an
+    // sc1 load per k-step (phase 2 alone: 8.4 us with per-step sc1 loads vs 5.0 us as a launch);
+    // res is stored plainly (the next launch reads it)
+    for (int t = w; t < ndn; t += G) gemm_tile<PRO_PLAIN, EPI_RESID, NWM, UM, false, true, 1>(P.dn, t, sm.g1, st, t == w, false, nullptr, &al);
   }
   // the last workgroup out re-arms the counters (every workgroup is past its wait)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -102,7 +111,7 @@ __global__ void __launch_bounds__(NWM * 64) fused_mlp_kernel(MlpArgs P) {
 // res [M, H] (in/out residual), g [M, I] scratch, wgu = shuffle_weight([gate; up] [2I, H], gamma, swiglu),
 // wd = shuffle_weight(W_down [H, I]); ws = the product split workspace; S = gate_up parts (1 = none).
 int launch_fused_mlp(void* res, void* g, const void* wgu, const void* wd, int* ws, int S, int* sync, int* err, int M,
-                     int H, int I, float eps, int grid, hipStream_t stream) {
+                     int H, int I, float eps, int grid, int phases, hipStream_t stream) {
   if (M < 1 || M > 16 || H % 32 || I % 32 || S < 1 || grid < 1) return -1;
   const RopeEpi none{};
   MlpArgs P;
@@ -116,6 +125,10 @@ int launch_fused_mlp(void* res, void* g, const void* wgu, const void* wd, int* w
   P.n_dn = H / 16;
   P.sync = sync;
   P.err = err;
-  hipLaunchKernelGGL(fused_mlp_kernel, dim3(grid), dim3(NWM * 64), 0, stream, P);
+  P.phases = phases;
+  if (phases & 4)   // diagnosis: plain phase-1 stores (wrong across XCDs, timing only)
+    hipLaunchKernelGGL(fused_mlp_kernel<false>, dim3(grid), dim3(NWM * 64), alds_bytes(M, I), stream, P);
+  else
+    hipLaunchKernelGGL(fused_mlp_kernel<true>, dim3(grid), dim3(NWM * 64), alds_bytes(M, I), stream, P);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }

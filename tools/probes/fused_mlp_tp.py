@@ -87,8 +87,14 @@ def main():
             gg = ops.skinny_gemm(res, Wgs[i], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps, **sk)
             ops.skinny_gemm(gg, Wds[i], ops.PRO_PLAIN, ops.EPI_RESID, res=res, **sk)
 
-        def fused(i):
-            exp.fused_mlp(res, g, Wgs[i], Wds[i], sw, S, sync, err, eps, grid)
+        def fused(i, phases=3):
+            exp.fused_mlp(res, g, Wgs[i], Wds[i], sw, S, sync, err, eps, grid, phases)
+
+        def gate_up_only(i):
+            ops.skinny_gemm(res, Wgs[i], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps, **sk)
+
+        def down_only(i):
+            ops.skinny_gemm(g, Wds[i], ops.PRO_PLAIN, ops.EPI_RESID, res=res, **sk)
 
         # numerics on copy 0: both paths vs the fp32 oracle, fused twice bit-equal
         xr = x0.float()
@@ -114,7 +120,16 @@ def main():
                "poll_expired": int(err.item())}
         t2 = timed(lambda: [two_launches(i % copies) for i in range(a.calls)]) / a.calls
         tf = timed(lambda: [fused(i % copies) for i in range(a.calls)]) / a.calls
+        # the phases apart: each product launch alone, each persistent phase alone (same launch)
+        tgu = timed(lambda: [gate_up_only(i % copies) for i in range(a.calls)]) / a.calls
+        tdn = timed(lambda: [down_only(i % copies) for i in range(a.calls)]) / a.calls
+        tf1 = timed(lambda: [fused(i % copies, 1) for i in range(a.calls)]) / a.calls
+        tf2 = timed(lambda: [fused(i % copies, 2) for i in range(a.calls)]) / a.calls
+        tf5 = timed(lambda: [fused(i % copies, 5) for i in range(a.calls)]) / a.calls   # phase 1, plain stores
         row.update(two_launch_us=round(t2, 2), fused_us=round(tf, 2), saving_us=round(t2 - tf, 2),
+                   gate_up_launch_us=round(tgu, 2), down_launch_us=round(tdn, 2),
+                   fused_phase1_only_us=round(tf1, 2), fused_phase2_only_us=round(tf2, 2),
+                   fused_phase1_plain_stores_us=round(tf5, 2),
                    mlp_bytes_mb=round(per / 1e6, 1), poll_expired_after=int(err.item()))
         out["rows"].append(row)
         print(json.dumps(row), flush=True)
