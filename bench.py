@@ -417,7 +417,7 @@ def _run(args, failsafe) -> int:
                    "simulated_tp": sim or None,
                    "sim_comm": ({"all_reduce_us": args.sim_k9_us, "gather_us": args.sim_gather_us,
                                  "spin_launch_us": round(tp._launch_us, 2) if getattr(tp, "_launch_us", None) else None,
-                                 "calls_per_rank": getattr(tp, "sim_comm_calls", 0)}
+                                 "stand_in_nodes_issued_at_capture_or_eagerly": getattr(tp, "sim_comm_calls", 0)}
                                 if sim and args.sim_k9_us else None),
                    "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),
                    "k9_us": getattr(getattr(engine.tp, "oneshot", None), "latency_us", None),

@@ -29,10 +29,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main(paths) -> int:
     from theroundtaible_amd.models.config import get_config
     from theroundtaible_amd.parallel.costmodel import Calibration, strong_round_ms
-    sims = {}
+    sims, dev = {}, {}
     for p in paths:
         d = json.load(open(p))
-        sims[int(d["config"]["tp"])] = d
+        # records with device-simulated collectives (bench.py --simulate-tp N --sim-k9-us X, round 5)
+        # are the model's check, not its input
+        (dev if (d["detail"].get("sim_comm") or None) else sims)[int(d["config"]["tp"])] = d
     base = sims.get(1)
     if base is None:
         raise SystemExit("need the tp=1 run (sim1.json)")
@@ -65,6 +67,23 @@ def main(paths) -> int:
             tot = strong_round_ms(d, n, us, cal.gather_us, cal=cal)
             cells.append(f"{tot:.0f} ({dec_tok / tot * 1e3:.0f})")
         print(f"| {n} | {comp:.0f} | {dstep:.3f} | {par:.1f} | " + " | ".join(cells) + " |")
+    if dev:
+        print("\nCheck of the additive model against the DEVICE-simulated collectives (round 5: `bench.py "
+              "--simulate-tp N --sim-k9-us X` — every all-reduce / gather is a kernel holding the K9 launch's CUs "
+              "for X us inside the captured graph, so the step pays it on the stream as a node would):\n")
+        print("| N | all-reduce us | compute-only decode ms/step | device-simulated decode ms/step | "
+              "additive model decode ms/step | device-simulated ms/round (tok/s) |")
+        print("|---|---|---|---|---|---|")
+        for n in sorted(dev):
+            d, c = dev[n], sims.get(n)
+            sc = d["detail"]["sim_comm"]
+            dd = d["detail"]["engine_decode_ms_per_round"] / steps
+            cc = c["detail"]["engine_decode_ms_per_round"] / steps if c else float("nan")
+            model = cc + (2 * L * sc["all_reduce_us"] + sc["gather_us"]) / 1e3
+            print(f"| {n} | {sc['all_reduce_us']:g} | {cc:.3f} | {dd:.3f} | {model:.3f} | "
+                  f"{d['ms_per_round']:.0f} ({d['value']:.0f}) |")
+        print("\n(The device stand-in charges a prefill all-reduce the same per-call latency; the additive "
+              "model's prefill column charges the RCCL ring bandwidth instead.)")
     print("\nK9 per call measured between ranks sharing one GPU (IPC, no xGMI hop): "
           "5.4 us (2 ranks, 16 KB) — tools/oneshot_check.py --bench, profiles/r03/k9_shared_gpu.log.")
     print(f"Logits gather per step: {cal.gather_us} us (K9 one-shot all-gather, 2 ranks sharing one GPU, "
