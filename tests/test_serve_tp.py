@@ -133,3 +133,52 @@ def test_serve_tp2_on_shared_gpu():
         assert "roundtable_requests_total 4" in metrics and "roundtable_request_errors_total 0" in metrics, metrics
     finally:
         _stop(p)
+
+
+def test_serve_tp2_follower_stall_ends_the_server_with_a_message():
+    """VERDICT r4 #3 (containment outside the bench) for ``serve --tp``: the follower rank stalls on
+    entering its first engine operation. Rank 0's operation waits in the outcome gather, the
+    follower's stage outlives ``--op-timeout``: the guard ends every rank (exit code 2) with ONE
+    message naming the rank and stage, instead of the HTTP request hanging for the 30-minute
+    process-group default."""
+    port = free_port()
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT, ROUNDTABLE_BENCH_FAULT="1:serve start:stall")
+    p = subprocess.Popen([sys.executable, "-m", "theroundtaible_amd", "serve", "--model", "tiny-llama",
+                          "--weights", "random-full:1", "--device", "cpu", "--tp", "2", "--port", str(port),
+                          "--max-batch", "4", "--max-tokens", "8", "--num-blocks", "256", "--op-timeout", "8"],
+                         cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         start_new_session=True)
+    url = f"http://127.0.0.1:{port}"
+    try:
+        deadline = time.time() + 180
+        while True:
+            try:
+                with urllib.request.urlopen(url + "/health", timeout=5) as r:
+                    if r.status == 200:
+                        break
+            except OSError:
+                pass
+            assert p.poll() is None and time.time() < deadline, p.stdout.read() if p.poll() is not None else ""
+            time.sleep(0.5)
+        t0 = time.time()
+        got = []
+        th = threading.Thread(target=lambda: got.append(_try_post(url)), daemon=True)
+        th.start()
+        rc = p.wait(timeout=120)
+        took = time.time() - t0
+        out = p.stdout.read()
+        assert rc != 0, out[-2000:]
+        # both ranks outlive the stage limit at about the same moment (rank 0 waits in the outcome
+        # gather): the message names the stage, and every rank's record rides along
+        assert "failed at stage 'serve start'" in out and "exceeded 8 s" in out, out[-3000:]
+        assert "rank 1 stalled" in out or "rank 1 failed" in out, out[-3000:]
+        assert took < 90, took
+    finally:
+        _stop(p)
+
+
+def _try_post(url):
+    try:
+        return _post(url + "/v1/completions", {"prompt": "Een vraag.", "max_tokens": 4, "temperature": 0})
+    except Exception as e:  # noqa: BLE001 - the server goes away under the request
+        return e

@@ -53,8 +53,7 @@ def _start_guard(cl, config) -> None:
     t = float(getattr(getattr(config, "rules", None), "timeout_per_turn_seconds", 120) or 120)
 
     def report(rec: dict) -> None:
-        sys.stderr.write(f"roundtable: rank {rec.get('failed_rank')} failed at stage {rec.get('failed_stage')!r}: "
-                         f"{rec.get('error')}\n")
+        sys.stderr.write(failsafe.describe(rec, "roundtable") + "\n")
 
     failsafe.RunGuard(cl.rank, cl.world, report, default_s=float("inf"), exit_code=2,
                       limits={"engine_load": 900.0, "k9_create": 900.0, "capture": t + 120.0}).start()
@@ -665,7 +664,8 @@ def cmd_serve(args, ui: UI) -> int:
     from .serve import build_server
     srv = build_server(args.model, weights=args.weights, device=args.device, dtype=args.dtype, host=args.host,
                        port=args.port, max_batch=args.max_batch, max_tokens=args.max_tokens,
-                       use_graphs=not args.no_graphs, num_blocks=args.num_blocks, tp=tp)
+                       use_graphs=not args.no_graphs, num_blocks=args.num_blocks, tp=tp,
+                       op_limit_s=float(args.op_timeout))
     if srv is None:            # a follower rank of serve --tp N: served rank 0 until shutdown
         return 0
     ui.ok(f"  ✓ {args.model} on {srv.engine.device}: {srv.engine.kv_capacity_tokens} KV tokens resident capacity")
@@ -772,6 +772,9 @@ def build_parser() -> argparse.ArgumentParser:
     sv.add_argument("--no-graphs", action="store_true")
     sv.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree: serve one model over N GPUs (N ranks; rank 0 serves HTTP)")
+    sv.add_argument("--op-timeout", type=float, default=660.0,
+                    help="--tp: seconds one engine operation may take on any rank; a rank past it (or one that "
+                         "raises) ends the server with a message naming it (collectives time out a minute later)")
     sv.set_defaults(fn=cmd_serve)
     b = sub.add_parser("bench", help="Run the roundtable benchmark (wraps bench.py)")
     b.add_argument("bench_args", nargs=argparse.REMAINDER)

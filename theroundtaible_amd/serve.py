@@ -591,8 +591,7 @@ def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", 
         if cluster.world != tp:
             raise ValueError(f"serve --tp {tp} needs {tp} ranks, {cluster.world} joined")
         failsafe.RunGuard(cluster.rank, cluster.world,
-                          lambda rec: sys.stderr.write(f"roundtable serve: rank {rec.get('failed_rank')} failed at "
-                                                       f"stage {rec.get('failed_stage')!r}: {rec.get('error')}\n"),
+                          lambda rec: sys.stderr.write(failsafe.describe(rec, "roundtable serve") + "\n"),
                           default_s=float("inf"), exit_code=2,
                           limits={"engine_load": 900.0, "k9_create": 900.0, "capture": op_limit_s}).start()
         tpi = TPInfo(size=tp, rank=cluster.rank, group=dist.group.WORLD)

@@ -122,6 +122,19 @@ def _maybe_fault(name: str) -> None:
             time.sleep(float(parts[2][5:]))
 
 
+def describe(rec: dict, prog: str) -> str:
+    """One human line for a guard record (the CLI commands' report): the primary failure, then
+    every other rank's record (a stall usually shows on several ranks at once: the stuck one and
+    the ones waiting for it in a collective)."""
+    line = f"{prog}: rank {rec.get('failed_rank')} failed at stage {rec.get('failed_stage')!r}: {rec.get('error')}"
+    others = [r for r in rec.get("failures", []) if r.get("failed_rank") != rec.get("failed_rank")]
+    if others:
+        line += "; also " + "; ".join(
+            f"rank {r.get('failed_rank')} {'stalled' if str(r.get('error', '')).startswith('stalled') else 'failed'} "
+            f"at stage {r.get('failed_stage')!r}" for r in others)
+    return line
+
+
 def run_dir() -> str:
     """One directory per launch, shared by the ranks of this node: every rank of a torchrun
     launch has the same parent (the elastic agent) and master port."""
