@@ -266,3 +266,48 @@ def test_heterogeneous_engines_share_gpu_concurrently():
     with ThreadPoolExecutor(2) as ex:
         both = list(ex.map(lambda e: e.run_turns([Turn("k", p, GREEDY)])[0].ids, engines))
     assert both == solo
+
+
+def test_simulated_tp_device_collectives_cost_their_latency_in_a_graph():
+    """``bench.py --simulate-tp N --sim-k9-us X`` (round 5): every simulated collective is a kernel
+    holding the K9 launch's CUs for X µs INSIDE the captured graph (csrc/oneshot_ar.hip
+    sim_comm_spin), calibrated so a call costs X µs there. 20 all-reduces at 20 µs must add
+    ~400 µs to a replay; with the stand-in off they cost nothing; values pass through unchanged."""
+    from theroundtaible_amd.parallel.tp import SimulatedTP
+    x = torch.randn(3, 4096, device="cuda").to(torch.bfloat16)
+    ref = x.clone()
+
+    def replay_us(tp, calls=20):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(calls):
+                tp.all_reduce(x)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(calls):
+                tp.all_reduce(x)
+        g.replay()
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(5):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            g.replay()
+            b.record()
+            torch.cuda.synchronize()
+            best = min(best, a.elapsed_time(b) * 1e3)
+        return best
+
+    on = SimulatedTP(8, comm_us=20.0)
+    on.calibrate_stand_in()
+    t_on = replay_us(on)
+    assert 0.85 * 400 < t_on < 1.25 * 400, t_on
+    off = SimulatedTP(8)
+    for _ in range(5):
+        off.all_reduce(x)                 # the identity: no stand-in launch at all
+    assert getattr(off, "sim_comm_calls", 0) == 0 and getattr(on, "sim_comm_calls", 0) > 0
+    assert torch.equal(x, ref)
+    g = on.all_gather_last(x[:, :512].contiguous())
+    assert g.shape == (3, 4096) and torch.equal(g[:, 512:1024], x[:, :512])
