@@ -150,7 +150,9 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: Optional[int] = None, ma
     # Llama-3-8B, 10K / 25K / 40K keys: 24 splits 15.9 / 26.3 / 36.8 us, 32 splits 15.0 / 25.9 /
     # 35.7 (profiles/r03/attn_b1_splits.md)
     num_cus = device_cus() if num_cus is None else num_cus
-    cus = num_cus * 3 // 4 if grouped and batch > 1 else num_cus
+    # ROUNDTABLE_GROUPED_CU_FRACTION: A/B knob for the grouped share of the CUs (default 3/4)
+    frac = float(os.environ.get("ROUNDTABLE_GROUPED_CU_FRACTION", "0.75"))
+    cus = int(num_cus * frac) if grouped and batch > 1 else num_cus
     want = cus // max(1, batch * n_kv_heads)        # never more workgroups than CUs: a second
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
