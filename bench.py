@@ -264,7 +264,7 @@ def _run(args, failsafe) -> int:
         from theroundtaible_amd.parallel.tp import SimulatedTP
         tp = SimulatedTP(sim, comm_us=args.sim_k9_us or None, gather_us=args.sim_gather_us or None)
         if tp.comm_us or tp.gather_us:
-            tp._spin_launch_us()      # calibrate the stand-in's launch cost before any capture
+            tp.calibrate_stand_in()      # calibrate the stand-in's launch cost before any capture
     elif T > 1:
         import torch.distributed as dist
         from theroundtaible_amd.parallel.tp import TPInfo
@@ -416,7 +416,7 @@ def _run(args, failsafe) -> int:
         "detail": {"world": cl.world, "backend": cl.backend, "c1_ranks": cl.world if cl.distributed else 1,
                    "simulated_tp": sim or None,
                    "sim_comm": ({"all_reduce_us": args.sim_k9_us, "gather_us": args.sim_gather_us,
-                                 "spin_launch_us": round(tp._launch_us, 2) if getattr(tp, "_launch_us", None) else None,
+                                 "spin_launch_us": round(tp.stand_in_launch_us, 2) if getattr(tp, "stand_in_launch_us", None) else None,
                                  "stand_in_nodes_issued_at_capture_or_eagerly": getattr(tp, "sim_comm_calls", 0)}
                                 if sim and args.sim_k9_us else None),
                    "k9_oneshot": bool(getattr(engine.tp, "oneshot", None)),

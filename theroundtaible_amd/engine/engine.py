@@ -579,7 +579,8 @@ class Engine:
         if f == "k9-extra":         # one K9 call on THIS rank alone: the group's call counters diverge
             os_ = self.tp.oneshot
             if os_ is not None:
-                os_(torch.zeros(os_.world * 64, dtype=torch.bfloat16, device=self.device))
+                with self._on_stream():   # in order with the turn's own calls (one call at a time per comm)
+                    os_(torch.zeros(os_.world * 64, dtype=torch.bfloat16, device=self.device))
             return
         raise AdapterError("engine", f"injected failure at call {call}", kind="unknown")
 

@@ -155,11 +155,12 @@ class DistributedPool:
             for idxs in sorted(groups.values(), key=place):
                 first = self.local[pairs[idxs[0]][0].knight_name]
                 ranks = tuple(self.placement[pairs[idxs[0]][0].knight_name])
-                if self.turn_rendezvous and len(ranks) > 1 and not self._rendezvous(ranks, (place(idxs) + 1) * timeout_s):
+                wait_s = (place(idxs) + 1) * timeout_s
+                if self.turn_rendezvous and len(ranks) > 1 and not self._rendezvous(ranks, wait_s):
                     self.rendezvous_skips += 1
                     for i in idxs:
                         local_res[i] = AdapterError(pairs[i][0].name, f"a rank of its tensor-parallel group {list(ranks)} "
-                                                    f"did not reach the turn within {timeout_s:.0f} s; turn skipped "
+                                                    f"did not reach the turn within {wait_s:.0f} s; turn skipped "
                                                     "on every rank of the group", kind="timeout")
                     continue
                 outs = first.execute_group([(self.local[pairs[i][0].knight_name], pairs[i][1]) for i in idxs],

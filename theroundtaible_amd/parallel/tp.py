@@ -178,7 +178,7 @@ class SimulatedTP(TPInfo):
         super().__init__(size=size, rank=0, group=None)
         self.comm_us = comm_us
         self.gather_us = gather_us if gather_us is not None else comm_us
-        self._launch_us: Optional[float] = None
+        self.stand_in_launch_us: Optional[float] = None
 
     def backend(self) -> str:
         return "nccl"            # keep hipGraph capture on, as on a real RCCL group
@@ -186,11 +186,11 @@ class SimulatedTP(TPInfo):
     def setup_oneshot(self) -> None:
         self.oneshot = None
 
-    def _spin_launch_us(self) -> float:
+    def calibrate_stand_in(self) -> float:
         """What a zero-length spin node costs inside a captured graph, back to back (subtracted,
         so a simulated collective costs ``comm_us`` per call in the captured step, node overhead
         included)."""
-        if self._launch_us is None:
+        if self.stand_in_launch_us is None:
             from .. import ops
             nat = ops.native()
             s = torch.cuda.Stream()
@@ -214,15 +214,15 @@ class SimulatedTP(TPInfo):
                 b.record()
                 torch.cuda.synchronize()
                 best = min(best, a.elapsed_time(b) * 1e3 / 100)
-            self._launch_us = best
-        return self._launch_us
+            self.stand_in_launch_us = best
+        return self.stand_in_launch_us
 
     def _spin(self, us: Optional[float], numel: int) -> None:
         if not us:
             return
         from .. import ops
         nb = max(1, min(64, numel // 2048))       # the K9 launch's workgroup count for this message
-        ticks = int(max(0.0, us - self._spin_launch_us()) * 100)   # s_memrealtime: 100 MHz
+        ticks = int(max(0.0, us - self.calibrate_stand_in()) * 100)   # s_memrealtime: 100 MHz
         ops.native().sim_comm_spin(ticks, nb)
         self.sim_comm_calls = getattr(self, "sim_comm_calls", 0) + 1
 

@@ -127,7 +127,7 @@ def main():
     for comm in (float(c) for c in a.comm.split(",")):
         tp = SimulatedTP(T, comm_us=comm or None, gather_us=a.gather if comm else None)
         if comm:
-            tp._spin_launch_us()
+            tp.calibrate_stand_in()
         one_mb = Micro(m, 0, 3, slots, bt, ctx, pos, S)
         mbs = [Micro(m, 0, 2, slots, bt, ctx, pos, S1), Micro(m, 2, 3, slots, bt, ctx, pos, S2)]
         side = torch.cuda.Stream()
