@@ -126,6 +126,9 @@ def _self_launch(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    if args.device != "cpu":
+        from theroundtaible_amd.parallel.cluster import limit_shared_gpu_queues
+        limit_shared_gpu_queues(env, args.gpus)     # gloo rehearsal ranks sharing one card
     return subprocess.run(cmd, env=env).returncode
 
 

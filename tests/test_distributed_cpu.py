@@ -460,3 +460,21 @@ def test_strong_prediction_sequential_rounds_count_every_speaker():
     # fixed per-call cost once per speaker
     assert abs((d_seq - d_par) - (2 * decode + 2 * 2 * 32 * 0.02)) < 0.01
     assert d_par > decode
+
+
+def test_rehearsal_ranks_sharing_a_gpu_cap_their_hardware_queues(monkeypatch):
+    """8 gloo rehearsal ranks on one card map at most 16 hardware queues together (2 each; the
+    4-queue default hung the captured K9 warm-up, profiles/r05/rehearsal/); 4 ranks keep HIP's
+    default, as do a lower value already set, RCCL worlds and one rank per card."""
+    from theroundtaible_amd.parallel import cluster
+    monkeypatch.setattr(cluster.torch.cuda, "device_count", lambda: 1)
+    env = {"ROUNDTABLE_DIST_BACKEND": "gloo"}
+    assert cluster.limit_shared_gpu_queues(env, 4) is None and "GPU_MAX_HW_QUEUES" not in env
+    assert cluster.limit_shared_gpu_queues(env, 8) == 2 and env["GPU_MAX_HW_QUEUES"] == "2"
+    env = {"ROUNDTABLE_DIST_BACKEND": "gloo", "GPU_MAX_HW_QUEUES": "4"}     # as the GPU boxes export it
+    assert cluster.limit_shared_gpu_queues(env, 8) == 2 and env["GPU_MAX_HW_QUEUES"] == "2"
+    env = {"ROUNDTABLE_DIST_BACKEND": "gloo", "GPU_MAX_HW_QUEUES": "1"}     # never raised
+    assert cluster.limit_shared_gpu_queues(env, 8) is None and env["GPU_MAX_HW_QUEUES"] == "1"
+    assert cluster.limit_shared_gpu_queues({}, 8) is None               # RCCL: one rank per card
+    monkeypatch.setattr(cluster.torch.cuda, "device_count", lambda: 8)
+    assert cluster.limit_shared_gpu_queues({"ROUNDTABLE_DIST_BACKEND": "gloo"}, 8) is None

@@ -83,6 +83,33 @@ _CLUSTER: Optional[Cluster] = None
 WAIT_TIMEOUT_S = 7 * 24 * 3600
 
 
+SHARED_GPU_QUEUE_BUDGET = 16   # hardware queues the ranks sharing one card may map together
+
+
+def limit_shared_gpu_queues(env: dict, world: int) -> Optional[int]:
+    """Rehearsal ranks sharing a card (``ROUNDTABLE_DIST_BACKEND=gloo``, more ranks than GPUs): cap
+    each rank's hardware queues (HIP's default is 4) in the launcher's child ``env`` so that all of
+    them stay mapped at once. Measured on one MI355X: 8 ranks x 4 queues hung the first captured K9
+    warm-up (a one-shot all-reduce whose peers' queues are not mapped waits out its poll bound,
+    call after call); 8 x 2 ran the full bench with 0 failed turns (profiles/r05/rehearsal/). The
+    HIP runtime reads the variable when it starts, so only a launcher (bench.py, ``roundtable``'s
+    SPMD launch) can set it for its ranks; it only ever lowers a value already in ``env`` (the GPU
+    boxes export HIP's default, 4). Returns the cap set."""
+    if world <= 1 or env.get("ROUNDTABLE_DIST_BACKEND", "").strip().lower() != "gloo":
+        return None
+    ndev = max(1, torch.cuda.device_count())      # counts devices without starting the runtime
+    per_dev = -(-world // ndev)
+    try:
+        have = int(env.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        have = 4
+    q = max(1, SHARED_GPU_QUEUE_BUDGET // per_dev)
+    if per_dev * have <= SHARED_GPU_QUEUE_BUDGET or q >= have:
+        return None
+    env["GPU_MAX_HW_QUEUES"] = str(q)
+    return q
+
+
 def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     """Initialize from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); single process otherwise.
     ``timeout_s``: every collective of the world / control groups (and, by default, of TP groups
@@ -94,11 +121,11 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    use_gpu = prefer_gpu and torch.cuda.is_available()
     # Rehearsal mode (ROUNDTABLE_DIST_BACKEND=gloo): more ranks than GPUs share devices round-robin
     # and the data plane runs over gloo (RCCL refuses two ranks on one GPU) — lets a 1-GPU box run
     # the multi-rank GPU path (engines, hipGraphs, C1 exchange, TP collectives) end to end.
     forced = os.environ.get("ROUNDTABLE_DIST_BACKEND", "").strip().lower()
+    use_gpu = prefer_gpu and torch.cuda.is_available()
     gpu_index = local % max(1, torch.cuda.device_count()) if use_gpu and forced == "gloo" else local
     device = f"cuda:{gpu_index}" if use_gpu else "cpu"
     if use_gpu:

@@ -108,6 +108,9 @@ def launch_ranks(n: int, argv: List[str], cpu: bool, why: str, quiet: bool = Fal
     env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     if cpu:
         env.setdefault("OMP_NUM_THREADS", "1")
+    else:
+        from .cluster import limit_shared_gpu_queues
+        limit_shared_gpu_queues(env, n)
     if not quiet:
         print(f"  Launching {n} ranks ({why})", file=sys.stderr, flush=True)
     return subprocess.run(cmd, env=env).returncode
