@@ -62,6 +62,10 @@ constexpr int W_ROW = W_TKI + C * LCAP;  // words per row; after the B rows: the
 constexpr int POOL_BYTES = NB * 4 * 3 + NB * 8;
 constexpr int POOLK = POOL_BYTES / 4;
 constexpr int NALLOW = NT;               // list path: at most this many allowed tokens (else the histogram path)
+// which branch decided a row (RT_SMP_PROBE=5 writes it in place of the token; + PATH_EXACT_PASS
+// when the accept test needed its exact pass over the row)
+constexpr int PATH_PLAIN = 0, PATH_ACCEPT = 1, PATH_RESCAN = 2, PATH_CANDIDATES = 3, PATH_HISTOGRAM = 4,
+              PATH_EXACT_PASS = 10;
 
 RT_DEVICE uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -476,7 +480,8 @@ struct SampleArgs {
   int max_blocks, BS, H;
   int64_t vocab;
   int probe;                    // microbench only (RT_SMP_PROBE): 1 = stop before the slow path,
-                                // 2 = after its coarse histogram, 3 = after the sub-histogram
+                                // 2 = after its coarse histogram, 3 = after the sub-histogram,
+                                // 5 = full sampler, but tok[b] = the path that decided (PATH_*)
 };
 
 template <typename T, bool VEC>
@@ -564,7 +569,8 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   const float sbin = sgrid > 0.f ? sgrid : invT * BW;
   // top-k rows with a small k: chunk top-k lists (the decider needs no pass over the row)
   const int per = ((V + C - 1) / C + 7) & ~7;
-  const bool lst = temp > 0.f && use_k && k <= KMAX && per <= POOLK && a.probe == 0;
+  const bool full = a.probe == 0 || a.probe == 5;
+  const bool lst = temp > 0.f && use_k && k <= KMAX && per <= POOLK && full;
   constexpr int KLO = sizeof(T) == 2 ? 16 : 0;
 
   // ---- 1: chunk records ----
@@ -740,6 +746,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
   }
   const float mx = ra.v;
   int tok;
+  int path = PATH_PLAIN;
   if (!(temp > 0.f)) {
     tok = ra.i;
   } else if (!use_k && !(p < 1.f)) {
@@ -786,7 +793,8 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
         pz = p * total;
         accepted = above < pz;
       }
-      if (!accepted && a.probe == 0) {
+      path = (accepted ? PATH_ACCEPT : PATH_RESCAN) + (decided ? 0 : PATH_EXACT_PASS);
+      if (!accepted && full) {
         // rejected j*: the nucleus cut from the SAME histograms, merged on the common z grid
         // (bin g = kmax - floor(v / T * BW), 0 = top). With the crossing bin g*, tokens in bins
         // above it are inside the nucleus, below it outside, in it undecided. A chunk's best
@@ -852,8 +860,10 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
           amb = block_argmax(amb, sv, si);
           if (win.i != 0x7fffffff && (amb.v < win.v || (amb.v == win.v && amb.i > win.i))) cand = win.i;
         }
-        if (cand < 0)
+        if (cand < 0) {
           cand = nucleus_by_candidates<T, VEC>(row, V, mx, invT, pz, vj, key, s_gv, s_gi, sv, si, red);
+          path += PATH_CANDIDATES - PATH_RESCAN;
+        }
       }
     }
     if (lst) {
@@ -933,6 +943,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
       tok = accepted ? g.i : (cand >= 0 ? cand : ra.i);
     } else {
       // ---- slow path: histogram threshold, then the Gumbel argmax over the allowed set ----
+      path = (path / PATH_EXACT_PASS) * PATH_EXACT_PASS + PATH_HISTOGRAM;
       // coarse bins span the row's actual z range [zlo, 0] (not a fixed [-ZR, 0]): the values
       // spread over all NB bins, so the LDS atomics of one workgroup rarely collide
       const float zlo = fmaxf(-ZR, fminf((rmin - mx) * invT, -1e-3f));
@@ -1087,7 +1098,7 @@ __global__ void __launch_bounds__(NT) smp_kernel(SampleArgs a) {
     for (int i = threadIdx.x; i < row8; i += NT) dst[i] = src[i];
   }
   if (threadIdx.x == 0) {
-    a.tok[b] = tok;
+    a.tok[b] = a.probe == 5 ? path : tok;
     if (a.adv) {
       if (st < a.max_steps) a.out[st * a.B + b] = tok;
       a.ids[b] = tok;
