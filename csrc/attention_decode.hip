@@ -8,10 +8,27 @@
 namespace {
 using namespace attn;
 
+// XCD-aware item order (p.xcd): blocks are dealt round-robin over the 8 XCDs (block b runs on
+// the XCD of b % 8, the same class->XCD map in consecutive launches: tools/probes/xcc_probe.hip),
+// so item j = (lin % 8) * (nwg / 8) + lin / 8 gives each XCD a contiguous run of items. Items are
+// ordered kv head slowest: one kv head's (sequence, split) items, whose partials its rows'
+// combine reads, share an XCD — and decode_combine_kernel orders its rows the same way. A
+// different placement changes only speed.
+RT_DEVICE int xcd_item(int lin, int nwg) { return (lin & 7) * (nwg >> 3) + (lin >> 3); }
+
 template <int D, int GM, int W = NW, bool PP = true>
 __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
   __shared__ AttnSmem<D, GM, W> sm;
-  attn_item<D, false, GM, W, PP>(p, blockIdx.x, blockIdx.y, sm);
+  int bh = blockIdx.x, split = blockIdx.y;
+  if (p.xcd) {
+    const int ns = gridDim.y, nb = gridDim.x / p.Hkv;
+    const int j = xcd_item(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * ns);
+    const int hk = j / (nb * ns), rem = j - hk * (nb * ns);
+    const int b = rem / ns;
+    split = rem - b * ns;
+    bh = b * p.Hkv + hk;
+  }
+  attn_item<D, false, GM, W, PP>(p, bh, split, sm);
 }
 
 // Split-KV combine as its own launch, for launches with many partial slots per query row
@@ -29,12 +46,23 @@ __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
 // Partials were stored write-through by the previous launch: the kernel boundary orders them.
 template <int D, int SPL>
 __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
-  const int row = blockIdx.x;                  // b * Hq + query head
+  const int G = p.Hq / p.Hkv;
+  int row = blockIdx.x;                        // b * Hq + query head
+  int chunk = blockIdx.y;
+  if (p.xcd) {   // rows of one kv head on the XCD that ran its attention items (xcd_item)
+    const int nc = gridDim.y, nb = gridDim.x / p.Hq;
+    const int j = xcd_item(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * nc);
+    const int per_h = nb * G * nc;
+    const int hk = j / per_h, r1 = j - hk * per_h;
+    const int bb = r1 / (G * nc), r2 = r1 - bb * (G * nc);
+    const int hh = r2 / nc;
+    chunk = r2 - hh * nc;
+    row = bb * p.Hq + hk * G + hh;
+  }
   const int b = row / p.Hq;
   const int dl = threadIdx.x & 7, sl = threadIdx.x >> 3;
   const int nsl = blockDim.x >> 3;
-  const int d0 = blockIdx.y * 32 + 4 * dl;
-  const int G = p.Hq / p.Hkv;
+  const int d0 = chunk * 32 + 4 * dl;
   const int stride = p.slot_stride > 0 ? p.slot_stride : p.num_splits;
   // the host's sizing: every split of every member of the largest group (slots past the row's
   // own count are inside the row's stride and loaded, never merged)
@@ -165,6 +193,13 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   // combine on one CU at every measured split count (profiles/r03/attn_ext_combine.md)
   static const int ext_min = getenv("RT_ATTN_EXT_SPLITS") ? atoi(getenv("RT_ATTN_EXT_SPLITS")) : 2;
   args.ext_combine = (ext_min > 0 && num_splits >= ext_min && probe == 0) ? 1 : 0;
+  // A/B knobs (profiles/r05/attn_xcd_ab.md): XCD-aware item order in both launches, and plain
+  // (L2-resident) partial stores for the separate combine
+  static const int xcd_env = getenv("RT_ATTN_XCD") ? atoi(getenv("RT_ATTN_XCD")) : 0;
+  static const int plain_env = getenv("RT_ATTN_PLAIN_PARTIALS") ? atoi(getenv("RT_ATTN_PLAIN_PARTIALS")) : 0;
+  const bool hk_split_ok = Hkv % 8 == 0 || 8 % Hkv == 0;
+  args.xcd = (xcd_env && (B * Hkv * num_splits) % 8 == 0 && (B * Hq * (D / 32)) % 8 == 0 && hk_split_ok) ? 1 : 0;
+  args.plain_partials = (plain_env && args.ext_combine && !defer_combine) ? 1 : 0;
   const int G = Hq / Hkv;
   // a group's n*G columns need the 16-column LDS merge buffers
   // K/V loop form (attn_core.h PP): the copy-free ping-pong wins where a workgroup streams many

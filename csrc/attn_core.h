@@ -94,6 +94,8 @@ struct AttnArgs {
   int slot_stride = 0;         // partial slots per (sequence, head) >= n * num_splits; 0 = num_splits
   int probe = 0;               // latency probe (microbench only, RT_ATTN_PROBE): stop after phase k
   int ext_combine = 0;         // 1: leave every partial for decode_combine_kernel (no in-launch combine)
+  int xcd = 0;                 // 1: XCD-aware item order (attention_decode.hip), the launch's grid % 8 == 0
+  int plain_partials = 0;      // 1 (ext_combine only): partials stay in the writer's L2 (plain stores)
 };
 
 // GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
@@ -369,10 +371,18 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       const float inv = L > 0.f ? 1.f / L : 0.f;
       store_bf16x4(out + (q0 + row) * D + d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv, SC1);
     } else {
-      // partials leave as 16-B write-through (sc1) stores: the combining workgroup, possibly
-      // on another XCD, reads them with sc1 loads and no L2 writeback/invalidate is needed
-      rt::sc1_store4(po_rsrc, ((row * stride + slot) * D + d0) * 4, O);
-      if (d0 == 0) rt::sc1_store4(pml_rsrc, (row * stride + slot) * 16, float4_{M, L, 0.f, 0.f});
+      if (P.plain_partials) {
+        // read by the NEXT launch only (decode_combine_kernel): the kernel boundary orders them,
+        // and plain stores keep the lines in this XCD's L2, where an XCD-aware combine reads them
+        const size_t e = ((q0 + row) * stride + slot);
+        *reinterpret_cast<float4_*>(part_o + e * D + d0) = O;
+        if (d0 == 0) *reinterpret_cast<float4_*>(part_ml + e * 4) = float4_{M, L, 0.f, 0.f};
+      } else {
+        // partials leave as 16-B write-through (sc1) stores: the combining workgroup, possibly
+        // on another XCD, reads them with sc1 loads and no L2 writeback/invalidate is needed
+        rt::sc1_store4(po_rsrc, ((row * stride + slot) * D + d0) * 4, O);
+        if (d0 == 0) rt::sc1_store4(pml_rsrc, (row * stride + slot) * 16, float4_{M, L, 0.f, 0.f});
+      }
     }
   }
   if (nslots == 1) {
