@@ -478,3 +478,21 @@ def test_rehearsal_ranks_sharing_a_gpu_cap_their_hardware_queues(monkeypatch):
     assert cluster.limit_shared_gpu_queues({}, 8) is None               # RCCL: one rank per card
     monkeypatch.setattr(cluster.torch.cuda, "device_count", lambda: 8)
     assert cluster.limit_shared_gpu_queues({"ROUNDTABLE_DIST_BACKEND": "gloo"}, 8) is None
+
+
+def test_rehearsal_cu_split_gives_each_sharing_rank_a_disjoint_slice(monkeypatch):
+    """ROUNDTABLE_REHEARSAL_CU_SPLIT=1: ranks sharing one card get disjoint, equal CU masks (the
+    mask HIP reads at start-up); off by default, and nothing for one rank per card."""
+    from theroundtaible_amd.parallel import cluster
+    monkeypatch.setattr(cluster.torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(cluster, "_card_cus", lambda default=256: 256)
+    monkeypatch.delenv("ROUNDTABLE_REHEARSAL_CU_SPLIT", raising=False)
+    monkeypatch.delenv("ROC_GLOBAL_CU_MASK", raising=False)
+    assert cluster.rehearsal_cu_split(4, 1) is None and "ROC_GLOBAL_CU_MASK" not in os.environ
+    monkeypatch.setenv("ROUNDTABLE_REHEARSAL_CU_SPLIT", "1")
+    masks = [int(cluster.rehearsal_cu_split(4, r), 16) for r in range(4)]
+    assert all(bin(m).count("1") == 64 for m in masks)
+    assert sum(masks) == (1 << 256) - 1 and all(a & b == 0 for i, a in enumerate(masks) for b in masks[i + 1:])
+    monkeypatch.setattr(cluster.torch.cuda, "device_count", lambda: 4)
+    monkeypatch.delenv("ROC_GLOBAL_CU_MASK", raising=False)
+    assert cluster.rehearsal_cu_split(4, 2) is None and "ROC_GLOBAL_CU_MASK" not in os.environ

@@ -30,6 +30,8 @@ def _bench(extra=(), nproc=2):
            "--gpus", str(nproc), "--model", "tiny-llama", "--steps", "2", "--warmup", "1", "--new-tokens", "16",
            "--temperature", "0", "--kv-fraction", "0.1", "--max-kv-tokens", "65536", *extra]
     env = dict(os.environ, ROUNDTABLE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    from theroundtaible_amd.parallel.cluster import limit_shared_gpu_queues
+    limit_shared_gpu_queues(env, nproc)      # 8 sharing ranks x 4 queues oversubscribe the card
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -89,11 +91,11 @@ def test_strong_scaling_sampled_decode_on_shared_gpu():
     assert out["detail"]["decode_tokens"] == 3 * 16 * 2, out["_log"]
 
 
-def _tp_check(nproc, model, layers, tokens=12, extra=(), fused_ar=None):
+def _tp_check(nproc, model, layers, tokens=12, extra=(), fused_ar=None, env_extra=None, tag=""):
     gc.collect()
     torch.cuda.empty_cache()
     port = free_port()
-    out = os.path.join(ROOT, "gpurun_out", f"tp_check_{model}_{layers}l_tp{nproc}.pt")
+    out = os.path.join(ROOT, "gpurun_out", f"tp_check_{model}_{layers}l_tp{nproc}{tag}.pt")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "tp_check.py"),
@@ -103,6 +105,9 @@ def _tp_check(nproc, model, layers, tokens=12, extra=(), fused_ar=None):
         # two ranks sharing the GPU co-schedule reliably: decode on the fused GEMM + exchange
         # (one rank per GPU enables it by default; more sharing ranks keep the separate K9)
         env["ROUNDTABLE_FUSED_AR"] = "1"
+    env.update(env_extra or {})
+    from theroundtaible_amd.parallel.cluster import limit_shared_gpu_queues
+    limit_shared_gpu_queues(env, nproc)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return torch.load(out, weights_only=True)
@@ -233,6 +238,27 @@ def test_fused_ar_four_ranks_on_one_gpu_is_contained():
     # agreed device-wait failure: the expiring rank names K9, its peers "a peer rank's device
     # wait expired" (Engine.device_flag_errors)
     assert all("K9" in e or "device wait expired" in e for e in errs), errs
+
+
+@pytest.mark.parametrize("tp", [4, 8])
+def test_fused_ar_correct_at_tp4_tp8_with_cu_split_on_shared_gpu(tp):
+    """EPI_AR (the o / down GEMM exchanging its tiles itself) completing a
+    CORRECT run at tp >= 4. Ranks sharing one card get disjoint CU slices
+    (ROUNDTABLE_REHEARSAL_CU_SPLIT=1, parallel/cluster.py rehearsal_cu_split: 256 / tp CUs each), so
+    their spinning grids co-run as on separate GPUs. The fused form must pass its creation
+    self-test, run every o / down of the captured decode (16 calls) with no expired wait, and match
+    a tp 1 engine on ONE rank's CU count (torch's device RNG draws the random-dev weights with
+    launch shapes that follow the CU count): prefill and decode logits cosine > 0.999."""
+    cus = 256 // tp
+    ref = _tp_check(1, "llama3-8b", 2, env_extra={"ROC_GLOBAL_CU_MASK": hex((1 << cus) - 1)}, tag=f"_cu{cus}")
+    got = _tp_check(tp, "llama3-8b", 2, extra=("--graphs", "--poll-limit", "262144"), fused_ar=True,
+                    env_extra={"ROUNDTABLE_REHEARSAL_CU_SPLIT": "1"}, tag="_cusplit")
+    assert got["fused_ar"] and got["fused_ar_calls"] > 0 and all(got["graphs_per_rank"]), got
+    assert all(e is None for e in got["errors"]) and not got["flag_errors"], got["errors"]
+    cos = torch.nn.functional.cosine_similarity
+    c_pre = float(cos(got["prefill_logits"][None], ref["prefill_logits"][None]))
+    c_dec = float(cos(got["decode_logits"][None], ref["decode_logits"][None]))
+    assert c_pre > 0.999 and c_dec > 0.999, (c_pre, c_dec)
 
 
 def test_k9_epoch_desync_fails_one_turn_then_resyncs_on_shared_gpu():

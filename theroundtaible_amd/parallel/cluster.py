@@ -110,6 +110,41 @@ def limit_shared_gpu_queues(env: dict, world: int) -> Optional[int]:
     return q
 
 
+def _card_cus(default: int = 256) -> int:
+    """Compute units of the first GPU from the KFD topology (no HIP runtime start)."""
+    import glob
+    for f in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
+        try:
+            kv = dict(line.split()[:2] for line in open(f) if len(line.split()) >= 2)
+            simd, per = int(kv.get("simd_count", 0)), int(kv.get("simd_per_cu", 0))
+        except (OSError, ValueError):
+            continue
+        if simd > 0 and per > 0:
+            return simd // per
+    return default
+
+
+def rehearsal_cu_split(world: int, local: int) -> Optional[str]:
+    """``ROUNDTABLE_REHEARSAL_CU_SPLIT=1`` (rehearsal ranks sharing a card): give each rank a
+    disjoint slice of the card's CUs (``ROC_GLOBAL_CU_MASK``, read when the HIP runtime starts,
+    so this runs first), so the ranks' kernels co-run like kernels on separate GPUs instead of
+    starving each other — a spinning fused-all-reduce grid of one rank cannot hold the CUs a
+    peer needs to reach its side of the exchange (profiles/r05/rehearsal/). A masked process sees
+    only its slice as the device's CU count, so launch shapes (and torch's random streams) follow
+    the slice. Returns the mask set."""
+    if os.environ.get("ROUNDTABLE_REHEARSAL_CU_SPLIT", "0") != "1" or world <= 1:
+        return None
+    ndev = max(1, torch.cuda.device_count())
+    per_card = -(-world // ndev)
+    if per_card <= 1:
+        return None
+    slot = local // ndev                       # ranks share cards round-robin (gpu = local % ndev)
+    per = _card_cus() // per_card
+    mask = hex(((1 << per) - 1) << (per * slot))
+    os.environ["ROC_GLOBAL_CU_MASK"] = mask
+    return mask
+
+
 def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     """Initialize from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); single process otherwise.
     ``timeout_s``: every collective of the world / control groups (and, by default, of TP groups
@@ -125,6 +160,8 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     # and the data plane runs over gloo (RCCL refuses two ranks on one GPU) — lets a 1-GPU box run
     # the multi-rank GPU path (engines, hipGraphs, C1 exchange, TP collectives) end to end.
     forced = os.environ.get("ROUNDTABLE_DIST_BACKEND", "").strip().lower()
+    if forced == "gloo" and prefer_gpu:
+        rehearsal_cu_split(world, local)
     use_gpu = prefer_gpu and torch.cuda.is_available()
     gpu_index = local % max(1, torch.cuda.device_count()) if use_gpu and forced == "gloo" else local
     device = f"cuda:{gpu_index}" if use_gpu else "cpu"
