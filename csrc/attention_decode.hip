@@ -196,6 +196,8 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   // A/B knobs (profiles/r05/attn_xcd_ab.md): XCD-aware item order in both launches, and plain
   // (L2-resident) partial stores for the separate combine
   static const int xcd_env = getenv("RT_ATTN_XCD") ? atoi(getenv("RT_ATTN_XCD")) : 0;
+  // latency decomposition only (microbench): the attention launch without its combine launch
+  static const bool skip_combine = getenv("RT_ATTN_SKIP_COMBINE") && atoi(getenv("RT_ATTN_SKIP_COMBINE")) == 1;
   static const int plain_env = getenv("RT_ATTN_PLAIN_PARTIALS") ? atoi(getenv("RT_ATTN_PLAIN_PARTIALS")) : 0;
   const bool hk_split_ok = Hkv % 8 == 0 || 8 % Hkv == 0;
   args.xcd = (xcd_env && (B * Hkv * num_splits) % 8 == 0 && (B * Hq * (D / 32)) % 8 == 0 && hk_split_ok) ? 1 : 0;
@@ -224,7 +226,7 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   if (args.ext_combine && defer_combine && D == 128) {
     // the caller runs the combine inside the next launch (combine_o.hip: combine + o-projection)
     if (deferred != nullptr) *deferred = 1;
-  } else if (args.ext_combine) {
+  } else if (args.ext_combine && !skip_combine) {
     // slots per row: every split of every member of the largest group (groups: n * G <= 16)
     const int nmax = groups != nullptr ? min(slot_stride, (16 / G) * num_splits) : num_splits;
     // slot-lanes (x 8 dim-lanes) per workgroup, capped at 32 (RT_COMBINE_NSL): fewer, wider lanes
