@@ -32,6 +32,13 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(GemmArgs p) {
   gemm_tile<PRO, EPI, NW, U, false>(p, blockIdx.x, sm, st0, false, blockIdx.x == 0);
 }
 
+// TN tiles per workgroup (skinny_core.h gemm_tiles): serving batches, M > 4
+template <int PRO, int EPI, int NW, int U, int TN>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_multi_kernel(GemmArgs p) {
+  __shared__ GemmSmemN<nacc<EPI>(), NW, TN> sm;
+  gemm_tiles<PRO, EPI, NW, U, TN>(p, blockIdx.x * TN, sm);
+}
+
 // the dynamic LDS of an ALDS launch: [16] row sums of squares, then the staged rows
 RT_DEVICE ALds alds_view(int kspan) {
   extern __shared__ float alds_dyn[];
@@ -323,6 +330,57 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
       else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_SK(PRO_PLAIN, EPI_SWIGLU);
       else return -2;
 #undef RT_SK
+      return hipGetLastError() == hipSuccess ? 0 : -6;
+    }
+  }
+  // Serving batches (M > 4): TN tiles per workgroup share each activation fragment (skinny_core.h
+  // gemm_tiles), as long as the launch still covers 3/4 of the CUs. MI355X, Llama-3-8B, M = 16
+  // (profiles/r05/gemm_multi_tile.md): lm_head 235.0 -> 163.2 us (TN 4), gate_up 42.1 -> 38.7
+  // (TN 4), qkv 16.7 -> 13.5 (TN 2); o / down (256 tiles) lose with fewer workgroups and keep one
+  // tile. RT_SKINNY_TN=<TN> (1 = off) pins the tile count, RT_SKINNY_TNCFG=<NW>x<U> the variant
+  // (microbenchmarks); the M <= 4 decode path is unchanged.
+  if (M > 4 && (pro == PRO_PLAIN || pro == PRO_NORM) && epi != EPI_AR) {
+    static const int tn_env = [] {
+      const char* e = getenv("RT_SKINNY_TN");
+      return e ? atoi(e) : -1;
+    }();
+    static const int tncfg = [] {
+      const char* e = getenv("RT_SKINNY_TNCFG");
+      int nw = 0, u = 0;
+      if (!e || sscanf(e, "%dx%d", &nw, &u) != 2) return 402;
+      return nw * 100 + u;
+    }();
+    const int T16 = N / 16, cus = device_cus(), need = cus * 3 / 4;
+    const int tn = tn_env >= 0 ? tn_env : (cus <= 0 ? 1 : (T16 / 4 >= need ? 4 : (T16 / 2 >= need ? 2 : 1)));
+    if (tn == 2 || tn == 4) {
+      GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
+                    eps, re, nullptr, nullptr};
+      args.kmajor = forced_order();
+      const int T = N / 16;
+      const dim3 grid((T + tn - 1) / tn);
+#define RT_MT(P, E)                                                                                               \
+  do {                                                                                                            \
+    if (tn == 2 && tncfg == 802)                                                                                  \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 8, 2, 2>), grid, dim3(512), 0, stream, args);           \
+    else if (tn == 2 && tncfg == 404)                                                                             \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 4, 2>), grid, dim3(256), 0, stream, args);           \
+    else if (tn == 2)                                                                                             \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 2, 2>), grid, dim3(256), 0, stream, args);           \
+    else if (tncfg == 802)                                                                                        \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 8, 2, 4>), grid, dim3(512), 0, stream, args);           \
+    else                                                                                                          \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 2, 4>), grid, dim3(256), 0, stream, args);           \
+  } while (0)
+      if (pro == PRO_PLAIN && epi == EPI_STORE) RT_MT(PRO_PLAIN, EPI_STORE);
+      else if (pro == PRO_NORM && epi == EPI_STORE) RT_MT(PRO_NORM, EPI_STORE);
+      else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_MT(PRO_PLAIN, EPI_RESID);
+      else if (pro == PRO_NORM && epi == EPI_RESID) RT_MT(PRO_NORM, EPI_RESID);
+      else if (pro == PRO_NORM && epi == EPI_SWIGLU) RT_MT(PRO_NORM, EPI_SWIGLU);
+      else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_MT(PRO_PLAIN, EPI_SWIGLU);
+      else if (pro == PRO_NORM && epi == EPI_ROPE) RT_MT(PRO_NORM, EPI_ROPE);
+      else if (pro == PRO_PLAIN && epi == EPI_ROPE) RT_MT(PRO_PLAIN, EPI_ROPE);
+      else return -2;
+#undef RT_MT
       return hipGetLastError() == hipSuccess ? 0 : -6;
     }
   }

@@ -684,4 +684,197 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   if constexpr (EPI == EPI_AR) ar_exchange<NW>(p, tile, v, m, n, live, sm);
   __syncthreads();  // LDS reduction buffers are reused by the next tile
 }
+
+// ---- TN tiles per workgroup (serving batches, M > 4) ----------------------------------------
+// At M = 16 every k-step's activation fragment is 16 distinct rows, 1 KiB per wave — as many
+// bytes as its weight fragment — and a one-tile workgroup streams the whole activation matrix
+// through its CU for 16 output columns (lm_head, M = 16: 8016 tiles x 128 KiB of activation
+// reads per step; 235 us vs 148 us at M = 3). Here each workgroup owns TN consecutive tiles:
+// one activation fragment per k-step feeds TN MFMAs (TN weight streams), the activation reads
+// fall TN-fold. Plain / NORM prologues, STORE / RESID / SWIGLU / ROPE epilogues, no split, no
+// SC1 (one launch per GEMM); the M <= 4 decode path keeps gemm_tile.
+template <int NACC, int NW, int TN>
+struct GemmSmemN {
+  float red[NW][NACC * TN][16][17];
+  float sq[NW][16];
+};
+
+template <int PRO, int EPI, int U, int TN>
+struct StageN {
+  short8 w[U][TN];
+  short8 w2[(EPI == EPI_SWIGLU) ? U : 1][(EPI == EPI_SWIGLU) ? TN : 1];
+  short8 a[U];
+};
+
+template <int PRO, int EPI, int NW, int U, int TN>
+RT_DEVICE void issue_wn(StageN<PRO, EPI, U, TN>& st, const short8* const* wt, int s0, int nsteps, int lane,
+                        WStride ws) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int s = min(s0 + NW * u, nsteps - 1);   // unconditional, as issue_w
+    const size_t o = ws.off(s, krec<EPI>());
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      st.w[u][t] = __builtin_nontemporal_load(wt[t] + o + lane);
+      if constexpr (EPI == EPI_SWIGLU) st.w2[u][t] = __builtin_nontemporal_load(wt[t] + o + 64 + lane);
+    }
+  }
+}
+
+template <int PRO, int EPI, int NW, int U, int TN>
+RT_DEVICE void issue_an(StageN<PRO, EPI, U, TN>& st, const XSrc& xr, int s0, int nsteps) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) st.a[u] = ld_x8<false>(xr, min(s0 + NW * u, nsteps - 1) * 32);
+}
+
+template <int PRO, int EPI, int NW, int U, int TN>
+RT_DEVICE void consume_n(const StageN<PRO, EPI, U, TN>& st, float4_* acc, float4_* acc2, float& ssq, int s0,
+                         int nsteps) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (s0 + NW * u < nsteps) {
+      const bf16x8 a = __builtin_bit_cast(bf16x8, st.a[u]);
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u][t]), acc[t], 0, 0, 0);
+        if constexpr (EPI == EPI_SWIGLU)
+          acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u][t]), acc2[t], 0, 0, 0);
+      }
+      if constexpr (PRO != PRO_PLAIN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = rt::bf2f((uint16_t)st.a[u][j]);
+          ssq = fmaf(f, f, ssq);
+        }
+      }
+    }
+  }
+}
+
+// Tiles tile0 .. tile0 + TN - 1 (those >= N / 16 are computed on a clamped copy, never stored).
+template <int PRO, int EPI, int NW, int U, int TN>
+RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), NW, TN>& sm) {
+  static_assert(PRO == PRO_PLAIN || PRO == PRO_NORM, "multi-tile launches: plain / norm prologues");
+  static_assert(EPI != EPI_AR, "multi-tile launches: no all-reduce epilogue");
+  constexpr int NA = nacc<EPI>();
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int M = p.M, N = p.N, K = p.K;
+  const int T = N / 16, nsteps = K / 32;
+  const bool row_ok = r < M;
+  const XSrc xr = make_xsrc<false>(p.x, (size_t)(row_ok ? r : 0) * K + 8 * g);
+  WStride sstride;
+  const short8* wt[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) wt[t] = tile_base<EPI>(p, min(tile0 + t, T - 1), sstride);
+
+  float4_ acc[TN], acc2[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) acc[t] = acc2[t] = float4_{0.f, 0.f, 0.f, 0.f};
+  float ssq = 0.f;
+  StageN<PRO, EPI, U, TN> st0, st1;
+  constexpr int SPAN = NW * U;
+  const int w0 = wid;
+  const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
+  issue_wn<PRO, EPI, NW, U, TN>(st0, wt, w0, nsteps, lane, sstride);
+  issue_an<PRO, EPI, NW, U, TN>(st0, xr, w0, nsteps);
+  // epilogue operands independent of the GEMM, loaded under the k-loop (as gemm_tile)
+  const int em = min((int)(threadIdx.x >> 4), M - 1), en = threadIdx.x & 15;
+  float e_res[TN], e_c[TN], e_s[TN];
+  int64_t e_slot = 0;
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int tt = min(tile0 + t, T - 1);
+    e_res[t] = e_c[t] = e_s[t] = 0.f;
+    if constexpr (EPI == EPI_RESID) e_res[t] = ld16<false>(p.res + (size_t)em * N + tt * 16 + en);
+    if constexpr (EPI == EPI_ROPE) {
+      const RopeEpi& re = p.re;
+      const int pp = (tt * 16 + en) % re.D;
+      const float* cs = re.cos_sin + (size_t)re.positions[em] * re.D;
+      e_c[t] = cs[pp >> 1];
+      e_s[t] = cs[(re.D >> 1) + (pp >> 1)];
+    }
+  }
+  if constexpr (EPI == EPI_ROPE) e_slot = p.re.slots[em];
+  int j = 0;
+  for (; j + 1 < nst; j += 2) {
+    const int s = w0 + SPAN * j;
+    issue_wn<PRO, EPI, NW, U, TN>(st1, wt, s + SPAN, nsteps, lane, sstride);
+    issue_an<PRO, EPI, NW, U, TN>(st1, xr, s + SPAN, nsteps);
+    consume_n<PRO, EPI, NW, U, TN>(st0, acc, acc2, ssq, s, nsteps);
+    issue_wn<PRO, EPI, NW, U, TN>(st0, wt, s + 2 * SPAN, nsteps, lane, sstride);
+    issue_an<PRO, EPI, NW, U, TN>(st0, xr, s + 2 * SPAN, nsteps);
+    consume_n<PRO, EPI, NW, U, TN>(st1, acc, acc2, ssq, s + SPAN, nsteps);
+  }
+  if (j < nst) consume_n<PRO, EPI, NW, U, TN>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps);
+
+  // C layout per tile: acc[t][i] = C[m = 4g + i][n = r]
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sm.red[wid][NA * t][4 * g + i][r] = acc[t][i];
+      if constexpr (EPI == EPI_SWIGLU) sm.red[wid][NA * t + NA - 1][4 * g + i][r] = acc2[t][i];
+    }
+  if constexpr (PRO != PRO_PLAIN) {
+    ssq += __shfl_xor(ssq, 16, 64);
+    ssq += __shfl_xor(ssq, 32, 64);
+    if (g == 0) sm.sq[wid][r] = ssq;
+  }
+  __syncthreads();
+  const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
+  const bool live = threadIdx.x < 256 && m < M;
+  float inv = 1.f;
+  if constexpr (PRO != PRO_PLAIN) {
+    float ss = 0.f;
+    if (live) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) ss += sm.sq[w][m];
+    }
+    inv = rsqrtf(ss / (float)K + p.eps);
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int tile = tile0 + t;
+    float v = 0.f, up = 0.f;
+    if (live) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        v += sm.red[w][NA * t][m][n];
+        if constexpr (EPI == EPI_SWIGLU) up += sm.red[w][NA * t + NA - 1][m][n];
+      }
+    }
+    float vpartner = 0.f;
+    if constexpr (EPI == EPI_ROPE) vpartner = __shfl_xor(v, 1, 64);   // every lane takes part
+    if (live && tile < T) {
+      v *= inv;
+      const int col = tile * 16 + n;
+      if constexpr (EPI == EPI_SWIGLU) {
+        st16<false>(p.out + (size_t)m * p.ldo + col, silu(v) * (up * inv));
+      } else if constexpr (EPI == EPI_RESID) {
+        st16<false>(p.res + (size_t)m * N + col, v + e_res[t]);
+      } else if constexpr (EPI == EPI_ROPE) {
+        const RopeEpi& re = p.re;
+        const int D = re.D, half = D >> 1;
+        const int h = col / D, pp = col - h * D;
+        const int64_t blk = e_slot / re.BS;
+        const int off = (int)(e_slot - blk * re.BS);
+        if (h < re.Hq + re.Hkv) {
+          const float partner = vpartner * inv;
+          const int i = pp >> 1, hi = pp & 1;
+          const float y = hi ? fmaf(v, e_c[t], partner * e_s[t]) : fmaf(v, e_c[t], -partner * e_s[t]);
+          const int d = i + hi * half;
+          uint16_t* dst = (h < re.Hq) ? p.out + ((size_t)m * re.Hq + h) * D + d
+                                      : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
+          st16<false>(dst, y);
+        } else {
+          const int hv = h - re.Hq - re.Hkv;
+          st16<false>(re.v_cache + (((size_t)blk * re.Hkv + hv) * D + pp) * re.BS + off, v);
+        }
+      } else {
+        st16<false>(p.out + (size_t)m * p.ldo + col, v);
+      }
+    }
+  }
+}
 }  // namespace skinny
