@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_multi_kernel(GemmArgs p) 
   gemm_tiles<PRO, EPI, NW, U, TN>(p, blockIdx.x * TN, sm);
 }
 
+
 // the dynamic LDS of an ALDS launch: [16] row sums of squares, then the staged rows
 RT_DEVICE ALds alds_view(int kspan) {
   extern __shared__ float alds_dyn[];
@@ -118,6 +119,26 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_splitk_kernel(GemmArgs p,
   } else {
     gemm_tile<PRO, EPI, NW, U, false>(p, tile, sm, st0, false, tile == 0, &sx);
   }
+}
+
+// TN tiles per workgroup (gemm_tiles) with each group of TN tiles' K range cut into S parts (SplitX hand-off; group ids dealt as
+// in skinny_gemm_splitk_kernel, so a group's parts share an XCD under round-robin dispatch)
+template <int PRO, int EPI, int NW, int U, int TN>
+__global__ void __launch_bounds__(NW * 64) skinny_gemm_multi_split_kernel(GemmArgs p, int* __restrict__ ws, int S) {
+  __shared__ GemmSmemN<nacc<EPI>(), NW, TN> sm;
+  const int G = (p.N / 16 + TN - 1) / TN;
+  const int b = blockIdx.x;
+  int grp, part;
+  if ((G & 7) == 0) {
+    const int j = b >> 3;
+    grp = (j / S) * 8 + (b & 7);
+    part = j % S;
+  } else {
+    grp = b / S;
+    part = b % S;
+  }
+  const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)grp * S * TN * SPLIT_STRIDE, ws + grp, part, S};
+  gemm_tiles<PRO, EPI, NW, U, TN>(p, grp * TN, sm, &sx);
 }
 
 int device_cus() {
@@ -352,6 +373,35 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     }();
     const int T16 = N / 16, cus = device_cus(), need = cus * 3 / 4;
     const int tn = tn_env >= 0 ? tn_env : (cus <= 0 ? 1 : (T16 / 4 >= need ? 4 : (T16 / 2 >= need ? 2 : 1)));
+    // one tile per workgroup would still fill the chip (o / down: 256 tiles): two tiles per
+    // workgroup over two K halves keep the workgroup count and halve the activation reads — from
+    // 9 rows on (M = 16: down 28.8 -> 23.6 us, o 11.0 -> 10.6; M = 8: o 8.8 -> 10.0, down even,
+    // profiles/r05/gemm_multi_tile.md). RT_SKINNY_TNS=0 keeps one tile.
+    static const int tns_env = [] {
+      const char* e = getenv("RT_SKINNY_TNS");
+      return e ? atoi(e) : 1;
+    }();
+    const int G2 = (T16 + 1) / 2;
+    if (tn == 1 && tn_env < 0 && tns_env && M > 8 && cus > 0 && T16 >= need && G2 <= SPLIT_CTRS && K / 32 >= 32 &&
+        split_ws != nullptr && split_ws_ints >= (int64_t)SPLIT_CTRS + (int64_t)G2 * 2 * 2 * SPLIT_STRIDE) {
+      GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
+                    eps, re, nullptr, nullptr};
+      args.kmajor = forced_order();
+      const dim3 grid(G2 * 2);
+#define RT_MS(P, E)                                                                                               \
+  hipLaunchKernelGGL((skinny_gemm_multi_split_kernel<P, E, 4, 2, 2>), grid, dim3(256), 0, stream, args, split_ws, 2)
+      if (pro == PRO_PLAIN && epi == EPI_STORE) RT_MS(PRO_PLAIN, EPI_STORE);
+      else if (pro == PRO_NORM && epi == EPI_STORE) RT_MS(PRO_NORM, EPI_STORE);
+      else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_MS(PRO_PLAIN, EPI_RESID);
+      else if (pro == PRO_NORM && epi == EPI_RESID) RT_MS(PRO_NORM, EPI_RESID);
+      else if (pro == PRO_NORM && epi == EPI_SWIGLU) RT_MS(PRO_NORM, EPI_SWIGLU);
+      else if (pro == PRO_PLAIN && epi == EPI_SWIGLU) RT_MS(PRO_PLAIN, EPI_SWIGLU);
+      else if (pro == PRO_NORM && epi == EPI_ROPE) RT_MS(PRO_NORM, EPI_ROPE);
+      else if (pro == PRO_PLAIN && epi == EPI_ROPE) RT_MS(PRO_PLAIN, EPI_ROPE);
+      else return -2;
+#undef RT_MS
+      return hipGetLastError() == hipSuccess ? 0 : -6;
+    }
     if (tn == 2 || tn == 4) {
       GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
                     eps, re, nullptr, nullptr};

@@ -752,15 +752,22 @@ RT_DEVICE void consume_n(const StageN<PRO, EPI, U, TN>& st, float4_* acc, float4
 }
 
 // Tiles tile0 .. tile0 + TN - 1 (those >= N / 16 are computed on a clamped copy, never stored).
+// `sx` (optional): this workgroup runs part sx->idx of sx->n K ranges of the TN tiles; partial
+// sums are handed over as in gemm_tile (sx->part holds [n][TN][SPLIT_STRIDE]) and the last
+// arrival sums the parts in index order and runs the epilogue — the o / down shapes (256 tiles)
+// keep a workgroup per CU while each workgroup reads the activations for two tiles.
 template <int PRO, int EPI, int NW, int U, int TN>
-RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), NW, TN>& sm) {
+RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), NW, TN>& sm,
+                          const SplitX* sx = nullptr) {
   static_assert(PRO == PRO_PLAIN || PRO == PRO_NORM, "multi-tile launches: plain / norm prologues");
   static_assert(EPI != EPI_AR, "multi-tile launches: no all-reduce epilogue");
   constexpr int NA = nacc<EPI>();
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int M = p.M, N = p.N, K = p.K;
-  const int T = N / 16, nsteps = K / 32;
+  const int T = N / 16, ksteps = K / 32;
+  const int s_lo = sx != nullptr ? (int)((long)ksteps * sx->idx / sx->n) : 0;
+  const int nsteps = sx != nullptr ? (int)((long)ksteps * (sx->idx + 1) / sx->n) : ksteps;
   const bool row_ok = r < M;
   const XSrc xr = make_xsrc<false>(p.x, (size_t)(row_ok ? r : 0) * K + 8 * g);
   WStride sstride;
@@ -774,7 +781,7 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
   float ssq = 0.f;
   StageN<PRO, EPI, U, TN> st0, st1;
   constexpr int SPAN = NW * U;
-  const int w0 = wid;
+  const int w0 = s_lo + wid;
   const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
   issue_wn<PRO, EPI, NW, U, TN>(st0, wt, w0, nsteps, lane, sstride);
   issue_an<PRO, EPI, NW, U, TN>(st0, xr, w0, nsteps);
@@ -824,26 +831,80 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
   __syncthreads();
   const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
   const bool live = threadIdx.x < 256 && m < M;
-  float inv = 1.f;
-  if constexpr (PRO != PRO_PLAIN) {
-    float ss = 0.f;
-    if (live) {
+  float ss = 0.f;
+  float vs[TN], ups[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) vs[t] = ups[t] = 0.f;
+  if (live) {
+    if constexpr (PRO != PRO_PLAIN) {
 #pragma unroll
       for (int w = 0; w < NW; ++w) ss += sm.sq[w][m];
     }
-    inv = rsqrtf(ss / (float)K + p.eps);
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        vs[t] += sm.red[w][NA * t][m][n];
+        if constexpr (EPI == EPI_SWIGLU) ups[t] += sm.red[w][NA * t + NA - 1][m][n];
+      }
   }
+  if (sx != nullptr) {   // hand-off as gemm_tile: sc1 payload -> vmcnt(0) -> barrier -> one add
+    float* mine = sx->part + (size_t)sx->idx * TN * SPLIT_STRIDE;
+    if (live) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        __hip_atomic_store(mine + t * SPLIT_STRIDE + threadIdx.x, vs[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (EPI == EPI_SWIGLU)
+          __hip_atomic_store(mine + t * SPLIT_STRIDE + 256 + threadIdx.x, ups[t], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (n == 0) __hip_atomic_store(mine + 512 + m, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(sx->ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = prev == sx->n - 1;
+      sm.sq[0][0] = last ? 1.f : 0.f;
+      if (last) __hip_atomic_store(sx->ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (sm.sq[0][0] == 0.f) return;   // not last: another workgroup finishes the tiles
+    if (live) {
+      float ss_sum = 0.f;
+      float v_sum[TN], up_sum[TN];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) v_sum[t] = up_sum[t] = 0.f;
+      for (int i = 0; i < sx->n; ++i) {   // fixed order: bit-identical whoever arrives last
+        const float* pi = sx->part + (size_t)i * TN * SPLIT_STRIDE;
+        const bool own = i == sx->idx;
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          v_sum[t] += own ? vs[t]
+                          : __hip_atomic_load(pi + t * SPLIT_STRIDE + threadIdx.x, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+          if constexpr (EPI == EPI_SWIGLU)
+            up_sum[t] += own ? ups[t]
+                             : __hip_atomic_load(pi + t * SPLIT_STRIDE + 256 + threadIdx.x, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if constexpr (PRO != PRO_PLAIN)
+          ss_sum += own ? ss : __hip_atomic_load(pi + 512 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ss = ss_sum;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        vs[t] = v_sum[t];
+        ups[t] = up_sum[t];
+      }
+    }
+  }
+  float inv = 1.f;
+  if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss / (float)K + p.eps);
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
     const int tile = tile0 + t;
-    float v = 0.f, up = 0.f;
-    if (live) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        v += sm.red[w][NA * t][m][n];
-        if constexpr (EPI == EPI_SWIGLU) up += sm.red[w][NA * t + NA - 1][m][n];
-      }
-    }
+    float v = vs[t], up = ups[t];
     float vpartner = 0.f;
     if constexpr (EPI == EPI_ROPE) vpartner = __shfl_xor(v, 1, 64);   // every lane takes part
     if (live && tile < T) {

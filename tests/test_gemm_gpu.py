@@ -79,6 +79,41 @@ def test_skinny_gemm_balanced_split(M, N, K):
     close(ops.skinny_gemm(x, Ws2, ops.PRO_NORM, ops.EPI_SWIGLU), outs[0], 0.02, 0.02)
 
 
+@pytest.mark.parametrize("M", [5, 8, 12, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (128256, 4096), (6144, 4096)])
+def test_skinny_gemm_serving_batch_multi_tile(M, N, K):
+    """Serving batches (M > 4): several tiles per workgroup share each activation fragment
+    (skinny_core.h gemm_tiles) — o / down (256 tiles, M > 8) as two tiles over two K halves with
+    the split hand-off, qkv-sized (384 tiles) two tiles, lm_head-sized four. Against the fp32 oracle
+    on the norm / residual / SwiGLU epilogues, deterministic over repeats, counters re-armed;
+    the same GEMMs with the multi-tile launches off (RT_SKINNY_TN=1 is read once per process, so
+    the one-tile launch is checked through M = 3 rows of the same operands instead)."""
+    x = bf(M, K, seed=71)
+    gam = bf(K, seed=72)
+    ws = ops.split_workspace(DEV)
+    W = bf(N, K, scale=0.05, seed=73)
+    Wg = ops.shuffle_weight(W, gam)
+    exp = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W.cpu(), gam.cpu()), 1, eps=1e-5).to(DEV)
+    outs = [ops.skinny_gemm(x, Wg, ops.PRO_NORM, split_ws=ws) for _ in range(3)]
+    for o in outs:
+        close(o, exp, 0.05, 0.02)
+        assert torch.equal(o, outs[0])
+    assert int(ws[:256].abs().sum()) == 0, "split counters must re-arm to zero"
+    # the first 3 rows through the M <= 4 one-tile launch: same values up to summation order
+    close(ops.skinny_gemm(x[:3].contiguous(), Wg, ops.PRO_NORM, split_ws=ws), outs[0][:3], 0.02, 0.02)
+    Ws = ops.shuffle_weight(W)
+    res = bf(M, N, seed=74)
+    res_ref = res.cpu().clone()
+    ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=ws)
+    ref.skinny_gemm(x.cpu(), W.cpu(), 0, 1, res=res_ref)
+    close(res, res_ref.to(DEV), 0.06, 0.02)
+    if N <= 14336:
+        W2 = bf(2 * N, K, scale=0.05, seed=75)
+        got = ops.skinny_gemm(x, ops.shuffle_weight(W2, gam, swiglu=True), ops.PRO_NORM, ops.EPI_SWIGLU, split_ws=ws)
+        close(got, ref.skinny_gemm(x.cpu(), ref.fold_gamma(W2.cpu(), gam.cpu()), 1, 2).to(DEV), 0.05, 0.03)
+    assert int(ws[:256].abs().sum()) == 0
+
+
 def test_shuffle_layout():
     N, K = 32, 64
     W = torch.arange(N * K, device=DEV).reshape(N, K).to(torch.float32).to(torch.bfloat16)

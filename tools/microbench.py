@@ -80,6 +80,8 @@ def bench_gemm(M):
         ("gate_up (norm+swiglu)", 2 * ffn, hid),
         ("gate_up balanced (norm+swiglu, split remainder)", 2 * ffn, hid),
         ("down (+resid)", hid, ffn),
+        ("o    (+resid, split ws as the engine)", hid, hq * d),
+        ("down (+resid, split ws as the engine)", hid, ffn),
         ("lm_head (norm)", vocab, hid),
         ("gate_up-plain (norm, unpaired)", 2 * ffn, hid),
     ]
@@ -94,6 +96,11 @@ def bench_gemm(M):
                                                          hkv, d, split_ws=sws)
         elif name.startswith("qkv"):
             fn = lambda i: ops.skinny_gemm_rope(x, Ws[i % copies], ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d)
+        elif "split ws" in name:      # the engine's row-parallel call (parallel/tp.py row_parallel)
+            inp = x if name.startswith("o ") else g_in
+            sws = ops.split_workspace(DEV)
+            fn = lambda i, inp=inp, sws=sws: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_RESID, res=res,
+                                                             split_ws=sws, split_mode=ops.SPLIT_K)
         elif name.startswith("o ") or name.startswith("down"):
             inp = x if name.startswith("o ") else g_in
             fn = lambda i, inp=inp: ops.skinny_gemm(inp, Ws[i % copies], ops.PRO_PLAIN, ops.EPI_RESID, res=res)
