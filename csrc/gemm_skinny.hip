@@ -360,7 +360,14 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
   // (TN 4), qkv 16.7 -> 13.5 (TN 2); o / down (256 tiles) lose with fewer workgroups and keep one
   // tile. RT_SKINNY_TN=<TN> (1 = off) pins the tile count, RT_SKINNY_TNCFG=<NW>x<U> the variant
   // (microbenchmarks); the M <= 4 decode path is unchanged.
-  if (M > 4 && (pro == PRO_PLAIN || pro == PRO_NORM) && epi != EPI_AR) {
+  // A/B knob: the smallest M the multi-tile rule applies to (M = 3 gains nothing: the activation
+  // fragments of 3 rows are L1 hits, profiles/r05/gemm_multi_tile.md); RT_SKINNY_TNS=2 forces the
+  // two-tile K-split below 9 rows
+  static const int tn_min_m = [] {
+    const char* e = getenv("RT_SKINNY_TN_MINM");
+    return e ? atoi(e) : 5;
+  }();
+  if (M >= tn_min_m && (pro == PRO_PLAIN || pro == PRO_NORM) && epi != EPI_AR) {
     static const int tn_env = [] {
       const char* e = getenv("RT_SKINNY_TN");
       return e ? atoi(e) : -1;
@@ -382,7 +389,7 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
       return e ? atoi(e) : 1;
     }();
     const int G2 = (T16 + 1) / 2;
-    if (tn == 1 && tn_env < 0 && tns_env && M > 8 && cus > 0 && T16 >= need && G2 <= SPLIT_CTRS && K / 32 >= 32 &&
+    if (tn == 1 && tn_env < 0 && tns_env && (M > 8 || tns_env == 2) && cus > 0 && T16 >= need && G2 <= SPLIT_CTRS && K / 32 >= 32 &&
         split_ws != nullptr && split_ws_ints >= (int64_t)SPLIT_CTRS + (int64_t)G2 * 2 * 2 * SPLIT_STRIDE) {
       GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
                     eps, re, nullptr, nullptr};
