@@ -364,7 +364,7 @@ void skinny_gemm(torch::Tensor out, torch::Tensor x, torch::Tensor Ws, int64_t p
   check_bf16(Ws, "Ws");
   TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm: x [M,K], Ws [N,K]");
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(M >= 1 && M <= 16, "skinny_gemm: 1 <= M <= 16");
+  TORCH_CHECK(M >= 1 && M <= 32, "skinny_gemm: 1 <= M <= 32");
   TORCH_CHECK(K % 32 == 0, "skinny_gemm: K must be a multiple of 32");
   int64_t N = Ws.size(0);
   if (epi == 2) {
@@ -410,7 +410,7 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   check_bf16(Ws, "Ws");
   TORCH_CHECK(x.dim() == 2 && Ws.dim() == 2 && x.size(1) == Ws.size(1), "skinny_gemm_rope: x [M,K], Ws [N,K]");
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(M >= 1 && M <= 16 && K % 32 == 0, "skinny_gemm_rope: 1 <= M <= 16, K % 32 == 0");
+  TORCH_CHECK(M >= 1 && M <= 32 && K % 32 == 0, "skinny_gemm_rope: 1 <= M <= 32, K % 32 == 0");
   TORCH_CHECK(Ws.size(0) == (Hq + 2 * Hkv) * D && D % 16 == 0, "skinny_gemm_rope: Ws must be [(Hq+2Hkv)*D, K]");
   TORCH_CHECK(q_out.numel() == M * Hq * D, "q_out must be [M, Hq, D]");
   check_type(positions, torch::kInt64, "positions");

@@ -33,10 +33,13 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_kernel(GemmArgs p) {
 }
 
 // TN tiles per workgroup (skinny_core.h gemm_tiles): serving batches, M > 4
-template <int PRO, int EPI, int NW, int U, int TN>
+template <int PRO, int EPI, int NW, int U, int TN, int MB = 1>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_multi_kernel(GemmArgs p) {
-  __shared__ GemmSmemN<nacc<EPI>(), NW, TN> sm;
-  gemm_tiles<PRO, EPI, NW, U, TN>(p, blockIdx.x * TN, sm);
+  // two row blocks x (gate + up) x 4 tiles would not fit the static LDS: that variant is never
+  // launched (the dispatcher caps SwiGLU at 2 tiles with two row blocks), compiled as 2 tiles
+  constexpr int TNX = (MB == 2 && nacc<EPI>() == 2 && TN > 2) ? 2 : TN;
+  __shared__ GemmSmemN<nacc<EPI>(), NW, TNX, MB> sm;
+  gemm_tiles<PRO, EPI, NW, U, TNX, MB>(p, blockIdx.x * TNX, sm);
 }
 
 
@@ -123,9 +126,9 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_splitk_kernel(GemmArgs p,
 
 // TN tiles per workgroup (gemm_tiles) with each group of TN tiles' K range cut into S parts (SplitX hand-off; group ids dealt as
 // in skinny_gemm_splitk_kernel, so a group's parts share an XCD under round-robin dispatch)
-template <int PRO, int EPI, int NW, int U, int TN>
+template <int PRO, int EPI, int NW, int U, int TN, int MB = 1>
 __global__ void __launch_bounds__(NW * 64) skinny_gemm_multi_split_kernel(GemmArgs p, int* __restrict__ ws, int S) {
-  __shared__ GemmSmemN<nacc<EPI>(), NW, TN> sm;
+  __shared__ GemmSmemN<nacc<EPI>(), NW, TN, MB> sm;
   const int G = (p.N / 16 + TN - 1) / TN;
   const int b = blockIdx.x;
   int grp, part;
@@ -137,8 +140,9 @@ __global__ void __launch_bounds__(NW * 64) skinny_gemm_multi_split_kernel(GemmAr
     grp = b / S;
     part = b % S;
   }
-  const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)grp * S * TN * SPLIT_STRIDE, ws + grp, part, S};
-  gemm_tiles<PRO, EPI, NW, U, TN>(p, grp * TN, sm, &sx);
+  const SplitX sx{reinterpret_cast<float*>(ws + SPLIT_CTRS) + (size_t)grp * S * TN * MB * SPLIT_STRIDE, ws + grp, part,
+                  S};
+  gemm_tiles<PRO, EPI, NW, U, TN, MB>(p, grp * TN, sm, &sx);
 }
 
 int device_cus() {
@@ -298,7 +302,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
                        int pro, int epi, const void* rope, const void* x2, void* xo, hipStream_t stream,
                        int* split_ws, int64_t split_ws_ints, int split_mode) {
   if (pro == PRO_NORM_ADD && x2 == nullptr) return -5;
-  if (M < 1 || M > 16 || K % 32 || N % 16) return -1;
+  // 17..32 rows: only the multi-tile launches below (two 16-row blocks per MFMA pass)
+  if (M < 1 || M > 32 || K % 32 || N % 16) return -1;
+  if (M > 16 && (pro == PRO_NORM_ADD || epi == EPI_AR)) return -1;
   RopeEpi re{};
   if (epi == EPI_ROPE) {
     if (rope == nullptr) return -3;
@@ -306,7 +312,7 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     if (re.D % 16 || N != (re.Hq + 2 * re.Hkv) * re.D) return -4;
   }
   // split-K (split_mode bit 1) when the shape has fewer tiles than CUs: tensor-parallel shards
-  if (split_ws != nullptr && (split_mode & 2)) {
+  if (split_ws != nullptr && (split_mode & 2) && M <= 16) {
     const int T = N / 16;
     const int S = splitk_parts(T, K / 32, device_cus(), split_ws_ints);
     if (S >= 2) {
@@ -367,7 +373,8 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     const char* e = getenv("RT_SKINNY_TN_MINM");
     return e ? atoi(e) : 5;
   }();
-  if (M >= tn_min_m && (pro == PRO_PLAIN || pro == PRO_NORM) && epi != EPI_AR) {
+  if ((M >= tn_min_m || M > 16) && (pro == PRO_PLAIN || pro == PRO_NORM) && epi != EPI_AR) {
+    const int MB = M > 16 ? 2 : 1;
     static const int tn_env = [] {
       const char* e = getenv("RT_SKINNY_TN");
       return e ? atoi(e) : -1;
@@ -379,7 +386,9 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
       return nw * 100 + u;
     }();
     const int T16 = N / 16, cus = device_cus(), need = cus * 3 / 4;
-    const int tn = tn_env >= 0 ? tn_env : (cus <= 0 ? 1 : (T16 / 4 >= need ? 4 : (T16 / 2 >= need ? 2 : 1)));
+    int tn = tn_env >= 0 ? tn_env : (cus <= 0 ? 1 : (T16 / 4 >= need ? 4 : (T16 / 2 >= need ? 2 : 1)));
+    // LDS: two row blocks x (gate + up) x 4 tiles would not fit
+    if (MB == 2) tn = tn >= 4 && epi != EPI_SWIGLU ? 4 : (tn >= 2 ? 2 : 1);
     // one tile per workgroup would still fill the chip (o / down: 256 tiles): two tiles per
     // workgroup over two K halves keep the workgroup count and halve the activation reads — from
     // 9 rows on (M = 16: down 28.8 -> 23.6 us, o 11.0 -> 10.6; M = 8: o 8.8 -> 10.0, down even,
@@ -390,13 +399,20 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
     }();
     const int G2 = (T16 + 1) / 2;
     if (tn == 1 && tn_env < 0 && tns_env && (M > 8 || tns_env == 2) && cus > 0 && T16 >= need && G2 <= SPLIT_CTRS && K / 32 >= 32 &&
-        split_ws != nullptr && split_ws_ints >= (int64_t)SPLIT_CTRS + (int64_t)G2 * 2 * 2 * SPLIT_STRIDE) {
+        split_ws != nullptr && split_ws_ints >= (int64_t)SPLIT_CTRS + (int64_t)G2 * 2 * 2 * MB * SPLIT_STRIDE) {
       GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
                     eps, re, nullptr, nullptr};
       args.kmajor = forced_order();
       const dim3 grid(G2 * 2);
 #define RT_MS(P, E)                                                                                               \
-  hipLaunchKernelGGL((skinny_gemm_multi_split_kernel<P, E, 4, 2, 2>), grid, dim3(256), 0, stream, args, split_ws, 2)
+  do {                                                                                                            \
+    if (MB == 2)                                                                                                  \
+      hipLaunchKernelGGL((skinny_gemm_multi_split_kernel<P, E, 4, 2, 2, 2>), grid, dim3(256), 0, stream, args,    \
+                         split_ws, 2);                                                                            \
+    else                                                                                                          \
+      hipLaunchKernelGGL((skinny_gemm_multi_split_kernel<P, E, 4, 2, 2>), grid, dim3(256), 0, stream, args,       \
+                         split_ws, 2);                                                                            \
+  } while (0)
       if (pro == PRO_PLAIN && epi == EPI_STORE) RT_MS(PRO_PLAIN, EPI_STORE);
       else if (pro == PRO_NORM && epi == EPI_STORE) RT_MS(PRO_NORM, EPI_STORE);
       else if (pro == PRO_PLAIN && epi == EPI_RESID) RT_MS(PRO_PLAIN, EPI_RESID);
@@ -409,7 +425,7 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
 #undef RT_MS
       return hipGetLastError() == hipSuccess ? 0 : -6;
     }
-    if (tn == 2 || tn == 4) {
+    if (tn == 2 || tn == 4 || MB == 2) {
       GemmArgs args{(uint16_t*)out, (const uint16_t*)x, (const short8*)Ws, (uint16_t*)res, M, N, K, ldo,
                     eps, re, nullptr, nullptr};
       args.kmajor = forced_order();
@@ -417,7 +433,13 @@ int launch_skinny_gemm(void* out, const void* x, const void* Ws, void* res, int 
       const dim3 grid((T + tn - 1) / tn);
 #define RT_MT(P, E)                                                                                               \
   do {                                                                                                            \
-    if (tn == 2 && tncfg == 802)                                                                                  \
+    if (MB == 2 && tn == 4)                                                                                       \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 2, 4, 2>), grid, dim3(256), 0, stream, args);        \
+    else if (MB == 2 && tn == 2)                                                                                  \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 2, 2, 2>), grid, dim3(256), 0, stream, args);        \
+    else if (MB == 2)                                                                                             \
+      hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 2, 1, 2>), grid, dim3(256), 0, stream, args);        \
+    else if (tn == 2 && tncfg == 802)                                                                             \
       hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 8, 2, 2>), grid, dim3(512), 0, stream, args);           \
     else if (tn == 2 && tncfg == 404)                                                                             \
       hipLaunchKernelGGL((skinny_gemm_multi_kernel<P, E, 4, 4, 2>), grid, dim3(256), 0, stream, args);           \

@@ -691,23 +691,25 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
 // through its CU for 16 output columns (lm_head, M = 16: 8016 tiles x 128 KiB of activation
 // reads per step; 235 us vs 148 us at M = 3). Here each workgroup owns TN consecutive tiles:
 // one activation fragment per k-step feeds TN MFMAs (TN weight streams), the activation reads
-// fall TN-fold. Plain / NORM prologues, STORE / RESID / SWIGLU / ROPE epilogues, no split, no
-// SC1 (one launch per GEMM); the M <= 4 decode path keeps gemm_tile.
-template <int NACC, int NW, int TN>
+// fall TN-fold. MB = 2 row blocks (17..32 rows): every weight fragment feeds both blocks' MFMAs,
+// so a 32-row batch streams the weights once. Plain / NORM prologues, STORE / RESID / SWIGLU /
+// ROPE epilogues, optional K split, no SC1 (one launch per GEMM); the M <= 4 decode path keeps
+// gemm_tile.
+template <int NACC, int NW, int TN, int MB>
 struct GemmSmemN {
-  float red[NW][NACC * TN][16][17];
-  float sq[NW][16];
+  float red[NW][NACC * TN * MB][16][17];
+  float sq[NW][16 * MB];
 };
 
-template <int PRO, int EPI, int U, int TN>
+template <int PRO, int EPI, int U, int TN, int MB>
 struct StageN {
   short8 w[U][TN];
   short8 w2[(EPI == EPI_SWIGLU) ? U : 1][(EPI == EPI_SWIGLU) ? TN : 1];
-  short8 a[U];
+  short8 a[U][MB];
 };
 
-template <int PRO, int EPI, int NW, int U, int TN>
-RT_DEVICE void issue_wn(StageN<PRO, EPI, U, TN>& st, const short8* const* wt, int s0, int nsteps, int lane,
+template <int PRO, int EPI, int NW, int U, int TN, int MB>
+RT_DEVICE void issue_wn(StageN<PRO, EPI, U, TN, MB>& st, const short8* const* wt, int s0, int nsteps, int lane,
                         WStride ws) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -721,30 +723,37 @@ RT_DEVICE void issue_wn(StageN<PRO, EPI, U, TN>& st, const short8* const* wt, in
   }
 }
 
-template <int PRO, int EPI, int NW, int U, int TN>
-RT_DEVICE void issue_an(StageN<PRO, EPI, U, TN>& st, const XSrc& xr, int s0, int nsteps) {
+template <int PRO, int EPI, int NW, int U, int TN, int MB>
+RT_DEVICE void issue_an(StageN<PRO, EPI, U, TN, MB>& st, const XSrc* xr, int s0, int nsteps) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) st.a[u] = ld_x8<false>(xr, min(s0 + NW * u, nsteps - 1) * 32);
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) st.a[u][b] = ld_x8<false>(xr[b], min(s0 + NW * u, nsteps - 1) * 32);
 }
 
-template <int PRO, int EPI, int NW, int U, int TN>
-RT_DEVICE void consume_n(const StageN<PRO, EPI, U, TN>& st, float4_* acc, float4_* acc2, float& ssq, int s0,
-                         int nsteps) {
+// acc / acc2: [TN][MB] accumulators, ssq: [MB]
+template <int PRO, int EPI, int NW, int U, int TN, int MB>
+RT_DEVICE void consume_n(const StageN<PRO, EPI, U, TN, MB>& st, float4_ (*acc)[MB], float4_ (*acc2)[MB], float* ssq,
+                         int s0, int nsteps) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (s0 + NW * u < nsteps) {
-      const bf16x8 a = __builtin_bit_cast(bf16x8, st.a[u]);
 #pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u][t]), acc[t], 0, 0, 0);
-        if constexpr (EPI == EPI_SWIGLU)
-          acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u][t]), acc2[t], 0, 0, 0);
-      }
-      if constexpr (PRO != PRO_PLAIN) {
+      for (int b = 0; b < MB; ++b) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, st.a[u][b]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = rt::bf2f((uint16_t)st.a[u][j]);
-          ssq = fmaf(f, f, ssq);
+        for (int t = 0; t < TN; ++t) {
+          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w[u][t]), acc[t][b], 0, 0, 0);
+          if constexpr (EPI == EPI_SWIGLU)
+            acc2[t][b] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, st.w2[u][t]), acc2[t][b], 0, 0, 0);
+        }
+        if constexpr (PRO != PRO_PLAIN) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float f = rt::bf2f((uint16_t)st.a[u][b][j]);
+            ssq[b] = fmaf(f, f, ssq[b]);
+          }
         }
       }
     }
@@ -753,11 +762,11 @@ RT_DEVICE void consume_n(const StageN<PRO, EPI, U, TN>& st, float4_* acc, float4
 
 // Tiles tile0 .. tile0 + TN - 1 (those >= N / 16 are computed on a clamped copy, never stored).
 // `sx` (optional): this workgroup runs part sx->idx of sx->n K ranges of the TN tiles; partial
-// sums are handed over as in gemm_tile (sx->part holds [n][TN][SPLIT_STRIDE]) and the last
+// sums are handed over as in gemm_tile (sx->part holds [n][TN][MB][SPLIT_STRIDE]) and the last
 // arrival sums the parts in index order and runs the epilogue — the o / down shapes (256 tiles)
 // keep a workgroup per CU while each workgroup reads the activations for two tiles.
-template <int PRO, int EPI, int NW, int U, int TN>
-RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), NW, TN>& sm,
+template <int PRO, int EPI, int NW, int U, int TN, int MB>
+RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), NW, TN, MB>& sm,
                           const SplitX* sx = nullptr) {
   static_assert(PRO == PRO_PLAIN || PRO == PRO_NORM, "multi-tile launches: plain / norm prologues");
   static_assert(EPI != EPI_AR, "multi-tile launches: no all-reduce epilogue");
@@ -768,97 +777,125 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
   const int T = N / 16, ksteps = K / 32;
   const int s_lo = sx != nullptr ? (int)((long)ksteps * sx->idx / sx->n) : 0;
   const int nsteps = sx != nullptr ? (int)((long)ksteps * (sx->idx + 1) / sx->n) : ksteps;
-  const bool row_ok = r < M;
-  const XSrc xr = make_xsrc<false>(p.x, (size_t)(row_ok ? r : 0) * K + 8 * g);
+  XSrc xr[MB];
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    const int row = 16 * b + r;
+    xr[b] = make_xsrc<false>(p.x, (size_t)(row < M ? row : 0) * K + 8 * g);   // rows >= M read row 0
+  }
   WStride sstride;
   const short8* wt[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) wt[t] = tile_base<EPI>(p, min(tile0 + t, T - 1), sstride);
 
-  float4_ acc[TN], acc2[TN];
+  float4_ acc[TN][MB], acc2[TN][MB];
+  float ssq[MB];
 #pragma unroll
-  for (int t = 0; t < TN; ++t) acc[t] = acc2[t] = float4_{0.f, 0.f, 0.f, 0.f};
-  float ssq = 0.f;
-  StageN<PRO, EPI, U, TN> st0, st1;
+  for (int b = 0; b < MB; ++b) {
+    ssq[b] = 0.f;
+#pragma unroll
+    for (int t = 0; t < TN; ++t) acc[t][b] = acc2[t][b] = float4_{0.f, 0.f, 0.f, 0.f};
+  }
+  StageN<PRO, EPI, U, TN, MB> st0, st1;
   constexpr int SPAN = NW * U;
   const int w0 = s_lo + wid;
   const int nst = w0 < nsteps ? (nsteps - w0 + SPAN - 1) / SPAN : 0;
-  issue_wn<PRO, EPI, NW, U, TN>(st0, wt, w0, nsteps, lane, sstride);
-  issue_an<PRO, EPI, NW, U, TN>(st0, xr, w0, nsteps);
-  // epilogue operands independent of the GEMM, loaded under the k-loop (as gemm_tile)
-  const int em = min((int)(threadIdx.x >> 4), M - 1), en = threadIdx.x & 15;
-  float e_res[TN], e_c[TN], e_s[TN];
-  int64_t e_slot = 0;
+  issue_wn<PRO, EPI, NW, U, TN, MB>(st0, wt, w0, nsteps, lane, sstride);
+  issue_an<PRO, EPI, NW, U, TN, MB>(st0, xr, w0, nsteps);
+  // epilogue operands independent of the GEMM, loaded under the k-loop (as gemm_tile); the
+  // epilogue thread (em, en) of row block b owns row 16 b + em
+  const int em = threadIdx.x >> 4, en = threadIdx.x & 15;
+  float e_res[TN][MB], e_c[TN][MB], e_s[TN][MB];
+  int64_t e_slot[MB];
 #pragma unroll
-  for (int t = 0; t < TN; ++t) {
-    const int tt = min(tile0 + t, T - 1);
-    e_res[t] = e_c[t] = e_s[t] = 0.f;
-    if constexpr (EPI == EPI_RESID) e_res[t] = ld16<false>(p.res + (size_t)em * N + tt * 16 + en);
-    if constexpr (EPI == EPI_ROPE) {
-      const RopeEpi& re = p.re;
-      const int pp = (tt * 16 + en) % re.D;
-      const float* cs = re.cos_sin + (size_t)re.positions[em] * re.D;
-      e_c[t] = cs[pp >> 1];
-      e_s[t] = cs[(re.D >> 1) + (pp >> 1)];
+  for (int b = 0; b < MB; ++b) {
+    const int row = min(16 * b + em, M - 1);
+    e_slot[b] = 0;
+    if constexpr (EPI == EPI_ROPE) e_slot[b] = p.re.slots[row];
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const int tt = min(tile0 + t, T - 1);
+      e_res[t][b] = e_c[t][b] = e_s[t][b] = 0.f;
+      if constexpr (EPI == EPI_RESID) e_res[t][b] = ld16<false>(p.res + (size_t)row * N + tt * 16 + en);
+      if constexpr (EPI == EPI_ROPE) {
+        const RopeEpi& re = p.re;
+        const int pp = (tt * 16 + en) % re.D;
+        const float* cs = re.cos_sin + (size_t)re.positions[row] * re.D;
+        e_c[t][b] = cs[pp >> 1];
+        e_s[t][b] = cs[(re.D >> 1) + (pp >> 1)];
+      }
     }
   }
-  if constexpr (EPI == EPI_ROPE) e_slot = p.re.slots[em];
   int j = 0;
   for (; j + 1 < nst; j += 2) {
     const int s = w0 + SPAN * j;
-    issue_wn<PRO, EPI, NW, U, TN>(st1, wt, s + SPAN, nsteps, lane, sstride);
-    issue_an<PRO, EPI, NW, U, TN>(st1, xr, s + SPAN, nsteps);
-    consume_n<PRO, EPI, NW, U, TN>(st0, acc, acc2, ssq, s, nsteps);
-    issue_wn<PRO, EPI, NW, U, TN>(st0, wt, s + 2 * SPAN, nsteps, lane, sstride);
-    issue_an<PRO, EPI, NW, U, TN>(st0, xr, s + 2 * SPAN, nsteps);
-    consume_n<PRO, EPI, NW, U, TN>(st1, acc, acc2, ssq, s + SPAN, nsteps);
+    issue_wn<PRO, EPI, NW, U, TN, MB>(st1, wt, s + SPAN, nsteps, lane, sstride);
+    issue_an<PRO, EPI, NW, U, TN, MB>(st1, xr, s + SPAN, nsteps);
+    consume_n<PRO, EPI, NW, U, TN, MB>(st0, acc, acc2, ssq, s, nsteps);
+    issue_wn<PRO, EPI, NW, U, TN, MB>(st0, wt, s + 2 * SPAN, nsteps, lane, sstride);
+    issue_an<PRO, EPI, NW, U, TN, MB>(st0, xr, s + 2 * SPAN, nsteps);
+    consume_n<PRO, EPI, NW, U, TN, MB>(st1, acc, acc2, ssq, s + SPAN, nsteps);
   }
-  if (j < nst) consume_n<PRO, EPI, NW, U, TN>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps);
+  if (j < nst) consume_n<PRO, EPI, NW, U, TN, MB>(st0, acc, acc2, ssq, w0 + SPAN * j, nsteps);
 
-  // C layout per tile: acc[t][i] = C[m = 4g + i][n = r]
+  // C layout per (tile, row block): acc[t][b][i] = C[m = 16 b + 4g + i][n = r]
 #pragma unroll
   for (int t = 0; t < TN; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      sm.red[wid][NA * t][4 * g + i][r] = acc[t][i];
-      if constexpr (EPI == EPI_SWIGLU) sm.red[wid][NA * t + NA - 1][4 * g + i][r] = acc2[t][i];
-    }
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sm.red[wid][(NA * t) * MB + b][4 * g + i][r] = acc[t][b][i];
+        if constexpr (EPI == EPI_SWIGLU) sm.red[wid][(NA * t + 1) * MB + b][4 * g + i][r] = acc2[t][b][i];
+      }
   if constexpr (PRO != PRO_PLAIN) {
-    ssq += __shfl_xor(ssq, 16, 64);
-    ssq += __shfl_xor(ssq, 32, 64);
-    if (g == 0) sm.sq[wid][r] = ssq;
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      float q = ssq[b];
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) sm.sq[wid][16 * b + r] = q;
+    }
   }
   __syncthreads();
   const int m = threadIdx.x >> 4, n = threadIdx.x & 15;
-  const bool live = threadIdx.x < 256 && m < M;
-  float ss = 0.f;
-  float vs[TN], ups[TN];
+  const bool thr = threadIdx.x < 256;
+  float ss[MB], vs[TN][MB], ups[TN][MB];
 #pragma unroll
-  for (int t = 0; t < TN; ++t) vs[t] = ups[t] = 0.f;
-  if (live) {
-    if constexpr (PRO != PRO_PLAIN) {
+  for (int b = 0; b < MB; ++b) {
+    ss[b] = 0.f;
+    const bool live = thr && 16 * b + m < M;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) ss += sm.sq[w][m];
-    }
+    for (int t = 0; t < TN; ++t) vs[t][b] = ups[t][b] = 0.f;
+    if (live) {
+      if constexpr (PRO != PRO_PLAIN) {
 #pragma unroll
-    for (int t = 0; t < TN; ++t)
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        vs[t] += sm.red[w][NA * t][m][n];
-        if constexpr (EPI == EPI_SWIGLU) ups[t] += sm.red[w][NA * t + NA - 1][m][n];
+        for (int w = 0; w < NW; ++w) ss[b] += sm.sq[w][16 * b + m];
       }
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          vs[t][b] += sm.red[w][(NA * t) * MB + b][m][n];
+          if constexpr (EPI == EPI_SWIGLU) ups[t][b] += sm.red[w][(NA * t + 1) * MB + b][m][n];
+        }
+    }
   }
   if (sx != nullptr) {   // hand-off as gemm_tile: sc1 payload -> vmcnt(0) -> barrier -> one add
-    float* mine = sx->part + (size_t)sx->idx * TN * SPLIT_STRIDE;
-    if (live) {
+    float* mine = sx->part + (size_t)sx->idx * TN * MB * SPLIT_STRIDE;
 #pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        __hip_atomic_store(mine + t * SPLIT_STRIDE + threadIdx.x, vs[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if constexpr (EPI == EPI_SWIGLU)
-          __hip_atomic_store(mine + t * SPLIT_STRIDE + 256 + threadIdx.x, ups[t], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    for (int b = 0; b < MB; ++b) {
+      if (thr && 16 * b + m < M) {
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          float* q = mine + (size_t)(t * MB + b) * SPLIT_STRIDE;
+          __hip_atomic_store(q + threadIdx.x, vs[t][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if constexpr (EPI == EPI_SWIGLU)
+            __hip_atomic_store(q + 256 + threadIdx.x, ups[t][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (n == 0)
+          __hip_atomic_store(mine + (size_t)b * SPLIT_STRIDE + 512 + m, ss[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (n == 0) __hip_atomic_store(mine + 512 + m, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -870,70 +907,78 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
     }
     __syncthreads();
     if (sm.sq[0][0] == 0.f) return;   // not last: another workgroup finishes the tiles
-    if (live) {
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      if (!(thr && 16 * b + m < M)) continue;
       float ss_sum = 0.f;
       float v_sum[TN], up_sum[TN];
 #pragma unroll
       for (int t = 0; t < TN; ++t) v_sum[t] = up_sum[t] = 0.f;
       for (int i = 0; i < sx->n; ++i) {   // fixed order: bit-identical whoever arrives last
-        const float* pi = sx->part + (size_t)i * TN * SPLIT_STRIDE;
+        const float* pi = sx->part + (size_t)i * TN * MB * SPLIT_STRIDE;
         const bool own = i == sx->idx;
 #pragma unroll
         for (int t = 0; t < TN; ++t) {
-          v_sum[t] += own ? vs[t]
-                          : __hip_atomic_load(pi + t * SPLIT_STRIDE + threadIdx.x, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
+          const float* q = pi + (size_t)(t * MB + b) * SPLIT_STRIDE;
+          v_sum[t] += own ? vs[t][b] : __hip_atomic_load(q + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if constexpr (EPI == EPI_SWIGLU)
-            up_sum[t] += own ? ups[t]
-                             : __hip_atomic_load(pi + t * SPLIT_STRIDE + 256 + threadIdx.x, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+            up_sum[t] += own ? ups[t][b]
+                             : __hip_atomic_load(q + 256 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if constexpr (PRO != PRO_PLAIN)
-          ss_sum += own ? ss : __hip_atomic_load(pi + 512 + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ss_sum += own ? ss[b]
+                        : __hip_atomic_load(pi + (size_t)b * SPLIT_STRIDE + 512 + m, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
       }
-      ss = ss_sum;
+      ss[b] = ss_sum;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        vs[t] = v_sum[t];
-        ups[t] = up_sum[t];
+        vs[t][b] = v_sum[t];
+        ups[t][b] = up_sum[t];
       }
     }
   }
-  float inv = 1.f;
-  if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss / (float)K + p.eps);
 #pragma unroll
-  for (int t = 0; t < TN; ++t) {
-    const int tile = tile0 + t;
-    float v = vs[t], up = ups[t];
-    float vpartner = 0.f;
-    if constexpr (EPI == EPI_ROPE) vpartner = __shfl_xor(v, 1, 64);   // every lane takes part
-    if (live && tile < T) {
-      v *= inv;
-      const int col = tile * 16 + n;
-      if constexpr (EPI == EPI_SWIGLU) {
-        st16<false>(p.out + (size_t)m * p.ldo + col, silu(v) * (up * inv));
-      } else if constexpr (EPI == EPI_RESID) {
-        st16<false>(p.res + (size_t)m * N + col, v + e_res[t]);
-      } else if constexpr (EPI == EPI_ROPE) {
-        const RopeEpi& re = p.re;
-        const int D = re.D, half = D >> 1;
-        const int h = col / D, pp = col - h * D;
-        const int64_t blk = e_slot / re.BS;
-        const int off = (int)(e_slot - blk * re.BS);
-        if (h < re.Hq + re.Hkv) {
-          const float partner = vpartner * inv;
-          const int i = pp >> 1, hi = pp & 1;
-          const float y = hi ? fmaf(v, e_c[t], partner * e_s[t]) : fmaf(v, e_c[t], -partner * e_s[t]);
-          const int d = i + hi * half;
-          uint16_t* dst = (h < re.Hq) ? p.out + ((size_t)m * re.Hq + h) * D + d
-                                      : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
-          st16<false>(dst, y);
+  for (int b = 0; b < MB; ++b) {
+    const int row = 16 * b + m;
+    const bool live = thr && row < M;
+    float inv = 1.f;
+    if constexpr (PRO != PRO_PLAIN) inv = rsqrtf(ss[b] / (float)K + p.eps);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const int tile = tile0 + t;
+      float v = vs[t][b];
+      const float up = ups[t][b];
+      float vpartner = 0.f;
+      if constexpr (EPI == EPI_ROPE) vpartner = __shfl_xor(v, 1, 64);   // every lane takes part
+      if (live && tile < T) {
+        v *= inv;
+        const int col = tile * 16 + n;
+        if constexpr (EPI == EPI_SWIGLU) {
+          st16<false>(p.out + (size_t)row * p.ldo + col, silu(v) * (up * inv));
+        } else if constexpr (EPI == EPI_RESID) {
+          st16<false>(p.res + (size_t)row * N + col, v + e_res[t][b]);
+        } else if constexpr (EPI == EPI_ROPE) {
+          const RopeEpi& re = p.re;
+          const int D = re.D, half = D >> 1;
+          const int h = col / D, pp = col - h * D;
+          const int64_t blk = e_slot[b] / re.BS;
+          const int off = (int)(e_slot[b] - blk * re.BS);
+          if (h < re.Hq + re.Hkv) {
+            const float partner = vpartner * inv;
+            const int i = pp >> 1, hi = pp & 1;
+            const float y = hi ? fmaf(v, e_c[t][b], partner * e_s[t][b]) : fmaf(v, e_c[t][b], -partner * e_s[t][b]);
+            const int d = i + hi * half;
+            uint16_t* dst = (h < re.Hq) ? p.out + ((size_t)row * re.Hq + h) * D + d
+                                        : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
+            st16<false>(dst, y);
+          } else {
+            const int hv = h - re.Hq - re.Hkv;
+            st16<false>(re.v_cache + (((size_t)blk * re.Hkv + hv) * D + pp) * re.BS + off, v);
+          }
         } else {
-          const int hv = h - re.Hq - re.Hkv;
-          st16<false>(re.v_cache + (((size_t)blk * re.Hkv + hv) * D + pp) * re.BS + off, v);
+          st16<false>(p.out + (size_t)row * p.ldo + col, v);
         }
-      } else {
-        st16<false>(p.out + (size_t)m * p.ldo + col, v);
       }
     }
   }

@@ -79,7 +79,7 @@ def test_skinny_gemm_balanced_split(M, N, K):
     close(ops.skinny_gemm(x, Ws2, ops.PRO_NORM, ops.EPI_SWIGLU), outs[0], 0.02, 0.02)
 
 
-@pytest.mark.parametrize("M", [5, 8, 12, 16])
+@pytest.mark.parametrize("M", [5, 8, 12, 16, 20, 32])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (128256, 4096), (6144, 4096)])
 def test_skinny_gemm_serving_batch_multi_tile(M, N, K):
     """Serving batches (M > 4): several tiles per workgroup share each activation fragment
@@ -87,7 +87,8 @@ def test_skinny_gemm_serving_batch_multi_tile(M, N, K):
     the split hand-off, qkv-sized (384 tiles) two tiles, lm_head-sized four. Against the fp32 oracle
     on the norm / residual / SwiGLU epilogues, deterministic over repeats, counters re-armed;
     the same GEMMs with the multi-tile launches off (RT_SKINNY_TN=1 is read once per process, so
-    the one-tile launch is checked through M = 3 rows of the same operands instead)."""
+    the one-tile launch is checked through M = 3 rows of the same operands instead). 17..32 rows
+    run as two 16-row blocks per MFMA pass (one weight stream for both)."""
     x = bf(M, K, seed=71)
     gam = bf(K, seed=72)
     ws = ops.split_workspace(DEV)
@@ -147,6 +148,34 @@ def test_fused_decode_matches_unfused():
     assert float(cos.min()) > 0.999
 
 
+@pytest.mark.parametrize("B", [12, 24, 32])
+def test_fused_decode_matches_unfused_serving_batch(B):
+    """Serving batches up to 32 rows take the fused decode path at tp 1 (two 16-row blocks in the
+    skinny GEMMs above 16 rows): logits agree with the unfused hipBLASLt path."""
+    from theroundtaible_amd.engine import Engine, EngineConfig
+    from theroundtaible_amd.models.llama import AttnMeta
+    e = Engine(EngineConfig(model="tiny-llama-128", weights="random-full:5", device=DEV, num_blocks=256,
+                            use_graphs=False))
+    base = e.encode_prompt("serving batch decode " * 3)
+    seqs = [e.kv.seq(f"s{i}") for i in range(B)]
+    e.prefill([(s, base[: len(base) - (i % 5)]) for i, s in enumerate(seqs)])
+    for s in seqs:
+        e.kv.ensure_capacity(s, s.length + 1)
+    pos = torch.tensor([s.length for s in seqs], device=DEV)
+    slots = torch.tensor([s.blocks[p // 32] * 32 + p % 32 for s, p in zip(seqs, pos.tolist())], device=DEV)
+    bt = torch.zeros(B, 8, dtype=torch.int32)
+    for j, s in enumerate(seqs):
+        bt[j, :len(s.blocks)] = torch.tensor(s.blocks)
+    meta = AttnMeta("decode", slots, bt.to(DEV), (pos + 1).to(torch.int32), num_splits=1)
+    tok = torch.arange(B, device=DEV) * 7 + 3
+    assert e.model.fused_decode_ok(tok)
+    fused = e.model.forward(tok, pos, e.kv, meta).float()
+    e.model.use_fused = False
+    plain = e.model.forward(tok, pos, e.kv, meta).float()
+    cos = torch.nn.functional.cosine_similarity(fused, plain, dim=-1)
+    assert float(cos.min()) > 0.999, cos
+
+
 def test_fused_decode_is_deterministic():
     from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
     sp = SamplingParams(temperature=0.0, max_new_tokens=32, ignore_eos=True, stop_on_consensus=False)
@@ -157,7 +186,8 @@ def test_fused_decode_is_deterministic():
     assert outs[0] == outs[1]
 
 
-@pytest.mark.parametrize("M,hq,hkv,d", [(1, 32, 8, 128), (3, 32, 8, 128), (16, 12, 4, 64), (5, 8, 8, 128)])
+@pytest.mark.parametrize("M,hq,hkv,d", [(1, 32, 8, 128), (3, 32, 8, 128), (16, 12, 4, 64), (5, 8, 8, 128),
+                                         (24, 32, 8, 128), (32, 12, 4, 64)])
 def test_skinny_gemm_rope_epilogue(M, hq, hkv, d):
     """qkv GEMM + RMSNorm + RoPE + paged K/V scatter in one kernel == fp32 GEMM -> K2 reference."""
     K = 512

@@ -13,6 +13,8 @@ Per layer (decode and prefill share the code; only the attention op differs):
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -75,8 +77,13 @@ class LlamaModel:
                                      meta.tile_map, split=meta.prefill_split)
 
     def fused_decode_ok(self, ids: torch.Tensor) -> bool:
+        """The fused decode path takes up to 16 rows, up to 32 at tp 1 (serving batches: the skinny
+        GEMMs' two-row-block launches, csrc/skinny_core.h gemm_tiles; the tensor-parallel epilogues
+        stay at 16)."""
         cfg = self.cfg
-        return (ids.is_cuda and 1 <= ids.shape[0] <= 16 and self.use_fused
+        rows = 32 if self.tp.size == 1 and not self.force_tp_path else 16
+        rows = min(rows, int(os.environ.get("ROUNDTABLE_FUSED_ROWS", rows)))   # A/B knob
+        return (ids.is_cuda and 1 <= ids.shape[0] <= rows and self.use_fused
                 and cfg.hidden % 32 == 0 and cfg.ffn % 32 == 0 and (cfg.n_heads * cfg.head_dim) % 32 == 0
                 and self.lm_rows % 16 == 0)
 

@@ -365,7 +365,7 @@ def skinny_gemm(x: torch.Tensor, Ws: torch.Tensor, pro: int = PRO_PLAIN, epi: in
                 res: Optional[torch.Tensor] = None, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
                 xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None,
                 split_mode: int = SPLIT_K | SPLIT_BALANCE) -> Optional[torch.Tensor]:
-    """Decode linear (M <= 16) on shuffled weights with fused RMSNorm prologue (gamma pre-folded)
+    """Decode linear (M <= 16; up to 32 with the plain / norm prologues) on shuffled weights with fused RMSNorm prologue (gamma pre-folded)
     and residual / SwiGLU epilogue. Returns the output (None for RESID, which updates ``res``).
     ``PRO_NORM_ADD``: normalizes ``bf16(x + x2)`` and writes that sum to ``xout`` (TP decode).
     ``split_ws`` (:func:`split_workspace`) enables, per ``split_mode`` bit: ``SPLIT_K`` — fewer
