@@ -39,11 +39,16 @@ static int failures = 0;
   } while (0)
 
 int main() {
-  // decode GEMM: M outside [1, 16], K not a multiple of 32, N not a multiple of 16, missing operands
+  // decode GEMM: M outside [1, 32] (17..32 only with plain / norm prologues and no all-reduce), K not a
+  // multiple of 32, N not a multiple of 16, missing operands
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 0, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
                             nullptr, nullptr, nullptr, 0, 3) == -1);
-  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 17, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 33, 16, 64, 16, 1e-5f, 0, 0, nullptr, nullptr,
                             nullptr, nullptr, nullptr, 0, 3) == -1);
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 17, 16, 64, 16, 1e-5f, 2, 0, nullptr, nullptr,
+                            nullptr, nullptr, nullptr, 0, 3) == -5);   // NORM_ADD without its operand
+  EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 17, 16, 64, 16, 1e-5f, 2, 0, nullptr, (const void*)1,
+                            nullptr, nullptr, nullptr, 0, 3) == -1);   // NORM_ADD above 16 rows
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 16, 48, 16, 1e-5f, 0, 0, nullptr, nullptr,
                             nullptr, nullptr, nullptr, 0, 3) == -1);
   EXPECT(launch_skinny_gemm(nullptr, nullptr, nullptr, nullptr, 3, 24, 64, 24, 1e-5f, 0, 0, nullptr, nullptr,
