@@ -149,10 +149,14 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: Optional[int] = None, ma
     # A lone sequence (B = 1: sequential rounds) shares nothing, so it takes the whole chip: B = 1,
     # Llama-3-8B, 10K / 25K / 40K keys: 24 splits 15.9 / 26.3 / 36.8 us, 32 splits 15.0 / 25.9 /
     # 35.7 (profiles/r03/attn_b1_splits.md)
+    # Larger tables take the whole chip again: B = 8 / 16 knights, 11K shared keys: 3 -> 4 splits
+    # 23.9 -> 21.4 us, 1 -> 2 splits 47.5 -> 29.9 us (the 3/4 rule left B = 16 at 128 workgroups;
+    # profiles/r05/attn_splits_large_tables.md)
     num_cus = device_cus() if num_cus is None else num_cus
     # ROUNDTABLE_GROUPED_CU_FRACTION: A/B knob for the grouped share of the CUs (default 3/4)
     frac = float(os.environ.get("ROUNDTABLE_GROUPED_CU_FRACTION", "0.75"))
-    cus = int(num_cus * frac) if grouped and batch > 1 else num_cus
+    full_from = int(os.environ.get("ROUNDTABLE_GROUPED_FULL_FROM", "5"))   # A/B knob
+    cus = int(num_cus * frac) if grouped and 1 < batch < full_from else num_cus
     want = cus // max(1, batch * n_kv_heads)        # never more workgroups than CUs: a second
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
