@@ -258,6 +258,44 @@ def test_skinny_gemm_rope_balanced_split(M, hq, hkv, K):
         close(a, b, 0.02, 0.02)
 
 
+@pytest.mark.parametrize("M", [12, 24, 32])
+@pytest.mark.parametrize("hq,hkv,K", [(16, 4, 4096), (32, 8, 4096), (4, 1, 4096)])
+def test_skinny_gemm_rope_serving_batches(M, hq, hkv, K):
+    """qkv (+RMSNorm, RoPE, paged K/V write) at serving batch sizes: (16, 4) = 192 tiles takes the
+    two-tile / two-K-half split launch (hand-off before the rotate-half partner read), (32, 8) =
+    384 tiles two tiles per workgroup, (4, 1) = 48 tiles one tile; above 16 rows every one of them
+    runs two row blocks. q / K / V cache equal the fp32 reference, repeats agree bit for bit, the
+    split counters re-arm."""
+    d = 128
+    N = (hq + 2 * hkv) * d
+    x = bf(M, K, seed=91)
+    W = bf(N, K, scale=0.05, seed=92)
+    gam = bf(K, seed=93)
+    cos_sin = ref.rope_cos_sin(4096, d, 500000.0, DEV)
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int64)
+    nb = 4
+    slots = torch.randperm(nb * 32, device=DEV)[:M].to(torch.int64)
+    Ws = ops.shuffle_weight(W, gam, rope_heads=hq + hkv, head_dim=d)
+    ws = ops.split_workspace(DEV)
+    runs = []
+    for _ in range(2):
+        kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+        vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+        q = ops.skinny_gemm_rope(x, Ws, ops.PRO_NORM, positions, cos_sin, kc, vc, slots, hq, hkv, d, 1e-5, split_ws=ws)
+        runs.append((q, kc, vc))
+    assert int(ws[:256].abs().sum()) == 0, "split counters must re-arm to zero"
+    kc_r = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16)
+    vc_r = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16)
+    Wp = ref.fold_gamma(W.cpu(), gam.cpu(), hq + hkv, d)
+    q_r = ref.skinny_gemm_rope(x.cpu(), Wp, 1, positions.cpu(), cos_sin.cpu(), kc_r, vc_r, slots.cpu(), hq, hkv, d,
+                               1e-5)
+    for q, kc, vc in runs:
+        close(q, q_r.to(DEV), 0.05, 0.02)
+        close(kc, kc_r.to(DEV), 0.05, 0.02)
+        close(vc, vc_r.to(DEV), 0.05, 0.02)
+    assert all(torch.equal(a, b) for a, b in zip(runs[0], runs[1]))
+
+
 def test_norm_add_prologue():
     """TP decode prologue: normalize bf16(x + x2), workgroup 0 publishes the sum."""
     M, N, K = 3, 512, 4096
