@@ -56,8 +56,8 @@ def test_decode_splits_bounds():
     assert ops.decode_splits(64, 8) == 1
     assert ops.decode_splits(3, 8) == 10
     assert ops.decode_splits(1, 1) == 64
-    # shared-prefix groups: 3/4 of the CUs for the 3-knight table, the whole chip from 5 rows on
-    assert ops.decode_splits(3, 8, num_cus=256, grouped=True) == 8
+    # shared-prefix groups: the whole chip, the 3-knight table included
+    assert ops.decode_splits(3, 8, num_cus=256, grouped=True) == 10
     assert ops.decode_splits(8, 8, num_cus=256, grouped=True) == 4
     assert ops.decode_splits(16, 8, num_cus=256, grouped=True) == 2
 

@@ -143,20 +143,19 @@ def decode_splits(batch: int, n_kv_heads: int, num_cus: Optional[int] = None, ma
     The kernel derives each split's key range from the *runtime* context length, so one
     captured hipGraph serves every length (splits past the end are empty and skipped by the
     combine) — no re-capture as a knight's discussion grows."""
-    # grouped (shared-prefix) decode: a workgroup streams 1/n of the group's shared keys, so the
-    # launch is shorter and its fixed latency chain weighs more — 3/4 of the CUs measured best
-    # (B=3, shared 22K/40K: 8 splits 30.8/42.7 us vs 10 splits 31.7/43.8, r2_gattn_v1.log)
+    # grouped (shared-prefix) decode takes the whole chip too. Round 2 measured 3/4 of the CUs best
+    # for the 3-knight table (B=3, shared 22K/40K: 8 splits 30.8/42.7 us vs 10 splits 31.7/43.8,
+    # r2_gattn_v1.log); with the round-5 copy-free K/V loop the whole chip wins (8 -> 10 splits:
+    # 29.0 -> 28.2 / 42.4 -> 40.9 us; driver-config bench 837.1 -> 840.1 tok/s, mean of three
+    # same-box passes), and for larger tables by far (16 knights: 1 -> 2 splits 47.5 -> 29.9 us;
+    # profiles/r05/attn_splits_large_tables.md).
     # A lone sequence (B = 1: sequential rounds) shares nothing, so it takes the whole chip: B = 1,
     # Llama-3-8B, 10K / 25K / 40K keys: 24 splits 15.9 / 26.3 / 36.8 us, 32 splits 15.0 / 25.9 /
     # 35.7 (profiles/r03/attn_b1_splits.md)
-    # Larger tables take the whole chip again: B = 8 / 16 knights, 11K shared keys: 3 -> 4 splits
-    # 23.9 -> 21.4 us, 1 -> 2 splits 47.5 -> 29.9 us (the 3/4 rule left B = 16 at 128 workgroups;
-    # profiles/r05/attn_splits_large_tables.md)
     num_cus = device_cus() if num_cus is None else num_cus
-    # ROUNDTABLE_GROUPED_CU_FRACTION: A/B knob for the grouped share of the CUs (default 3/4)
-    frac = float(os.environ.get("ROUNDTABLE_GROUPED_CU_FRACTION", "0.75"))
-    full_from = int(os.environ.get("ROUNDTABLE_GROUPED_FULL_FROM", "5"))   # A/B knob
-    cus = int(num_cus * frac) if grouped and 1 < batch < full_from else num_cus
+    # ROUNDTABLE_GROUPED_CU_FRACTION: A/B knob for the grouped share of the CUs (default: all)
+    frac = float(os.environ.get("ROUNDTABLE_GROUPED_CU_FRACTION", "1.0"))
+    cus = int(num_cus * frac) if grouped and batch > 1 else num_cus
     want = cus // max(1, batch * n_kv_heads)        # never more workgroups than CUs: a second
     return int(max(1, min(max_splits, want)))       # wave of workgroups doubles the tail
 
