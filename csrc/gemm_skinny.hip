@@ -1,4 +1,4 @@
-// Decode-path linear layers (M <= 16 rows): y[M,N] = x[M,K] . W[N,K]^T on MFMA, with the
+// Decode-path linear layers (M <= 16 rows, up to 32 with plain / norm prologues): y[M,N] = x[M,K] . W[N,K]^T on MFMA, with the
 // layer's elementwise work fused in, so a decode layer needs no separate norm/act kernels.
 // The tile code (weight layout, pipeline, prologues, epilogues) lives in skinny_core.h and is
 // shared with the persistent decode-layer kernel; this file holds the one-tile-per-workgroup

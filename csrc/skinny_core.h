@@ -1,4 +1,4 @@
-// Device core of the decode-path GEMMs (M <= 16 rows): shared by the standalone launches in
+// Device core of the decode-path GEMMs (M <= 16 rows; 17..32 through gemm_tiles): shared by the standalone launches in
 // gemm_skinny.hip and the persistent decode-layer kernel in decode_layer.hip.
 //
 // Weight layout ("fragment-shuffled", built once at load time by `shuffle_weight`):
