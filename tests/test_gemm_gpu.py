@@ -115,6 +115,27 @@ def test_skinny_gemm_serving_batch_multi_tile(M, N, K):
     assert int(ws[:256].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("M", [12, 20])
+@pytest.mark.parametrize("N", [4112, 6160, 12304])
+def test_skinny_gemm_serving_batch_odd_tile_counts(M, N):
+    """Tile counts that do not divide by the tiles per workgroup: 257 tiles on the two-K-half path
+    (a last group with one real tile), 385 on two tiles, 769 on four — the past-the-end tile of a
+    workgroup is computed on a clamped copy and never stored (skinny_core.h gemm_tiles)."""
+    K = 4096
+    x = bf(M, K, seed=81)
+    W = bf(N, K, scale=0.05, seed=82)
+    ws = ops.split_workspace(DEV)
+    Ws = ops.shuffle_weight(W)
+    res = bf(M, N, seed=83)
+    res_ref = res.cpu().clone()
+    ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=ws)
+    ref.skinny_gemm(x.cpu(), W.cpu(), 0, 1, res=res_ref)
+    close(res, res_ref.to(DEV), 0.06, 0.02)
+    got = ops.skinny_gemm(x, Ws, ops.PRO_PLAIN, split_ws=ws)
+    close(got, ref.skinny_gemm(x.cpu(), W.cpu(), 0).to(DEV), 0.05, 0.02)
+    assert int(ws[:256].abs().sum()) == 0
+
+
 def test_shuffle_layout():
     N, K = 32, 64
     W = torch.arange(N * K, device=DEV).reshape(N, K).to(torch.float32).to(torch.bfloat16)
