@@ -202,6 +202,13 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   const bool hk_split_ok = Hkv % 8 == 0 || 8 % Hkv == 0;
   args.xcd = (xcd_env && (B * Hkv * num_splits) % 8 == 0 && (B * Hq * (D / 32)) % 8 == 0 && hk_split_ok) ? 1 : 0;
   args.plain_partials = (plain_env && args.ext_combine && !defer_combine) ? 1 : 0;
+  // K row read order (attn_core.h AttnArgs::kperm): each K load instruction reads 64 contiguous
+  // bytes per row (16 rows x 64 B) instead of 4 x 16 B at a 64-B stride (32 half-used cache lines):
+  // half the L1 line requests per K tile. Llama-3-8B tp 1, B = 3 grouped, 22K / 40K shared keys
+  // 29.5 -> 28.1 / 43.5 -> 41.6 us, private rows -9 %, B = 1 25K 28.0 -> 26.6, tp 8 shard even
+  // (profiles/r05/attn_kperm_ab.md). RT_ATTN_KPERM=0 restores the old order (A/B)
+  static const int kperm_env = getenv("RT_ATTN_KPERM") ? atoi(getenv("RT_ATTN_KPERM")) : 1;
+  args.kperm = kperm_env ? 1 : 0;
   const int G = Hq / Hkv;
   // a group's n*G columns need the 16-column LDS merge buffers
   // K/V loop form (attn_core.h PP): the copy-free ping-pong wins where a workgroup streams many

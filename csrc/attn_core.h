@@ -44,14 +44,15 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 template <int D>
 struct Tile {
-  short8 k[2][D / 32];  // [half][chunk]: K row key(h, r), d = (D/4)*g + 8c + j
+  short8 k[2][D / 32];  // [half][chunk]: K row key(h, r), d = kg + kc*c + j (kperm: kg = 8g, kc = 32;
+                        // else kg = (D/4)g, kc = 8 — the same permutation of d for Q and K)
   short8 v[D / 16];     // [d-chunk]: V[keys 8g..8g+7][d = 16e + r]
 };
 
 // SC1: the block may hold K/V written earlier in the same launch (persistent kernel): sc1 loads.
 template <int D, bool SC1>
 RT_DEVICE void load_tile(Tile<D>& t, const uint16_t* __restrict__ kblk, const uint16_t* __restrict__ vblk, int r,
-                         int g) {
+                         int g, int kg, int kc) {
   const int krow = 8 * (r >> 2) + (r & 3);
   if constexpr (SC1) {
     const auto kr_ = rt::buf_rsrc(kblk), vr_ = rt::buf_rsrc(vblk);
@@ -59,16 +60,16 @@ RT_DEVICE void load_tile(Tile<D>& t, const uint16_t* __restrict__ kblk, const ui
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int c = 0; c < D / 32; ++c)
-        t.k[h][c] = __builtin_bit_cast(short8, rt::sc1_load4(kr_, 2 * ((krow + 4 * h) * D + (D / 4) * g + 8 * c)));
+        t.k[h][c] = __builtin_bit_cast(short8, rt::sc1_load4(kr_, 2 * ((krow + 4 * h) * D + kg + kc * c)));
 #pragma unroll
     for (int e = 0; e < D / 16; ++e)
       t.v[e] = __builtin_bit_cast(short8, rt::sc1_load4(vr_, 2 * ((16 * e + r) * BS + 8 * g)));
   } else {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint16_t* kr = kblk + (krow + 4 * h) * D + (D / 4) * g;
+      const uint16_t* kr = kblk + (krow + 4 * h) * D + kg;
 #pragma unroll
-      for (int c = 0; c < D / 32; ++c) t.k[h][c] = *reinterpret_cast<const short8*>(kr + 8 * c);
+      for (int c = 0; c < D / 32; ++c) t.k[h][c] = *reinterpret_cast<const short8*>(kr + kc * c);
     }
 #pragma unroll
     for (int e = 0; e < D / 16; ++e) t.v[e] = *reinterpret_cast<const short8*>(vblk + (16 * e + r) * BS + 8 * g);
@@ -96,6 +97,8 @@ struct AttnArgs {
   int ext_combine = 0;         // 1: leave every partial for decode_combine_kernel (no in-launch combine)
   int xcd = 0;                 // 1: XCD-aware item order (attention_decode.hip), the launch's grid % 8 == 0
   int plain_partials = 0;      // 1 (ext_combine only): partials stay in the writer's L2 (plain stores)
+  int kperm = 0;               // 1: lane group g reads d = 32c + 8g.. (64 contiguous bytes of a K row per
+                               // load instruction instead of 4 x 16 B at a 64-B stride; Q the same way)
 };
 
 // GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
@@ -163,6 +166,8 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int rseq = r / G, rhead = r - (r / G) * G;  // column r -> (member, head within the kv group)
+  // reduction-dim order of the QK^T MFMAs (any permutation of d, the same for Q and K)
+  const int kg = P.kperm ? 8 * g : (D / 4) * g, kc = P.kperm ? 32 : 8;
 
   if (P.probe == 1) {          // launch + metadata round trip only
     if (ctx == -12345) out[0] = 0;
@@ -181,14 +186,14 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
   short8 qf[D / 32];
   {
     const bool live = r < ncol;
-    const uint16_t* qr = q + ((size_t)(b0 + (live ? rseq : 0)) * Hq + hk * G + (live ? rhead : 0)) * D + (D / 4) * g;
+    const uint16_t* qr = q + ((size_t)(b0 + (live ? rseq : 0)) * Hq + hk * G + (live ? rhead : 0)) * D + kg;
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) {
       short8 v;
       if constexpr (SC1)   // uniform base + per-lane offset (a per-lane resource would waterfall)
-        v = __builtin_bit_cast(short8, rt::sc1_load4(rt::buf_rsrc(q), (int)((qr - q) + 8 * c) * 2));
+        v = __builtin_bit_cast(short8, rt::sc1_load4(rt::buf_rsrc(q), (int)((qr - q) + kc * c) * 2));
       else
-        v = *reinterpret_cast<const short8*>(qr + 8 * c);
+        v = *reinterpret_cast<const short8*>(qr + kc * c);
       if (!live) v = short8{0, 0, 0, 0, 0, 0, 0, 0};
       qf[c] = v;
     }
@@ -218,7 +223,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       blk_lane = tt < nv ? bt_entry(tt) : 0;
     }
     const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, j & 63) * blk_stride + (size_t)hk * BS * D;
-    load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g);
+    load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g, kg, kc);
   };
   // one 32-key tile: S^T = K Q^T, online softmax down each column, O += P V
   auto step = [&](const Tile<D>& cur, int v) {
@@ -296,7 +301,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
         blk_lane = tt < nv ? bt_entry(tt) : 0;
       }
       const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, jj & 63) * blk_stride + (size_t)hk * BS * D;
-      load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g);
+      load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g, kg, kc);
     };
     Tile<D> ta, tb;
     if (v < nv) {
