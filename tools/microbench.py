@@ -239,20 +239,21 @@ def bench_sample(B):
         B * V * 2)
 
 
-def bench_prefill(T):
+def bench_prefill(T, prefix=0):
+    """Causal prefill of T new tokens after ``prefix`` cached ones (one sequence, Llama-3-8B heads)."""
     hq, hkv, d = 32, 8, 128
-    nblk = (T + 31) // 32
+    nblk = (prefix + T + 31) // 32
     kc = bf(nblk, hkv, 32, d)
     vc = bf(nblk, hkv, d, 32)
     q = bf(T, hq, d)
     bt = torch.arange(nblk, device=DEV, dtype=torch.int32)[None]
     cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
-    sp = torch.zeros(1, device=DEV, dtype=torch.int32)
+    sp = torch.full((1,), prefix, device=DEV, dtype=torch.int32)
     rows = ops.native().prefill_rows_per_tile(hq // hkv, d)
     tm = ops.prefill_tile_map(cu.cpu(), rows, sp.cpu()).to(DEV)
-    flops = 4 * hq * d * T * T / 2
+    flops = 4 * hq * d * T * (prefix + T / 2)
     us = timed(lambda i: ops.prefill_attention(q, kc, vc, bt, cu, sp, 1 / math.sqrt(d), tm), iters=5, reps=3)
-    row(f"prefill attn causal T={T}", us, None, flops)
+    row(f"prefill attn causal T={T} prefix={prefix}", us, None, flops)
 
 
 def main():
@@ -264,6 +265,7 @@ def main():
     ap.add_argument("--shared", default="22000:1500", help="grouped attention: shared:private tokens list, comma-sep")
     ap.add_argument("--tp", default="2,4,8", help="gemm_tp: tensor-parallel degrees of the shard shapes")
     ap.add_argument("--model", default="llama3-8b", help="gemm_tp: model preset")
+    ap.add_argument("--prefill", default="4096:0", help="prefill: new:prefix token counts, comma-sep")
     a = ap.parse_args()
     only = set(a.only.split(","))
     torch.manual_seed(0)
@@ -283,7 +285,9 @@ def main():
     if "sample" in only:
         bench_sample(a.batch)
     if "prefill" in only:
-        bench_prefill(4096)
+        for pf in a.prefill.split(","):
+            t, pre = (int(x) for x in pf.split(":"))
+            bench_prefill(t, pre)
     print("\n| op | us | TB/s | TF/s |\n|---|---|---|---|")
     for r in ROWS:
         print("| " + " | ".join(r) + " |")
