@@ -100,6 +100,8 @@ def validate_config(cfg: Dict[str, Any]) -> None:
         raise ConfigError("rules.round_mode must be 'sequential' or 'parallel'.")
     if rules.get("prompt_layout", "reference") not in ("reference", "append", "shared"):
         raise ConfigError("rules.prompt_layout must be 'reference', 'append' or 'shared'.")
+    if rules.get("placeholder_semantics", "literal") not in ("literal", "reference"):
+        raise ConfigError("rules.placeholder_semantics must be 'literal' or 'reference'.")
     if not cfg.get("adapter_config") and cfg.get("adapter_config") != {}:
         raise ConfigError("config.json missing 'adapter_config' section.")
     if cfg.get("adapter_config") is None:

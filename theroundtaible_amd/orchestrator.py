@@ -165,13 +165,15 @@ class Orchestrator:
     # ---- prompt --------------------------------------------------------------------------
     def _prompt(self, knight: KnightConfig, ctx: TurnContext, visible: Sequence[RoundEntry], rnd: int,
                 king_demand: bool, resolved_files: str, resolved_commands: str) -> Prompt:
+        sem = self.config.rules.placeholder_semantics
         if self.layout == "append":
-            return build_turn_prompt_append(knight, self.config.knights, ctx, self.transcript, rnd)
+            return build_turn_prompt_append(knight, self.config.knights, ctx, self.transcript, rnd, semantics=sem)
         if self.layout == "shared":
             return build_turn_prompt_shared(knight, self.config.knights, ctx, self.transcript, rnd,
-                                            shared_key=self.table_id + "@table")
+                                            shared_key=self.table_id + "@table", semantics=sem)
         return build_turn_prompt_reference(knight, self.config.knights, ctx, visible, king_demand=king_demand,
-                                           resolved_files=resolved_files, resolved_commands=resolved_commands)
+                                           resolved_files=resolved_files, resolved_commands=resolved_commands,
+                                           semantics=sem)
 
     def _append_transcript(self, entry: RoundEntry, res: Optional[TurnResult]) -> None:
         if self.layout not in ("append", "shared"):
@@ -351,7 +353,8 @@ class Orchestrator:
             if n == 0:
                 return None
             return build_turn_prompt_shared(order[0], self.config.knights, self.ctx, segs, rnd + 1,
-                                            shared_key=self.table_id + "@table")
+                                            shared_key=self.table_id + "@table",
+                                            semantics=self.config.rules.placeholder_semantics)
         return predict
 
     def record_parallel(self, rnd: int, order: Sequence[KnightConfig],

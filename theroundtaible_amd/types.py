@@ -76,13 +76,17 @@ class RulesConfig:
     ignore: List[str] = field(default_factory=lambda: [".git", "node_modules", "dist", "build", ".next"])
     # MI355X extensions. Reference semantics are the defaults.
     round_mode: str = "sequential"        # "sequential" (reference) | "parallel"
-    prompt_layout: str = "reference"      # "reference" (byte-exact) | "append" (KV-friendly)
+    prompt_layout: str = "reference"      # "reference" (reference shape) | "append" | "shared" (KV-friendly)
+    # "literal" (every occurrence, verbatim) | "reference" (JS String.replace: first occurrence,
+    # $-patterns expanded; prompt.py)
+    placeholder_semantics: str = "literal"
 
     @classmethod
     def from_dict(cls, d: Dict[str, Any]) -> "RulesConfig":
         r = cls()
         for k in ("max_rounds", "consensus_threshold", "timeout_per_turn_seconds",
-                  "escalate_to_user_after", "auto_execute", "round_mode", "prompt_layout"):
+                  "escalate_to_user_after", "auto_execute", "round_mode", "prompt_layout",
+                  "placeholder_semantics"):
             if k in d and d[k] is not None:
                 setattr(r, k, d[k])
         if isinstance(d.get("ignore"), list):
