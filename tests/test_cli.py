@@ -144,3 +144,20 @@ def test_scripted_unanimous_rejection(project):
     st = json.load(open(_session(project) / "status.json"))
     assert st["consensus_reached"] is True and st["round"] == 1
     assert "Unanimous rejection in 1 round(s)" in open(project / ".roundtable" / "chronicle.md").read()
+
+
+def test_resume_missing_session_is_session_error(project):
+    """--resume <typo> must raise SessionError (exit 3) before reading any rounds file."""
+    _init(project, "tiny-llama", knights=1, max_new=4)
+    from theroundtaible_amd.errors import ExitCode
+    rc = main(["--quiet", "discuss", "x", "--no-read-codebase", "--choice", "0", "--device", "cpu",
+               "--resume", "no-such-session"])
+    assert rc == ExitCode.SESSION_ERROR == 3
+
+
+@pytest.mark.parametrize("raw,want", [("2", 2), ("2 ", 2), (" 2", 2), ("2abc", 2), ("+3", 3), ("-1", -1),
+                                      ("0x2", 2), ("abc", None), ("", None), (" ", None), ("0xg", None),
+                                      ("1.9", 1), ("07", 7)])
+def test_king_choice_parses_like_js_parseint(raw, want):
+    from theroundtaible_amd.cli import js_parse_int
+    assert js_parse_int(raw) == want

@@ -315,6 +315,22 @@ def _make_backends(config, ui: UI, device: Optional[str] = None):
     return initialize_backends(config, ui, factory), factory
 
 
+def js_parse_int(text: str) -> Optional[int]:
+    """JavaScript ``parseInt(text)`` (no radix, discuss.ts:181): leading whitespace and a sign,
+    a ``0x`` prefix means hex, then the longest digit run — ``"2 "`` and ``"2abc"`` are 2;
+    ``None`` where JS gives NaN."""
+    import re
+    t = (text or "").lstrip()
+    if re.match(r"[+-]?0[xX]", t) and not re.match(r"[+-]?0[xX][0-9a-fA-F]", t):
+        return None                       # "0x" with no hex digit: NaN
+    m = re.match(r"([+-]?)(0[xX][0-9a-fA-F]+|\d+)", t)
+    if m is None:
+        return None
+    body = m.group(2)
+    v = int(body[2:], 16) if body[:2] in ("0x", "0X") else int(body)
+    return -v if m.group(1) == "-" else v
+
+
 def last_proposals(all_rounds):
     """(discuss.ts:229-260) last entry per knight with a one-line summary."""
     import re
@@ -405,9 +421,9 @@ def _resume_state(root: str, session: str) -> ContinueOptions:
         if info is None:
             raise SessionError("No session to resume.")
         path = info.path
-    entries = store.load_round_entries(path)
     if not os.path.isdir(path):
         raise SessionError(f"Session not found: {session}")
+    entries = store.load_round_entries(path)
     last = max((e.round for e in entries), default=0)
     return ContinueOptions(path, entries, last + 1)
 
@@ -440,11 +456,8 @@ def _no_consensus(root, topic, result, args, ui: UI) -> str:
         ui.print(f"  {i}. {p['knight']} ({p['score']}/10) — {p['summary']}")
     ui.print(f"  {len(props) + 1}. Send them back — they must reach unanimity!")
     raw = str(args.choice) if args.choice is not None else ask(ui, f"  What say you, Your Majesty? [1-{len(props) + 1}]", "")
-    try:
-        choice = int(raw)
-    except ValueError:
-        choice = -1
-    if choice < 1 or choice > len(props) + 1:
+    choice = js_parse_int(raw)
+    if choice is None or choice < 1 or choice > len(props) + 1:
         ui.dim("  The King waves dismissively. Perhaps another time.")
         return "done"
     if choice == len(props) + 1:
