@@ -295,3 +295,29 @@ def test_discuss_tp2_knight_skipped_when_a_rank_stalls(tmp_path):
     # timestamped stage transitions name where each rank is
     assert "stage 'turn 1'" in r.stderr and "stage 'turn 2'" in r.stderr
     assert took < 200, took
+
+
+def test_discuss_tp2_waits_for_a_slow_loading_rank(tmp_path):
+    """ranks load their engines one after another, and a real checkpoint can
+    take minutes longer on one rank than on its peers. Those peers must wait for it under the LOAD
+    limit (the load-timeout gloo groups of parallel/cluster.py: the TP group meets there after
+    loading its weights, and every rank meets there after building all its engines), not inside a
+    short-timeout collective. Here the containment timeout of every collective is 10 s and rank 0
+    enters each load stage 15 s late: its second engine (Klein, tp 1) loads after Groot's TP group
+    set-up, while rank 1 has nothing left to load. The run still completes, both knights speak
+    (before the load groups, rank 1 died in its first control collective after 10 s)."""
+    from test_distributed_cpu import _tp_project
+    _tp_project(tmp_path, {"Groot": {"tp": 2}, "Klein": {}})
+    cfg_path = tmp_path / ".roundtable" / "config.json"
+    cfg = json.loads(cfg_path.read_text())
+    cfg["rules"].update(max_rounds=1, timeout_per_turn_seconds=60)
+    cfg_path.write_text(json.dumps(cfg))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               ROUNDTABLE_BENCH_FAULT="0:engine_load:sleep15", ROUNDTABLE_COLLECTIVE_TIMEOUT_S="10")
+    r = subprocess.run([sys.executable, "-m", "theroundtaible_amd", "discuss", "Laad traag", "--no-read-codebase",
+                        "--choice", "4"], capture_output=True, text=True, timeout=400, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    sessions = os.listdir(tmp_path / ".roundtable" / "sessions")
+    disc = (tmp_path / ".roundtable" / "sessions" / sessions[0] / "discussion.md").read_text()
+    assert "Round 1 — Groot" in disc and "Round 1 — Klein" in disc, disc[:2000]

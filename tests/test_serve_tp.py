@@ -62,7 +62,8 @@ def test_serve_tp2_matches_tp1():
     finally:
         ref.close()
     port = free_port()
-    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    # idle keepalive every 1 s: the follower takes rank 0's pings between requests
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT, ROUNDTABLE_SERVE_PING_S="1")
     p = subprocess.Popen([sys.executable, "-m", "theroundtaible_amd", "serve", "--model", "tiny-llama",
                           "--weights", "random-full:1", "--device", "cpu", "--tp", "2", "--port", str(port),
                           "--max-batch", "4", "--max-tokens", "8", "--num-blocks", "256"],
@@ -84,6 +85,7 @@ def test_serve_tp2_matches_tp1():
             time.sleep(1)
         assert health["tp"] == 2 and health["status"] == "ok", health
         assert _ask(url, prompts[:1]) == want_single
+        time.sleep(4)                      # idle: several keepalive pings go to the follower
         assert _ask(url, prompts) == want_batch
         metrics = urllib.request.urlopen(url + "/metrics", timeout=10).read().decode()
         assert "roundtable_requests_total 4" in metrics

@@ -131,6 +131,11 @@ class Engine:
                 del weights
                 self.model.decode_weights(drop_originals=(mode == "shuffled"))
                 self.weight_residency = mode
+        if self.tp.size > 1 and self.tp.load_group is not None:
+            # every rank of the group has its weights before the group's first collective
+            import torch.distributed as dist
+            with failsafe.stage("engine_load"):
+                dist.barrier(group=self.tp.load_group)
         if self.on_gpu and self.tp.size > 1:
             with failsafe.stage("k9_create"):
                 self.tp.setup_oneshot()      # K9: collective over the TP group; RCCL stays the fallback

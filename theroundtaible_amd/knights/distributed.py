@@ -100,6 +100,15 @@ class DistributedPool:
         if len(self.events) > 4096:
             del self.events[:1024], self.event_ns[:1024]
 
+    def _store(self):
+        """The launcher's key-value store, fetched once per pool: torch exposes the default
+        group's store only through ``_get_default_store`` (stable since torch 1.x); the pool
+        keeps the handle instead of asking every turn."""
+        if getattr(self, "_kv_store", None) is None:
+            import torch.distributed as dist
+            self._kv_store = dist.distributed_c10d._get_default_store()
+        return self._kv_store
+
     def _rendezvous(self, ranks: tuple, wait_s: float) -> bool:
         """Turn-start agreement of one tensor-parallel group, outside its process groups (the
         launcher's TCP key-value store): each rank counts itself in, and the FIRST rank to see
@@ -110,8 +119,7 @@ class DistributedPool:
         the turn's first collective for the process-group timeout, and a late rank never enters
         collectives its peers have abandoned (reference: a failed turn is skipped and the round
         continues, /root/reference/src/orchestrator.ts:521-535)."""
-        import torch.distributed as dist
-        store = dist.distributed_c10d._get_default_store()
+        store = self._store()
         n = self._rv_count[ranks] = self._rv_count.get(ranks, 0) + 1
         key = f"rt/turn/{'-'.join(map(str, ranks))}/{n}"
         store.add(key + "/n", 1)
@@ -127,6 +135,12 @@ class DistributedPool:
                 dec = store.compare_set(key + "/d", "", "skip")
                 break
             time.sleep(0.002)
+        # the last of the group's ranks to read the decision removes the turn's keys: the store
+        # holds O(groups) keys for the whole session, not O(turns). A rank that never
+        # reaches this turn leaves them; the decision itself is already fixed either way.
+        if store.add(key + "/r", 1) >= len(ranks):
+            for k in (key + "/n", key + "/d", key + "/r"):
+                store.delete_key(k)
         return dec == b"go"
 
     def execute_round(self, pairs: Sequence[Tuple["RemoteKnight", TurnRequest]],

@@ -18,13 +18,14 @@ discuss "..."``, every rank runs the same CLI/orchestrator program (SPMD,
 """
 from __future__ import annotations
 
+import datetime
 import threading
 from typing import Dict, List, Tuple
 
 from ..config import engine_settings
 from ..engine.engine import Engine, EngineConfig
 from ..engine.sampler import SamplingParams
-from ..parallel.cluster import Cluster
+from ..parallel.cluster import Cluster, load_group_for
 from ..parallel.tp import TPInfo
 from ..types import RoundtableConfig
 from ..utils.local_detect import resolve_model
@@ -66,10 +67,15 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
     import torch.distributed as dist
     placement = plan_placement(config, cluster.world)
     groups: Dict[Tuple[int, ...], object] = {}
+    load_groups: Dict[Tuple[int, ...], object] = {}
     for ranks in placement.values():           # identical order on every rank (collective)
         key = tuple(ranks)
         if len(key) > 1 and key not in groups:
-            groups[key] = dist.new_group(list(key)) if cluster.distributed else None
+            # the containment timeout (torch's new_group default would be 30 min); safe for the
+            # group's first collective because Engine meets on the load group before it
+            groups[key] = dist.new_group(list(key), timeout=datetime.timedelta(seconds=cluster.timeout_s)) \
+                if cluster.distributed else None
+            load_groups[key] = load_group_for(key) if cluster.distributed else None
     engines: Dict[tuple, Tuple[Engine, threading.Lock]] = {}
     local: Dict[str, EngineBackend] = {}
     tokenizer = None
@@ -79,7 +85,8 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         if cluster.rank not in ranks or aid in local:
             continue
         st = engine_settings(config, aid)
-        tp = TPInfo(size=len(ranks), rank=ranks.index(cluster.rank), group=groups.get(tuple(ranks)))
+        tp = TPInfo(size=len(ranks), rank=ranks.index(cluster.rank), group=groups.get(tuple(ranks)),
+                    load_group=load_groups.get(tuple(ranks)))
         ekey = (st["model"], str(st.get("weights", "random:0")), str(st.get("dtype", "bf16")), tuple(ranks))
         if ekey not in engines:
             model, overrides = resolve_model(st["model"], str(st.get("weights", "random:0")), st.get("model_overrides"))
@@ -105,6 +112,11 @@ def build_spmd_backends(config: RoundtableConfig, cluster: Cluster, ui: UI = NUL
         local[aid] = EngineBackend(display_name(aid, config), aid, engine, params, lock,
                                    script=ConsensusScript.from_config(st.get("scripted_consensus")))
         ui.ok(f"  ✓ {k.name}: {st['model']} on rank(s) {ranks}" + (f" (tp={len(ranks)})" if len(ranks) > 1 else ""))
+    # no rank enters a turn-time (short-timeout) collective before every rank has loaded its
+    # engines: ranks load one engine after another, a real checkpoint can take minutes longer on
+    # one of them; the wait runs under the load limit
+    with failsafe.stage("engine_load"):
+        cluster.load_rendezvous()
     if tokenizer is None:   # a rank hosting no knight still decodes exchanged ids
         from ..engine.tokenizer import get_tokenizer
         from ..models.config import get_config

@@ -29,6 +29,16 @@ class Cluster:
     # answer, a server's next request): the data and control collectives keep the short,
     # containment-sized timeout of init_cluster
     wait_group: Optional[object] = None
+    # gloo group whose timeout covers engine loading (LOAD_TIMEOUT_S): the load rendezvous
+    # (load_rendezvous) runs on it, so a rank that loads a checkpoint minutes longer than its
+    # peers is waited for there, not in a short-timeout collective
+    load_group: Optional[object] = None
+    timeout_s: int = 1800        # containment timeout of the world / control (and TP) groups
+
+    def load_rendezvous(self) -> None:
+        """Every rank has finished loading its engines (no-op for one rank)."""
+        if self.distributed and self.load_group is not None:
+            dist.barrier(group=self.load_group)
 
     @property
     def is_leader(self) -> bool:
@@ -81,6 +91,18 @@ _CLUSTER: Optional[Cluster] = None
 
 
 WAIT_TIMEOUT_S = 7 * 24 * 3600
+# engine loading: the failsafe guard's per-stage limit (engine_load / k9_create, 900 s) plus margin;
+# a rank that really hangs there is ended by the guard first, with the stage named
+LOAD_STAGE_LIMIT_S = 900.0
+LOAD_TIMEOUT_S = int(LOAD_STAGE_LIMIT_S + 60)
+
+
+def load_group_for(ranks) -> Optional[object]:
+    """A gloo group over ``ranks`` with the load timeout (collective over the WORLD: call it in the
+    same order on every rank, like ``dist.new_group``)."""
+    if not dist.is_initialized():
+        return None
+    return dist.new_group(list(ranks), backend="gloo", timeout=datetime.timedelta(seconds=LOAD_TIMEOUT_S))
 
 
 SHARED_GPU_QUEUE_BUDGET = 16   # hardware queues the ranks sharing one card may map together
@@ -147,8 +169,8 @@ def rehearsal_cu_split(world: int, local: int) -> Optional[str]:
 
 def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     """Initialize from torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); single process otherwise.
-    ``timeout_s``: every collective of the world / control groups (and, by default, of TP groups
-    created later) fails after it — the commands size it from the turn timeout
+    ``timeout_s``: every collective of the world / control groups (and of the TP groups the SPMD
+    commands create, knights/spmd.py) fails after it — the commands size it from the turn timeout
     (parallel/launch.py collective_timeout_s), so a stalled rank surfaces within minutes."""
     global _CLUSTER
     if _CLUSTER is not None:
@@ -167,7 +189,7 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
     device = f"cuda:{gpu_index}" if use_gpu else "cpu"
     if use_gpu:
         torch.cuda.set_device(gpu_index)
-    c = Cluster(rank=rank, world=world, local_rank=local, device=device)
+    c = Cluster(rank=rank, world=world, local_rank=local, device=device, timeout_s=int(timeout_s))
     # a 1-rank world normally runs without a process group; ROUNDTABLE_DIST_BACKEND=nccl forces an
     # RCCL one (exercises the RCCL data plane on a 1-GPU box, tools/nccl_check.py)
     if world > 1 or (forced == "nccl" and use_gpu):
@@ -182,6 +204,7 @@ def init_cluster(prefer_gpu: bool = True, timeout_s: int = 1800) -> Cluster:
         td = datetime.timedelta(seconds=timeout_s)
         c.cpu_group = dist.new_group(backend="gloo", timeout=td) if backend == "nccl" else dist.group.WORLD
         c.wait_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=WAIT_TIMEOUT_S))
+        c.load_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=LOAD_TIMEOUT_S))
     _CLUSTER = c
     return c
 

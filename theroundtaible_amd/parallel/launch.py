@@ -123,6 +123,9 @@ def collective_timeout_s(config: RoundtableConfig, world: Optional[int] = None) 
     rank runs one after another, plus a minute of margin — 180 s for the usual one group per rank,
     instead of torch's 30-minute default. Waits on a person (the King) use the cluster's
     long-timeout wait group instead."""
+    env = os.environ.get("ROUNDTABLE_COLLECTIVE_TIMEOUT_S")   # explicit override (operators, tests)
+    if env:
+        return max(1, int(float(env)))
     t = float(getattr(config.rules, "timeout_per_turn_seconds", 120) or 120)
     world = world or int(os.environ.get("WORLD_SIZE", "1"))
     per_rank = 1

@@ -26,6 +26,11 @@ class TPInfo:
     rank: int = 0
     group: Optional[object] = None   # torch.distributed ProcessGroup
     oneshot: Optional[object] = None  # parallel.oneshot.OneShotAllReduce (decode-size messages)
+    # gloo group over the same ranks with the engine-load timeout (parallel/cluster.py
+    # load_group_for): Engine construction meets there after loading its weights and before the
+    # group's first collective (K9 set-up), so a rank that loads slowly is waited for with the load
+    # limit, not the short containment timeout of ``group``
+    load_group: Optional[object] = None
 
     @property
     def enabled(self) -> bool:

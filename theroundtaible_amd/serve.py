@@ -237,6 +237,9 @@ class Scheduler:
             active = still
 
 
+PING_INTERVAL_S = float(os.environ.get("ROUNDTABLE_SERVE_PING_S", "600"))
+
+
 class MirroredEngine:
     """Rank 0's view of a tensor-parallel engine: the scheduler's engine operations are announced
     to the follower ranks (:func:`serve_follower`) over the control plane, then run locally —
@@ -248,6 +251,22 @@ class MirroredEngine:
         self._op_limit_s = op_limit_s
         self._lock = threading.Lock()    # one announced operation at a time, in issue order
         self.diverged: Optional[str] = None   # set when a follower's outcome differed from ours
+        self._last_op = time.monotonic()
+        self._stopped = False
+        # an idle server pings its followers: their wait for the next operation then
+        # never runs into the wait group's (7-day) timeout, however long no request comes
+        self.ping_s = PING_INTERVAL_S
+        threading.Thread(target=self._keepalive, name="serve-tp-keepalive", daemon=True).start()
+
+    def _keepalive(self) -> None:
+        while True:
+            time.sleep(min(self.ping_s, 60.0))
+            with self._lock:
+                if self._stopped or self.diverged is not None:
+                    return
+                if time.monotonic() - self._last_op >= self.ping_s:
+                    self._cluster.broadcast_object(("ping",), wait=True)
+                    self._last_op = time.monotonic()
 
     def __getattr__(self, name):
         return getattr(self._engine, name)
@@ -263,6 +282,7 @@ class MirroredEngine:
         # the operation and the outcome gather run on the containment-timeout groups and under a
         # stage limit, so a follower that stalls mid-operation ends the server with a message
         self._cluster.broadcast_object(op, wait=True)
+        self._last_op = time.monotonic()
         res, err = None, None
         try:
             with failsafe.stage(f"serve {op[0]}", limit_s=self._op_limit_s):
@@ -293,8 +313,9 @@ class MirroredEngine:
 
     def stop_followers(self) -> None:
         with self._lock:
-            if self.diverged is None:
+            if self.diverged is None and not self._stopped:
                 self._cluster.broadcast_object(("stop",), wait=True)
+            self._stopped = True
 
 
 def _outcome(err: Optional[BaseException]) -> tuple:
@@ -313,6 +334,8 @@ def serve_follower(engine: Engine, cluster, op_limit_s: Optional[float] = None) 
         kind = op[0]
         if kind == "stop":
             return n
+        if kind == "ping":                                  # rank 0's idle keepalive
+            continue
         err = None
         try:
             with failsafe.stage(f"serve {kind}", limit_s=op_limit_s):
@@ -594,7 +617,8 @@ def build_server(model: str, weights: str = "random:0", device: str = "cuda:0", 
                           lambda rec: sys.stderr.write(failsafe.describe(rec, "roundtable serve") + "\n"),
                           default_s=float("inf"), exit_code=2,
                           limits={"engine_load": 900.0, "k9_create": 900.0, "capture": op_limit_s}).start()
-        tpi = TPInfo(size=tp, rank=cluster.rank, group=dist.group.WORLD)
+        # the engine meets on the load-timeout group after loading (a slower follower is waited for)
+        tpi = TPInfo(size=tp, rank=cluster.rank, group=dist.group.WORLD, load_group=cluster.load_group)
         if device != "cpu":
             device = cluster.device
     ecfg = EngineConfig(model=model, weights=weights, device=device, dtype=dtype, use_graphs=use_graphs,

@@ -31,7 +31,7 @@ import threading
 import time
 from typing import Callable, Dict, Optional
 
-_lock = threading.Lock()
+_lock = threading.RLock()   # re-entrant: the SIGTERM handler reads the stage on the main thread
 # stage stack per thread: engines capture from their own threads (orchestrator.execute_plan), so
 # a process-global stage saved / restored by overlapping sub-stages could restore a stale value;
 # each thread keeps its own stack and the guard checks every thread's innermost stage
