@@ -191,3 +191,79 @@ def test_shared_system_prompt_concurrent_batch(server):
     for t in ts:
         t.join()
     assert not errs and res == [200] * 4
+
+
+def _stream_events(url, body):
+    """POST with stream=true; (list of parsed SSE data objects, arrival times relative to the POST)."""
+    req = urllib.request.Request(url, data=json.dumps(body).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    t0 = time.perf_counter()
+    events, times = [], []
+    with urllib.request.urlopen(req, timeout=120) as r:
+        assert r.status == 200 and r.headers["Content-Type"].startswith("text/event-stream")
+        for raw in r:
+            line = raw.decode().strip()
+            if not line.startswith("data: "):
+                continue
+            payload = line[len("data: "):]
+            events.append(payload if payload == "[DONE]" else json.loads(payload))
+            times.append(time.perf_counter() - t0)
+    return events, times
+
+
+def test_streaming_emits_chunks_during_decode(server):
+    """a 64-token completion streams >= 2 content chunks before [DONE] (one per
+    host readback of the decode loop), and the chunks concatenate to the non-streamed text (greedy)."""
+    body = {"messages": [{"role": "user", "content": "Vertel over de ronde tafel"}], "max_tokens": 64,
+            "temperature": 0, "ignore_eos": True}
+    want = json.loads(_post(server.url + "/v1/chat/completions", body)[1])["choices"][0]["message"]["content"]
+    events, times = _stream_events(server.url + "/v1/chat/completions", dict(body, stream=True))
+    assert events[-1] == "[DONE]"
+    content = [e["choices"][0]["delta"].get("content", "") for e in events[:-1]]
+    pieces = [c for c in content if c]
+    assert len(pieces) >= 2, content
+    assert "".join(pieces) == want
+    assert events[0]["choices"][0]["delta"]["role"] == "assistant"
+    assert events[-2]["choices"][0]["finish_reason"] == "length"
+    # the text arrives while decoding: the first content chunk well before the end of the stream
+    first = next(i for i, c in enumerate(content) if c)
+    assert times[first] < times[-1]
+    # the completions endpoint and Ollama NDJSON stream the same way
+    cb = {"prompt": "Onderwerp:", "max_tokens": 40, "temperature": 0, "ignore_eos": True}
+    want_c = json.loads(_post(server.url + "/v1/completions", cb)[1])["choices"][0]["text"]
+    ev_c, _ = _stream_events(server.url + "/v1/completions", dict(cb, stream=True))
+    assert "".join(e["choices"][0]["text"] for e in ev_c[:-1]) == want_c
+    ob = {"messages": [{"role": "user", "content": "q"}], "options": {"num_predict": 40, "temperature": 0}}
+    want_o = json.loads(_post(server.url + "/api/chat", dict(ob, stream=False))[1])["message"]["content"]
+    req = urllib.request.Request(server.url + "/api/chat", data=json.dumps(dict(ob, stream=True)).encode(),
+                                 method="POST", headers={"Content-Type": "application/json"})
+    with urllib.request.urlopen(req, timeout=120) as r:
+        lines = [json.loads(l) for l in r.read().decode().splitlines() if l.strip()]
+    assert lines[-1]["done"] is True and all(not l["done"] for l in lines[:-1]) and len(lines) >= 3
+    assert "".join(l["message"]["content"] for l in lines) == want_o
+
+
+def test_sixty_four_concurrent_clients_all_served(server):
+    """a burst of 64 clients connecting at once must get 64 x HTTP 200 (the
+    listen backlog was socketserver's 5; an overflow is reset by the kernel)."""
+    n = 64
+    codes, errs = [], []
+    bar = threading.Barrier(n)
+    lock = threading.Lock()
+
+    def go(i):
+        bar.wait()
+        try:
+            c = _post(server.url + "/v1/completions", {"prompt": f"vraag {i}", "max_tokens": 2})[0]
+            with lock:
+                codes.append(c)
+        except Exception as e:  # noqa: BLE001
+            with lock:
+                errs.append(repr(e))
+    ts = [threading.Thread(target=go, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and codes == [200] * n, (errs[:3], len(codes))
+    assert server.httpd.request_queue_size >= 128

@@ -91,6 +91,13 @@ class _Request:
     done: threading.Event = field(default_factory=threading.Event)
     result: Any = None
     error: Optional[BaseException] = None
+    # streaming: the scheduler puts the generated ids so far after every host readback (the first
+    # token after prefill, then every decode chunk), then None when the request is complete
+    stream_q: Optional["queue.Queue"] = None
+
+    def publish(self, gen: List[int]) -> None:
+        if self.stream_q is not None:
+            self.stream_q.put(list(gen))
 
 
 @dataclass
@@ -186,6 +193,8 @@ class Scheduler:
             except Exception:  # noqa: BLE001
                 pass
         r.done.set()
+        if r.stream_q is not None:
+            r.stream_q.put(None)
 
     # ---- engine loop --------------------------------------------------------------------------
     def _loop(self) -> None:
@@ -208,6 +217,7 @@ class Scheduler:
                         self.stats["admitted_midflight"] += len(started)
                 for r, t, (sq, first, m) in zip(new, turns, started):
                     a = _Active(r, sq, t, [first], dict(m, batch=0), time.perf_counter())
+                    r.publish(a.gen)
                     if self._finished(a):
                         self._complete(a)
                     else:
@@ -226,6 +236,8 @@ class Scheduler:
             for a, toks in zip(active, outs):
                 a.gen.extend(toks)
                 a.metrics["batch"] = max(a.metrics.get("batch", 0), len(active))
+                if not self._finished(a):          # a finished request's text comes with its result
+                    a.req.publish(a.gen)
             with self._lock:
                 self.stats["batches"] += 1
                 self.stats["decode_steps"] += max(1, steps)
@@ -354,6 +366,18 @@ def serve_follower(engine: Engine, cluster, op_limit_s: Optional[float] = None) 
             return n
 
 
+class _HTTPServer(ThreadingHTTPServer):
+    """``ThreadingHTTPServer`` with a listen backlog for bursts of clients. socketserver's default
+    backlog is 5: when more connections arrive than the accept thread takes in time (it shares the
+    GIL with the scheduler and every handler thread), Linux resets the overflow — 32-64 client
+    bursts lost 1-9 requests (CPU repro with 128 simultaneous clients against a
+    5-deep backlog: 54 of 384 requests reset, 0 with 1024). The kernel caps the value at
+    ``net.core.somaxconn``."""
+    request_queue_size = 1024
+    daemon_threads = True
+    allow_reuse_address = True
+
+
 @dataclass
 class _Output:
     text: str
@@ -380,8 +404,11 @@ class RoundtableServer:
         class Handler(BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
 
-            def log_message(self, fmt, *args):  # quiet by default
+            def log_message(self, fmt, *args):  # quiet by default (one line per request)
                 pass
+
+            def log_error(self, fmt, *args):     # errors are never silent (stderr)
+                sys.stderr.write("roundtable serve: %s - %s\n" % (self.address_string(), fmt % args))
 
             def _send(self, code: int, obj: Any, ctype: str = "application/json") -> None:
                 body = obj if isinstance(obj, bytes) else (
@@ -391,6 +418,52 @@ class RoundtableServer:
                 self.send_header("Content-Length", str(len(body)))
                 self.end_headers()
                 self.wfile.write(body)
+
+            def _chunk(self, data: bytes) -> None:
+                """One HTTP/1.1 chunk (Transfer-Encoding: chunked), flushed at once."""
+                self.wfile.write(b"%x\r\n%s\r\n" % (len(data), data))
+                self.wfile.flush()
+
+            def _stream(self, prompt, body, session, first, delta, last, sse: bool = True) -> None:
+                """Stream a completion as it decodes: SSE ``data:`` events (OpenAI) or NDJSON lines
+                (Ollama). Text goes out after every host readback of the decode loop (the first
+                token after prefill, then each decode chunk); the pieces concatenate to exactly
+                the non-streamed text (Server.visible_text, the final result's cut and decode)."""
+                r = server.submit(prompt, body, session, stream=True)
+                self.send_response(200)
+                self.send_header("Content-Type", "text/event-stream" if sse else "application/x-ndjson")
+                self.send_header("Cache-Control", "no-cache")
+                self.send_header("Transfer-Encoding", "chunked")
+                self.end_headers()
+
+                def emit(obj) -> None:
+                    self._chunk((f"data: {json.dumps(obj)}\n\n" if sse else json.dumps(obj) + "\n").encode())
+                if first is not None:
+                    emit(first)
+                sent = ""
+                deadline = time.monotonic() + server.sched.timeout_s + 30
+                while True:
+                    try:
+                        ids = r.stream_q.get(timeout=max(0.1, deadline - time.monotonic()))
+                    except queue.Empty:
+                        r.error = r.error or TimeoutError("generation timed out")
+                        break
+                    if ids is None:
+                        break
+                    text = server.visible_text(ids, r.params)
+                    if text.startswith(sent) and len(text) > len(sent):
+                        emit(delta(text[len(sent):]))
+                        sent = text
+                if r.error is None and r.result is not None:
+                    final = r.result.text
+                    if final.startswith(sent) and len(final) > len(sent):
+                        emit(delta(final[len(sent):]))
+                    emit(last(r.result, r))
+                else:
+                    emit({"error": {"message": str(r.error), "type": "server_error"}})
+                if sse:
+                    self._chunk(b"data: [DONE]\n\n")
+                self._chunk(b"")                      # end of the chunked body
 
             def _json_body(self) -> Dict[str, Any]:
                 n = int(self.headers.get("Content-Length") or 0)
@@ -440,18 +513,20 @@ class RoundtableServer:
                 msgs = body.get("messages")
                 if not isinstance(msgs, list) or not msgs:
                     raise ValueError("'messages' must be a non-empty list")
-                out, r = server.generate(server.chat_prompt(msgs), body, body.get("user") or body.get("session"))
                 rid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
-                usage = server.usage(out)
                 if body.get("stream"):
-                    chunk = {"id": rid, "object": "chat.completion.chunk", "created": int(time.time()),
-                             "model": server.model_name,
-                             "choices": [{"index": 0, "delta": {"role": "assistant", "content": out.text},
-                                          "finish_reason": None}]}
-                    end = dict(chunk, choices=[{"index": 0, "delta": {}, "finish_reason": server.finish(out, r)}])
-                    sse = f"data: {json.dumps(chunk)}\n\ndata: {json.dumps(end)}\n\ndata: [DONE]\n\n"
-                    self._send(200, sse, "text/event-stream")
+                    base = {"id": rid, "object": "chat.completion.chunk", "created": int(time.time()),
+                            "model": server.model_name}
+
+                    def piece(delta, finish=None):
+                        return dict(base, choices=[{"index": 0, "delta": delta, "finish_reason": finish}])
+                    self._stream(server.chat_prompt(msgs), body, body.get("user") or body.get("session"),
+                                 first=piece({"role": "assistant", "content": ""}),
+                                 delta=lambda t: piece({"content": t}),
+                                 last=lambda out, r: piece({}, server.finish(out, r)))
                     return
+                out, r = server.generate(server.chat_prompt(msgs), body, body.get("user") or body.get("session"))
+                usage = server.usage(out)
                 self._send(200, {"id": rid, "object": "chat.completion", "created": int(time.time()),
                                  "model": server.model_name,
                                  "choices": [{"index": 0, "message": {"role": "assistant", "content": out.text},
@@ -464,6 +539,15 @@ class RoundtableServer:
                     prompt = "".join(str(p) for p in prompt)
                 if not isinstance(prompt, str):
                     raise ValueError("'prompt' must be a string")
+                if body.get("stream"):
+                    base = {"id": f"cmpl-{uuid.uuid4().hex[:24]}", "object": "text_completion",
+                            "created": int(time.time()), "model": server.model_name}
+
+                    def piece(text, finish=None):
+                        return dict(base, choices=[{"index": 0, "text": text, "finish_reason": finish}])
+                    self._stream(prompt, body, body.get("user"), first=None, delta=piece,
+                                 last=lambda out, r: piece("", server.finish(out, r)))
+                    return
                 out, r = server.generate(prompt, body, body.get("user"))
                 self._send(200, {"id": f"cmpl-{uuid.uuid4().hex[:24]}", "object": "text_completion",
                                  "created": int(time.time()), "model": server.model_name,
@@ -478,14 +562,29 @@ class RoundtableServer:
                 params = {"temperature": opts.get("temperature"), "top_p": opts.get("top_p"),
                           "top_k": opts.get("top_k"), "seed": opts.get("seed"),
                           "max_tokens": opts.get("num_predict")}
+                if body.get("stream"):
+                    # Ollama's NDJSON stream: one message object per line, then a done record
+                    # (a request without "stream" keeps the one-object reply of rounds 1-5)
+                    def line(text):
+                        return {"model": server.model_name, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ"),
+                                "message": {"role": "assistant", "content": text}, "done": False}
+
+                    def done(out, r):
+                        return {"model": server.model_name, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ"),
+                                "message": {"role": "assistant", "content": ""}, "done": True,
+                                "done_reason": server.finish(out, r),
+                                "prompt_eval_count": int(out.metrics.get("prompt_tokens", 0)),
+                                "eval_count": len(out.ids)}
+                    self._stream(server.chat_prompt(msgs), params, body.get("session"), first=None, delta=line,
+                                 last=done, sse=False)
+                    return
                 out, _ = server.generate(server.chat_prompt(msgs), params, body.get("session"))
                 self._send(200, {"model": server.model_name, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ"),
                                  "message": {"role": "assistant", "content": out.text}, "done": True,
                                  "prompt_eval_count": int(out.metrics.get("prompt_tokens", 0)),
                                  "eval_count": len(out.ids)})
 
-        self.httpd = ThreadingHTTPServer((host, port), Handler)
-        self.httpd.daemon_threads = True
+        self.httpd = _HTTPServer((host, port), Handler)
         self.host, self.port = self.httpd.server_address[:2]
         self._thread: Optional[threading.Thread] = None
 
@@ -525,10 +624,23 @@ class RoundtableServer:
                               max_new_tokens=min(max_tokens, 8192), ignore_eos=bool(body.get("ignore_eos", False)),
                               stop_on_consensus=False)
 
-    def generate(self, prompt: str, body: Dict[str, Any], session: Optional[str]) -> Tuple[Any, _Request]:
+    def submit(self, prompt, body: Dict[str, Any], session: Optional[str], stream: bool = False) -> _Request:
         params = self.sampling(body)
         key = f"session:{session}" if session else f"anon:{next(self._anon)}"
-        r = self.sched.submit(_Request(key, prompt, params, persistent=bool(session)))
+        return self.sched.submit(_Request(key, prompt, params, persistent=bool(session),
+                                          stream_q=queue.Queue() if stream else None))
+
+    def visible_text(self, ids: List[int], params: SamplingParams) -> str:
+        """The text of ``ids`` so far as the final result will show it (cut at max_new_tokens and at
+        a stop id, decoded), minus a trailing incomplete UTF-8 character (a byte-level BPE token
+        can end mid-character: held back until the next piece completes it)."""
+        gen = ids[:params.max_new_tokens]
+        if not params.ignore_eos:
+            gen = cut_at_stop(gen, self.engine.tokenizer.stop_ids)
+        return self.engine.tokenizer.decode(gen).rstrip("\ufffd")
+
+    def generate(self, prompt: str, body: Dict[str, Any], session: Optional[str]) -> Tuple[Any, _Request]:
+        r = self.submit(prompt, body, session)
         if not r.done.wait(self.sched.timeout_s + 30):
             raise TimeoutError("generation timed out")
         if r.error is not None:
