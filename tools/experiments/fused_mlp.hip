@@ -28,8 +28,43 @@ struct MlpArgs {
   int n_gu, n_dn;     // tiles per phase
   int* sync;          // [2] counters, zero at launch (re-armed by the last workgroup out)
   int* err;
-  int phases;         // diagnosis: 3 = both (the experiment), 1 = gate_up only, 2 = down only; +4 plain phase-1 stores
+  int phases;         // diagnosis: 3 = both (the experiment), 1 = gate_up only, 2 = down only; +4 plain phase-1 stores;
+                      // +8 no in-launch synchronisation at all (timing only: phase 2 may read stale g);
+                      // +16 the hand-off and the exit re-arm on 8 sharded counters (round 6, below)
 };
+
+// Round 6: the 2.3x phase-1 anomaly. Phase 1 "alone" still ran the whole
+// single-counter protocol: one arrival per item on ONE device-scope word (224 at tp 8), a poll by
+// every workgroup on that word, and one exit arrival per workgroup on a second single word. The
+// MI355X price list puts a 255 -> 1 fan-in on one counter at 3.6-4.5 us under streaming and a
+// single-counter grid barrier at 7.4 us (MI355X_MICROARCH "fanin", "barrier-counter"). The sharded
+// form below spreads arrivals over 8 words on separate 128-B lines, labelled by blockIdx % 8 (a
+// label, not a placement assumption: the waiter sums all eight), so no word takes more than
+// ceil(G / 8) arrivals; the exit re-arm is two-level (last of a shard -> top word).
+constexpr int SH_STRIDE = 32;       // ints between shard words (128 B)
+RT_DEVICE int* sh_arr(int* sync, int s) { return sync + SH_STRIDE * (1 + s); }
+RT_DEVICE int* sh_exit(int* sync, int s) { return sync + SH_STRIDE * (9 + s); }
+RT_DEVICE int* sh_top(int* sync) { return sync + SH_STRIDE * 17; }
+
+RT_DEVICE void wait_sharded(int* sync, int target, int* err) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    long long it = 0;
+    while (true) {
+      int v = lane < 8 ? __hip_atomic_load(sh_arr(sync, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) v += __shfl_xor(v, o, 64);
+      v = __shfl(v, 0, 64);              // every lane takes lane 0's total (a uniform exit)
+      if (v >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > POLL_LIMIT) {
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
 
 union MlpSmem {
   GemmSmem<2, NWM> g2;
@@ -83,26 +118,42 @@ __global__ void __launch_bounds__(NWM * 64) fused_mlp_kernel(MlpArgs P) {
       Stage<PRO_NORM, EPI_SWIGLU, UM> st;
       gemm_tile<PRO_NORM, EPI_SWIGLU, NWM, UM, ST1, false, 0>(P.gu, b, sm.g2, st, false, false);
     }
-    arrive(P.sync);
+    if (P.phases & 16) arrive(sh_arr(P.sync, w & 7));
+    else if (!(P.phases & 8)) arrive(P.sync);
   }
   {
     Stage<PRO_PLAIN, EPI_RESID, UM> st;
     const int ndn = (P.phases & 2) ? P.n_dn : 0;
     if (w < ndn) gemm_prefetch<PRO_PLAIN, EPI_RESID, NWM, UM>(P.dn, w, st);
-    wait_for(P.sync, items, P.err);
+    if (P.phases & 16) wait_sharded(P.sync, items, P.err);
+    else if (!(P.phases & 8)) wait_for(P.sync, items, P.err);
     // g was written in this launch: staged ONCE per tile into LDS with sc1 loads (ALDS), not an
     // sc1 load per k-step (phase 2 alone: 8.4 us with per-step sc1 loads vs 5.0 us as a launch);
     // res is stored plainly (the next launch reads it)
     for (int t = w; t < ndn; t += G) gemm_tile<PRO_PLAIN, EPI_RESID, NWM, UM, false, true, 1>(P.dn, t, sm.g1, st, t == w, false, nullptr, &al);
   }
   // the last workgroup out re-arms the counters (every workgroup is past its wait)
+  if (P.phases & 8) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(P.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == G - 1) {
-      __hip_atomic_store(P.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(P.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (P.phases & 16) {
+      const int sh = w & 7, n_sh = (G - sh + 7) / 8, n_used = G < 8 ? G : 8;
+      const int prev = __hip_atomic_fetch_add(sh_exit(P.sync, sh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == n_sh - 1) {
+        __hip_atomic_store(sh_exit(P.sync, sh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int t = __hip_atomic_fetch_add(sh_top(P.sync), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == n_used - 1) {
+          for (int k = 0; k < 8; ++k) __hip_atomic_store(sh_arr(P.sync, k), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sh_top(P.sync), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {
+      const int prev = __hip_atomic_fetch_add(P.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == G - 1) {
+        __hip_atomic_store(P.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(P.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }

@@ -29,7 +29,7 @@ from theroundtaible_amd import ops  # noqa: E402
 DEV = "cuda"
 
 
-def timed(fn, reps=5):
+def timed(fn, reps=5, tag=""):
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -49,6 +49,7 @@ def timed(fn, reps=5):
         b.record()
         torch.cuda.synchronize()
         best = min(best, a.elapsed_time(b) * 1e3)
+    print(f"  timed {tag}: {best:.1f} us per graph", flush=True)
     return best
 
 
@@ -79,7 +80,7 @@ def main():
         res = x0.clone()
         g = torch.empty(M, I, dtype=torch.bfloat16, device=DEV)
         sw = ops.split_workspace(DEV)
-        sync = torch.zeros(2, dtype=torch.int32, device=DEV)
+        sync = torch.zeros(576, dtype=torch.int32, device=DEV)   # legacy words 0-1, sharded words (fused_mlp.hip)
         err = torch.zeros(1, dtype=torch.int32, device=DEV)
         sk = dict(split_ws=sw, split_mode=ops.SPLIT_K)
 
@@ -126,6 +127,22 @@ def main():
         tf1 = timed(lambda: [fused(i % copies, 1) for i in range(a.calls)]) / a.calls
         tf2 = timed(lambda: [fused(i % copies, 2) for i in range(a.calls)]) / a.calls
         tf5 = timed(lambda: [fused(i % copies, 5) for i in range(a.calls)]) / a.calls   # phase 1, plain stores
+        # round 6: the synchronisation apart — no in-launch sync at all (timing only),
+        # and the hand-off + exit re-arm on 8 sharded counters
+        tf9 = timed(lambda: [fused(i % copies, 9) for i in range(a.calls)]) / a.calls     # phase 1, no sync
+        tf10 = timed(lambda: [fused(i % copies, 10) for i in range(a.calls)]) / a.calls   # phase 2, no sync
+        tf11 = timed(lambda: [fused(i % copies, 11) for i in range(a.calls)]) / a.calls   # both, no sync (wrong g)
+        tf17 = timed(lambda: [fused(i % copies, 17) for i in range(a.calls)]) / a.calls   # phase 1, sharded
+        tf18 = timed(lambda: [fused(i % copies, 18) for i in range(a.calls)]) / a.calls   # phase 2, sharded
+        tf19 = timed(lambda: [fused(i % copies, 19) for i in range(a.calls)]) / a.calls   # both, sharded
+        res.copy_(x0)
+        fused(0, 19)
+        r_sh = res.clone()
+        torch.cuda.synchronize()
+        row.update(fused_phase1_nosync_us=round(tf9, 2), fused_phase2_nosync_us=round(tf10, 2),
+                   fused_nosync_us=round(tf11, 2), fused_phase1_sharded_us=round(tf17, 2),
+                   fused_phase2_sharded_us=round(tf18, 2), fused_sharded_us=round(tf19, 2),
+                   sharded_saving_us=round(t2 - tf19, 2), sharded_equals_fused=bool(torch.equal(r_sh, r_f1)))
         row.update(two_launch_us=round(t2, 2), fused_us=round(tf, 2), saving_us=round(t2 - tf, 2),
                    gate_up_launch_us=round(tgu, 2), down_launch_us=round(tdn, 2),
                    fused_phase1_only_us=round(tf1, 2), fused_phase2_only_us=round(tf2, 2),
