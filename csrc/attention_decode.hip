@@ -16,7 +16,7 @@ using namespace attn;
 // different placement changes only speed.
 RT_DEVICE int xcd_item(int lin, int nwg) { return (lin & 7) * (nwg >> 3) + (lin >> 3); }
 
-template <int D, int GM, int W = NW, bool PP = true>
+template <int D, int GM, int W = NW, bool PP = true, int LM = 0>
 __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
   __shared__ AttnSmem<D, GM, W> sm;
   int bh = blockIdx.x, split = blockIdx.y;
@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
     split = rem - b * ns;
     bh = b * p.Hkv + hk;
   }
-  attn_item<D, false, GM, W, PP>(p, bh, split, sm);
+  attn_item<D, false, GM, W, PP, LM>(p, bh, split, sm);
 }
 
 // Split-KV combine as its own launch, for launches with many partial slots per query row
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
 }  // namespace
 
 
-// q [B, Hq, D]; k_cache [NB, Hkv, 32, D]; v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32;
+// q [B, Hq, D]; k_cache [NB, Hkv, 32, D] (chunk-major blocks, common.h kc_elem); v_cache [NB, Hkv, D, 32]; block_tables [B, max_blocks] int32;
 // defer_combine: leave the separate combine to the caller (*deferred = 1 when it was needed);
 // part_o >= B*Hq*slot_stride*D floats, part_ml >= B*Hq*slot_stride*4 floats, counters >= B*Hkv ints
 // (zeroed once). groups: nullptr or [B][3] {first, n, shared blocks} (shared-prefix groups,
@@ -202,13 +202,6 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   const bool hk_split_ok = Hkv % 8 == 0 || 8 % Hkv == 0;
   args.xcd = (xcd_env && (B * Hkv * num_splits) % 8 == 0 && (B * Hq * (D / 32)) % 8 == 0 && hk_split_ok) ? 1 : 0;
   args.plain_partials = (plain_env && args.ext_combine && !defer_combine) ? 1 : 0;
-  // K row read order (attn_core.h AttnArgs::kperm): each K load instruction reads 64 contiguous
-  // bytes per row (16 rows x 64 B) instead of 4 x 16 B at a 64-B stride (32 half-used cache lines):
-  // half the L1 line requests per K tile. Llama-3-8B tp 1, B = 3 grouped, 22K / 40K shared keys
-  // 29.5 -> 28.1 / 43.5 -> 41.6 us, private rows -9 %, B = 1 25K 28.0 -> 26.6, tp 8 shard even
-  // (profiles/r05/attn_kperm_ab.md). RT_ATTN_KPERM=0 restores the old order (A/B)
-  static const int kperm_env = getenv("RT_ATTN_KPERM") ? atoi(getenv("RT_ATTN_KPERM")) : 1;
-  args.kperm = kperm_env ? 1 : 0;
   const int G = Hq / Hkv;
   // a group's n*G columns need the 16-column LDS merge buffers
   // K/V loop form (attn_core.h PP): the copy-free ping-pong wins where a workgroup streams many
@@ -217,12 +210,29 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   // copy loop (profiles/r05/attn_pingpong_ab.md). RT_ATTN_PP=0 / 1 pins it (A/B).
   static const int pp_env = getenv("RT_ATTN_PP") ? atoi(getenv("RT_ATTN_PP")) : -1;
   const bool pp = pp_env >= 0 ? pp_env != 0 : Hkv >= 4;
-#define RT_PD2(DV, PPV)                                                                                       \
-  do {                                                                                                        \
-    if (groups != nullptr) hipLaunchKernelGGL((paged_decode_kernel<DV, 16, NW, PPV>), grid, block, 0, stream, args); \
-    else if (G <= 4) hipLaunchKernelGGL((paged_decode_kernel<DV, 4, NW, PPV>), grid, block, 0, stream, args);   \
-    else if (G <= 8) hipLaunchKernelGGL((paged_decode_kernel<DV, 8, NW, PPV>), grid, block, 0, stream, args); \
-    else hipLaunchKernelGGL((paged_decode_kernel<DV, 16, NW, PPV>), grid, block, 0, stream, args);         \
+  // K/V load mode (attn_core.h LM_*): nontemporal K and V loads where every K/V byte is read
+  // once per launch — shared-prefix groups (each shared block streamed once for the group) and
+  // a single row. Rows without groups may hold the same blocks (forked prefixes): there the
+  // default policy lets the 2nd..nth reads hit L2 / MALL (private rows over one 22K prefix:
+  // 33.8 us default vs 35.9 nt). With the chunk-major K blocks, tp 1, 3 knights x 22K shared
+  // keys 27.9 -> 25.2 us, 40K 41.2 -> 38.1, B = 1 25K 25.9 -> 23.7 (profiles/r06/attn_kchunk.md).
+  // RT_ATTN_LM pins the mode (0..3, A/B).
+  static const int lm_env = getenv("RT_ATTN_LM") ? atoi(getenv("RT_ATTN_LM")) : -1;
+  const int lm = lm_env >= 0 ? (lm_env & 3) : ((groups != nullptr || B == 1) ? (LM_NTK | LM_NTV) : 0);
+  args.lm = lm;
+#define RT_PD3(DV, PPV, LMV)                                                                                          \
+  do {                                                                                                                \
+    if (groups != nullptr) hipLaunchKernelGGL((paged_decode_kernel<DV, 16, NW, PPV, LMV>), grid, block, 0, stream, args); \
+    else if (G <= 4) hipLaunchKernelGGL((paged_decode_kernel<DV, 4, NW, PPV, LMV>), grid, block, 0, stream, args);   \
+    else if (G <= 8) hipLaunchKernelGGL((paged_decode_kernel<DV, 8, NW, PPV, LMV>), grid, block, 0, stream, args);   \
+    else hipLaunchKernelGGL((paged_decode_kernel<DV, 16, NW, PPV, LMV>), grid, block, 0, stream, args);              \
+  } while (0)
+#define RT_PD2(DV, PPV)                             \
+  do {                                              \
+    if (lm == 0) RT_PD3(DV, PPV, 0);                \
+    else if (lm == 1) RT_PD3(DV, PPV, 1);           \
+    else if (lm == 2) RT_PD3(DV, PPV, 2);           \
+    else RT_PD3(DV, PPV, 3);                        \
   } while (0)
 #define RT_PD(DV) do { if (pp) RT_PD2(DV, true); else RT_PD2(DV, false); } while (0)
   if (D == 128) RT_PD(128);
@@ -230,6 +240,7 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   else return -2;
 #undef RT_PD
 #undef RT_PD2
+#undef RT_PD3
   if (args.ext_combine && defer_combine && D == 128) {
     // the caller runs the combine inside the next launch (combine_o.hip: combine + o-projection)
     if (deferred != nullptr) *deferred = 1;

@@ -112,8 +112,9 @@ __global__ void __launch_bounds__(256) prefill_kernel(
     unsigned char* vb = kb + C::KBYTES;
 #pragma unroll
     for (int i = 0; i < C::KLD; ++i) {
-      const int ch = tid * C::KLD + i;  // global 16-byte chunk index within the K tile
-      const int row = ch / C::NCH, c = ch - (ch / C::NCH) * C::NCH;
+      const int ch = tid * C::KLD + i;  // 16-byte chunk of the chunk-major K block (common.h kc_chunk)
+      int row, c;
+      rt::kc_chunk(ch, BS, row, c);
       *reinterpret_cast<uint4*>(kb + row * C::KROW + 16 * (c ^ (row & (C::NCH - 1)))) = kreg[i];
     }
 #pragma unroll

@@ -74,10 +74,9 @@ struct Loader {
                       const Blocks<NW>& b, size_t blk_stride, size_t head_off, int tid) {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
-      const int ch = tid * KL + i;          // 16-B chunk of the 64x128 K tile
-      const int row = ch >> 4, c = ch & 15;  // key, d-chunk
-      k[i] = *reinterpret_cast<const rt::u32x4*>(k_cache + (size_t)b.k[i] * blk_stride + head_off + (row & 31) * D +
-                                                 8 * c);
+      const int ch = tid * KL + i;          // 16-B chunk of the 64x128 K tile: block ch >> 9, whose
+                                            // chunk-major bytes are read in order (common.h kc_chunk)
+      k[i] = *reinterpret_cast<const rt::u32x4*>(k_cache + (size_t)b.k[i] * blk_stride + head_off + 8 * (ch & 511));
     }
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
@@ -90,7 +89,9 @@ struct Loader {
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
       const int ch = tid * KL + i;
-      const int row = ch >> 4, c = ch & 15;
+      int key, c;
+      rt::kc_chunk(ch & 511, 32, key, c);
+      const int row = ((ch >> 9) << 5) + key;
       *reinterpret_cast<rt::u32x4*>(kb + row * KROW + 16 * (c ^ (row & 15))) = k[i];
     }
 #pragma unroll

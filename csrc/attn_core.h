@@ -14,7 +14,8 @@
 // (r, g) of the S^T accumulator holds keys 8g..8g+7 of column r — exactly the A-operand
 // fragment of P.V (P never leaves registers) — and the matching B fragment of the
 // transposed value cache ([D][32] per block) is ONE 16-byte load per lane per d-chunk.
-// K rows are read as 64 contiguous bytes per lane (d permuted consistently on K and Q).
+// K blocks are chunk-major ([D/32][32 keys][32 dims]): each K load instruction reads 8 whole
+// 128-B lines (d permuted consistently on K and Q).
 // K/V go straight to VGPRs (cdna_hip_programming App. B "Attention decode") with the next
 // tile's loads in flight while the current tile computes. The 8 waves' softmax states
 // merge through LDS; the splits of one (sequence, kv head) are combined in the same launch
@@ -44,15 +45,32 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 template <int D>
 struct Tile {
-  short8 k[2][D / 32];  // [half][chunk]: K row key(h, r), d = kg + kc*c + j (kperm: kg = 8g, kc = 32;
-                        // else kg = (D/4)g, kc = 8 — the same permutation of d for Q and K)
+  short8 k[2][D / 32];  // [half][chunk]: K row key(h, r), d = 32c + 8g + j (the same order of d for Q)
   short8 v[D / 16];     // [d-chunk]: V[keys 8g..8g+7][d = 16e + r]
 };
 
+// K/V load mode (LM bits, the round-6 stream study, attention_decode.hip): nontemporal loads
+// (global_load ... nt, the cache policy of the weight streams) for the K tiles (LM_NTK) and the
+// V tiles (LM_NTV). Right where every K/V byte is read once per launch (grouped launches, one row).
+constexpr int LM_NTK = 1;
+constexpr int LM_NTV = 2;
+
+template <bool NT>
+RT_DEVICE short8 ld16(const uint16_t* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(reinterpret_cast<const short8*>(p));
+  else
+    return *reinterpret_cast<const short8*>(p);
+}
+
+// One 32-key tile for lane (r, g). K blocks are chunk-major ([D/32][32 keys][32 dims], common.h
+// kc_elem): the A fragment of half h, chunk c is key krow + 4h, dims 32c + 8g..+7, so one load
+// instruction reads 16 keys x 64 B = 8 whole 128-B lines (4-key runs of 256 B). V blocks are
+// [D][32 keys]: fragment e is dims 16e + r, keys 8g..8g+7, 1 KB contiguous per instruction.
 // SC1: the block may hold K/V written earlier in the same launch (persistent kernel): sc1 loads.
-template <int D, bool SC1>
+template <int D, bool SC1, int LM = 0>
 RT_DEVICE void load_tile(Tile<D>& t, const uint16_t* __restrict__ kblk, const uint16_t* __restrict__ vblk, int r,
-                         int g, int kg, int kc) {
+                         int g) {
   const int krow = 8 * (r >> 2) + (r & 3);
   if constexpr (SC1) {
     const auto kr_ = rt::buf_rsrc(kblk), vr_ = rt::buf_rsrc(vblk);
@@ -60,26 +78,25 @@ RT_DEVICE void load_tile(Tile<D>& t, const uint16_t* __restrict__ kblk, const ui
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int c = 0; c < D / 32; ++c)
-        t.k[h][c] = __builtin_bit_cast(short8, rt::sc1_load4(kr_, 2 * ((krow + 4 * h) * D + kg + kc * c)));
+        t.k[h][c] = __builtin_bit_cast(short8, rt::sc1_load4(kr_, 2 * (c * (BS * 32) + (krow + 4 * h) * 32 + 8 * g)));
 #pragma unroll
     for (int e = 0; e < D / 16; ++e)
       t.v[e] = __builtin_bit_cast(short8, rt::sc1_load4(vr_, 2 * ((16 * e + r) * BS + 8 * g)));
   } else {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint16_t* kr = kblk + (krow + 4 * h) * D + kg;
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int c = 0; c < D / 32; ++c) t.k[h][c] = *reinterpret_cast<const short8*>(kr + kc * c);
-    }
+      for (int c = 0; c < D / 32; ++c)
+        t.k[h][c] = ld16<(LM & LM_NTK) != 0>(kblk + c * (BS * 32) + (krow + 4 * h) * 32 + 8 * g);
 #pragma unroll
-    for (int e = 0; e < D / 16; ++e) t.v[e] = *reinterpret_cast<const short8*>(vblk + (16 * e + r) * BS + 8 * g);
+    for (int e = 0; e < D / 16; ++e) t.v[e] = ld16<(LM & LM_NTV) != 0>(vblk + (16 * e + r) * BS + 8 * g);
   }
 }
 
 struct AttnArgs {
   uint16_t* out;               // [B, Hq, D]
   const uint16_t* q;           // [B, Hq, D]
-  const uint16_t* k_cache;     // [NB, Hkv, 32, D]
+  const uint16_t* k_cache;     // [NB, Hkv, 32, D] bytes, each block chunk-major [D/32][32][32]
   const uint16_t* v_cache;     // [NB, Hkv, D, 32]
   const int* block_tables;     // [B, max_blocks]
   const int* ctx_lens;         // [B]
@@ -97,8 +114,7 @@ struct AttnArgs {
   int ext_combine = 0;         // 1: leave every partial for decode_combine_kernel (no in-launch combine)
   int xcd = 0;                 // 1: XCD-aware item order (attention_decode.hip), the launch's grid % 8 == 0
   int plain_partials = 0;      // 1 (ext_combine only): partials stay in the writer's L2 (plain stores)
-  int kperm = 0;               // 1: lane group g reads d = 32c + 8g.. (64 contiguous bytes of a K row per
-                               // load instruction instead of 4 x 16 B at a 64-B stride; Q the same way)
+  int lm = 0;                  // K/V load mode actually launched (LM_*), for the host's record
 };
 
 // GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
@@ -127,7 +143,8 @@ RT_DEVICE void store_bf16x4(uint16_t* dst, float a, float b_, float c, float d, 
 // W = waves per workgroup (8; 16 for grouped launches: twice the K/V in flight per CU and
 // enough threads to combine a whole group's slots in one round trip).
 // PP: ping-pong K/V tiles (two in flight per wave); false = the round-4 cur/nxt copy loop (A/B)
-template <int D, bool SC1, int GM = 16, int W = NW, bool PP = true>
+// LM: K/V load mode (LM_NTK / LM_NTV above)
+template <int D, bool SC1, int GM = 16, int W = NW, bool PP = true, int LM = 0>
 RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W>& S) {
   uint16_t* __restrict__ out = P.out;
   const uint16_t* __restrict__ q = P.q;
@@ -166,8 +183,9 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int rseq = r / G, rhead = r - (r / G) * G;  // column r -> (member, head within the kv group)
-  // reduction-dim order of the QK^T MFMAs (any permutation of d, the same for Q and K)
-  const int kg = P.kperm ? 8 * g : (D / 4) * g, kc = P.kperm ? 32 : 8;
+  // reduction-dim order of the QK^T MFMAs: lane group g holds d = 32c + 8g.. of chunk c (the same
+  // permutation of d for Q and K; it matches the chunk-major K block)
+  const int kg = 8 * g, kc = 32;
 
   if (P.probe == 1) {          // launch + metadata round trip only
     if (ctx == -12345) out[0] = 0;
@@ -223,7 +241,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       blk_lane = tt < nv ? bt_entry(tt) : 0;
     }
     const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, j & 63) * blk_stride + (size_t)hk * BS * D;
-    load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g, kg, kc);
+    load_tile<D, SC1, LM>(t, k_cache + base, v_cache + base, r, g);
   };
   // one 32-key tile: S^T = K Q^T, online softmax down each column, O += P V
   auto step = [&](const Tile<D>& cur, int v) {
@@ -301,7 +319,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
         blk_lane = tt < nv ? bt_entry(tt) : 0;
       }
       const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, jj & 63) * blk_stride + (size_t)hk * BS * D;
-      load_tile<D, SC1>(t, k_cache + base, v_cache + base, r, g, kg, kc);
+      load_tile<D, SC1, LM>(t, k_cache + base, v_cache + base, r, g);
     };
     Tile<D> ta, tb;
     if (v < nv) {

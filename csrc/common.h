@@ -73,6 +73,19 @@ RT_DEVICE float block_max(float v, float* scratch) {
   return wave_max(t);
 }
 
+// ---- paged K cache layout (round 6): every [block][kv head] K block is CHUNK-MAJOR,
+// [D/32][BS keys][32 dims], not [BS keys][D]: the decode attention's MFMA A fragment for 32-dim
+// chunk c (16 keys x 32 dims) is then 8 whole 128-B lines per load instruction instead of 16
+// half lines (profiles/r06/attn_kchunk.md). The tensors keep their [NB, Hkv, BS, D] shape
+// (same bytes per block); every K writer and reader goes through these two helpers.
+RT_DEVICE int kc_elem(int BS, int key, int d) { return (d >> 5) * (BS * 32) + key * 32 + (d & 31); }
+// flat 16-B chunk w of one K block -> (key, 16-B chunk c of that key's D-row)
+RT_DEVICE void kc_chunk(int w, int BS, int& key, int& c) {
+  const int c32 = w / (BS * 4), r = w - c32 * (BS * 4);
+  key = r >> 2;
+  c = c32 * 4 + (r & 3);
+}
+
 // ---- cross-workgroup hand-off I/O (MI355X_MICROARCH "Valid forms": every handed-off byte
 // stored sc1 (write-through past the XCD L2) and loaded sc1 (L1-bypassing), 16 B per lane).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));

@@ -4,7 +4,7 @@
 // q and k are rotated with the Llama rotate-half convention using a host-precomputed
 // fp32 cos|sin table (no on-device trig: cdna_hip_programming App. B "Element-wise"),
 // q is written to its own [T, Hq, D] tensor, k is scattered to the paged key cache
-// (rows contiguous: [blk][h][off][D]) and v to the transposed value cache
+// (chunk-major blocks, [blk][h][D/32][off][32]: common.h kc_elem) and v to the transposed value cache
 // ([blk][h][D][off]) that the MFMA P.V B-operand reads with contiguous loads.
 // One workgroup per token; each thread rotates 4 pairs (8-byte loads from both halves).
 #include "common.h"
@@ -45,14 +45,18 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
       oa[j] = (short)rt::f2bf(x1);
       ob[j] = (short)rt::f2bf(x2);
     }
-    uint16_t* dst;
+    // 4 dims p..p+3 (p % 4 == 0) never cross a 32-dim chunk
+    uint16_t *da, *db;
     if (h < Hq) {
-      dst = q_out + ((size_t)t * Hq + h) * D;
+      da = q_out + ((size_t)t * Hq + h) * D + p;
+      db = da + half;
     } else {
-      dst = k_cache + (((size_t)blk * Hkv + (h - Hq)) * BS + off) * D;
+      uint16_t* kb = k_cache + ((size_t)blk * Hkv + (h - Hq)) * BS * D;
+      da = kb + rt::kc_elem(BS, off, p);
+      db = kb + rt::kc_elem(BS, off, half + p);
     }
-    *reinterpret_cast<rt::short4*>(dst + p) = oa;
-    *reinterpret_cast<rt::short4*>(dst + half + p) = ob;
+    *reinterpret_cast<rt::short4*>(da) = oa;
+    *reinterpret_cast<rt::short4*>(db) = ob;
   }
   // v: Hkv x D elements, transposed store (stride BS)
   const uint16_t* vsrc = row + (size_t)(Hq + Hkv) * D;

@@ -669,7 +669,8 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
         const float y = hi ? fmaf(v, c, partner * sn) : fmaf(v, c, -partner * sn);
         const int d = i + hi * half;
         uint16_t* dst = (h < re.Hq) ? p.out + ((size_t)m * re.Hq + h) * D + d
-                                    : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
+                                    : re.k_cache + ((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS * D +
+                                          rt::kc_elem(re.BS, off, d);
         st16<SC1>(dst, y);
       } else {
         const int hv = h - re.Hq - re.Hkv;
@@ -970,7 +971,8 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
             const float y = hi ? fmaf(v, e_c[t][b], partner * e_s[t][b]) : fmaf(v, e_c[t][b], -partner * e_s[t][b]);
             const int d = i + hi * half;
             uint16_t* dst = (h < re.Hq) ? p.out + ((size_t)row * re.Hq + h) * D + d
-                                        : re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * D + d;
+                                        : re.k_cache + ((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS * D +
+                                              rt::kc_elem(re.BS, off, d);
             st16<false>(dst, y);
           } else {
             const int hv = h - re.Hq - re.Hkv;

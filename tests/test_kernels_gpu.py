@@ -193,7 +193,7 @@ def test_paged_decode_spike():
     q = bf(1, hq, d, seed=4)
     # make key 650 align strongly with every query of kv head 0
     blk, off = 650 // 32, 650 % 32
-    kc[blk, 0, off] = (q[0, :4].float().mean(0) * 8).to(torch.bfloat16)
+    ref.set_k_row(kc, blk, 0, off, (q[0, :4].float().mean(0) * 8).to(torch.bfloat16))
     bt = torch.arange(nb, dtype=torch.int32)[None]
     cl = torch.tensor([L], dtype=torch.int32)
     for splits in (1, 4):

@@ -152,3 +152,20 @@ def test_prefill_split_plan_shapes():
         mine = sorted((tb, te) for s2, r2, tb, te, p in items.tolist() if (s2, r2) == (s, r))
         assert mine[0][0] == 0 and all(a[1] == b[0] for a, b in zip(mine, mine[1:]))
         assert sorted(p for s2, r2, tb, te, p in items.tolist() if (s2, r2) == (s, r)) == list(range(p0, p0 + n))
+
+
+def test_k_cache_blocks_are_chunk_major():
+    """The K cache layout every kernel and the oracle share (csrc/common.h kc_elem): block
+    [blk, head] holds [head_dim/32][block_size][32]; write_k / k_rows / set_k_row index it."""
+    hkv, d = 2, 64
+    kc = torch.zeros(4, hkv, 32, d)
+    k = torch.randn(3, hkv, d)
+    ref.write_k(kc, torch.tensor([1, 1, 3]), torch.tensor([0, 5, 31]), k)
+    rows = ref.k_rows(kc, torch.tensor([1, 3]))
+    assert torch.equal(rows[0], k[0]) and torch.equal(rows[5], k[1]) and torch.equal(rows[32 + 31], k[2])
+    flat = kc.view(-1)
+    for (blk, h, key, dd, want) in [(1, 0, 5, 40, k[1, 0, 40]), (3, 1, 31, 7, k[2, 1, 7]), (1, 1, 0, 63, k[0, 1, 63])]:
+        assert flat[(blk * hkv + h) * 32 * d + (dd // 32) * 32 * 32 + key * 32 + dd % 32] == want
+    r = torch.randn(d)
+    ref.set_k_row(kc, 2, 1, 9, r)
+    assert torch.equal(ref.k_rows(kc, torch.tensor([2]))[9, 1], r)

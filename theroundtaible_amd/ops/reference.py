@@ -3,7 +3,10 @@
 These run on CPU (unit tests, the GPT-2 CPU plumbing config) and are what the HIP
 kernels in ``csrc/`` are tested against. Layouts are the engine's:
 
-* ``k_cache``: ``[num_blocks, n_kv_heads, block_size, head_dim]`` (key rows contiguous)
+* ``k_cache``: allocated ``[num_blocks, n_kv_heads, block_size, head_dim]``, but each
+  ``[block, head]`` block is CHUNK-MAJOR in memory: ``[head_dim/32][block_size][32]`` (round 6,
+  csrc/common.h ``kc_elem``: a decode-attention K load instruction then reads whole 128-B lines).
+  Index it through :func:`k_blocks` / :func:`k_rows` / :func:`write_k`, never as ``[blk, h, off, :]``.
 * ``v_cache``: ``[num_blocks, n_kv_heads, head_dim, block_size]`` (V stored transposed per
   block, so the P.V MFMA B-operand is a contiguous load; see csrc/attention_decode.hip)
 * ``slot = block_id * block_size + offset``
@@ -71,16 +74,40 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional
     bs = k_cache.shape[2]
     slots = slot_mapping.long()
     blk, off = slots // bs, slots % bs
-    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
+    write_k(k_cache, blk, off, k)
     v_cache[blk, :, :, off] = v.to(v_cache.dtype)
     return q.to(qkv.dtype)
+
+
+def k_blocks(k_cache: torch.Tensor) -> torch.Tensor:
+    """The chunk-major view of a K cache: ``[num_blocks, n_kv_heads, head_dim/32, block_size, 32]``."""
+    nb, hkv, bs, d = k_cache.shape
+    return k_cache.view(nb, hkv, d // 32, bs, 32)
+
+
+def k_rows(k_cache: torch.Tensor, blocks: torch.Tensor) -> torch.Tensor:
+    """Key rows of ``blocks`` in order: ``[len(blocks) * block_size, n_kv_heads, head_dim]``."""
+    kb = k_blocks(k_cache)[blocks]                       # [n, Hkv, D/32, BS, 32]
+    n, hkv, c, bs, w = kb.shape
+    return kb.permute(0, 3, 1, 2, 4).reshape(n * bs, hkv, c * w)
+
+
+def write_k(k_cache: torch.Tensor, blk: torch.Tensor, off: torch.Tensor, k: torch.Tensor) -> None:
+    """Store key rows ``k`` ``[T, n_kv_heads, head_dim]`` at (block, offset) pairs."""
+    T, hkv, d = k.shape
+    k_blocks(k_cache)[blk, :, :, off, :] = k.reshape(T, hkv, d // 32, 32).to(k_cache.dtype)
+
+
+def set_k_row(k_cache: torch.Tensor, blk: int, head: int, off: int, row: torch.Tensor) -> None:
+    """Store one key row ``[head_dim]`` of one KV head (tests)."""
+    k_blocks(k_cache)[blk, head, :, off, :] = row.reshape(-1, 32).to(k_cache.dtype)
 
 
 def _gather_kv(k_cache, v_cache, block_table, n):
     bs = k_cache.shape[2]
     nblk = (n + bs - 1) // bs
     blocks = block_table[:nblk].long()
-    k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nblk * bs, k_cache.shape[1], -1)[:n]
+    k = k_rows(k_cache, blocks)[:n]
     v = v_cache[blocks].permute(0, 3, 1, 2).reshape(nblk * bs, v_cache.shape[1], -1)[:n]
     return k.float(), v.float()
 
