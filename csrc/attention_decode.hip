@@ -210,15 +210,15 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   // copy loop (profiles/r05/attn_pingpong_ab.md). RT_ATTN_PP=0 / 1 pins it (A/B).
   static const int pp_env = getenv("RT_ATTN_PP") ? atoi(getenv("RT_ATTN_PP")) : -1;
   const bool pp = pp_env >= 0 ? pp_env != 0 : Hkv >= 4;
-  // K/V load mode (attn_core.h LM_*): nontemporal K and V loads where every K/V byte is read
-  // once per launch — shared-prefix groups (each shared block streamed once for the group) and
-  // a single row. Rows without groups may hold the same blocks (forked prefixes): there the
-  // default policy lets the 2nd..nth reads hit L2 / MALL (private rows over one 22K prefix:
-  // 33.8 us default vs 35.9 nt). With the chunk-major K blocks, tp 1, 3 knights x 22K shared
-  // keys 27.9 -> 25.2 us, 40K 41.2 -> 38.1, B = 1 25K 25.9 -> 23.7 (profiles/r06/attn_kchunk.md).
-  // RT_ATTN_LM pins the mode (0..3, A/B).
-  static const int lm_env = getenv("RT_ATTN_LM") ? atoi(getenv("RT_ATTN_LM")) : -1;
-  const int lm = lm_env >= 0 ? (lm_env & 3) : ((groups != nullptr || B == 1) ? (LM_NTK | LM_NTV) : 0);
+  // K/V load mode (attn_core.h LM_*): nontemporal K and V loads. With the chunk-major K blocks,
+  // tp 1, 3 knights x 22K / 40K shared keys 27.6 -> 25.4 / 41.9 -> 37.8 us; rows with distinct
+  // contexts B = 1 25K 25.9 -> 23.7, B = 3 25K 59.3 -> 55.3, B = 16 2K 31.0 -> 28.6; tp 8 shard even
+  // (profiles/r06/attn_kchunk.md). The one loser: ungrouped rows that read the SAME blocks (3 rows
+  // over one 22K prefix without groups, 33.5 -> 35.4: the 2nd / 3rd reads no longer hit L2 / MALL)
+  // — the engine decodes shared prefixes as groups, so that case does not arise there.
+  // RT_ATTN_LM pins the mode (0 = default policy, 1 = K nt, 2 = V nt, 3 = both; A/B).
+  static const int lm_env = getenv("RT_ATTN_LM") ? atoi(getenv("RT_ATTN_LM")) : (LM_NTK | LM_NTV);
+  const int lm = lm_env & 3;
   args.lm = lm;
 #define RT_PD3(DV, PPV, LMV)                                                                                          \
   do {                                                                                                                \
