@@ -31,6 +31,27 @@ __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
   attn_item<D, false, GM, W, PP, LM>(p, bh, split, sm);
 }
 
+// Per-step work plan: one workgroup per item (sequence b, split) writes the item's key range
+// (item_range, exactly as attn_item derives it) and its block ids. A decode step runs this once;
+// every layer's attention launch then requests an item header and its first block ids together
+// at launch-known addresses — one dependent round trip ahead of the K/V stream instead of two.
+__global__ void __launch_bounds__(256) attn_plan_kernel(AttnArgs p, int G, int GM, int* __restrict__ plan) {
+  const int b = blockIdx.x, split = blockIdx.y;
+  const bool grouped = p.groups != nullptr;
+  const int* gp = grouped ? p.groups + 3 * b : p.ctx_lens + b;
+  const int go = grouped ? 1 : 0;
+  const ItemRange it = item_range(p.ctx_lens[b], gp[0], gp[go], gp[2 * go], grouped, b, split, G, GM, p.num_splits);
+  int* hdr = plan + (size_t)(b * p.num_splits + split) * p.plan_stride;
+  if (threadIdx.x == 0) {
+    hdr[0] = it.b0; hdr[1] = it.n; hdr[2] = it.sh; hdr[3] = it.ctx;
+    hdr[4] = it.sh_b; hdr[5] = it.nsh; hdr[6] = it.pr_b; hdr[7] = it.nv;
+  }
+  const int lim = min(it.nv, p.plan_stride - PLAN_HDR);
+  for (int tt = threadIdx.x; tt < lim; tt += blockDim.x)
+    hdr[PLAN_HDR + tt] = tt < it.nsh ? p.block_tables[(size_t)it.b0 * p.max_blocks + it.sh_b + tt]
+                                     : p.block_tables[(size_t)b * p.max_blocks + it.pr_b + (tt - it.nsh)];
+}
+
 // Split-KV combine as its own launch, for launches with many partial slots per query row
 // (tensor-parallel shards: 1-2 KV heads per rank -> 32-64 splits so the K/V stream still
 // covers the CUs; a table of 3 knights then leaves 3 x 64 = 192 slots per row). The in-launch
@@ -172,7 +193,7 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
-                        hipStream_t stream, int defer_combine, int* deferred) {
+                        hipStream_t stream, int defer_combine, int* deferred, const int* plan, int plan_stride) {
   if (deferred != nullptr) *deferred = 0;
   if (B == 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16) return -1;
@@ -186,6 +207,11 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
                       groups, groups != nullptr ? slot_stride : 0};
   static const int probe = getenv("RT_ATTN_PROBE") ? atoi(getenv("RT_ATTN_PROBE")) : 0;
   args.probe = probe;
+  if (plan != nullptr) {
+    if (plan_stride <= PLAN_HDR) return -5;
+    args.plan = plan;
+    args.plan_stride = plan_stride;
+  }
   // separate combine launch from this many splits on (RT_ATTN_EXT_SPLITS pins it; 0 = never):
   // r03 probes, 3 knights x 40K shared keys: in-launch combine 8.7 us at 16 splits (48 slots),
   // 23 us at 64 (192 slots); whole launch(es), grouped B=3: tp8 shard 32.6 -> 14.9 us (64
@@ -273,4 +299,21 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
 #undef RT_CB
   }
   return 0;
+}
+
+// The per-step plan for launch_paged_decode's ``plan`` (same B, heads, num_splits, groups, block
+// tables and lengths as the launches that read it): plan >= B * num_splits * plan_stride ints.
+int launch_attn_plan(int* plan, int plan_stride, const int* block_tables, const int* ctx_lens, const int* groups,
+                     int B, int Hq, int Hkv, int max_blocks, int num_splits, hipStream_t stream) {
+  if (B == 0) return 0;
+  if (Hq % Hkv || Hq / Hkv > 16 || num_splits < 1 || num_splits > MAXS || plan_stride <= PLAN_HDR) return -1;
+  AttnArgs args{};
+  args.block_tables = block_tables;
+  args.ctx_lens = ctx_lens;
+  args.max_blocks = max_blocks;
+  args.num_splits = num_splits;
+  args.groups = groups;
+  args.plan_stride = plan_stride;
+  hipLaunchKernelGGL(attn_plan_kernel, dim3(B, num_splits), dim3(256), 0, stream, args, Hq / Hkv, 16, plan);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
 }

@@ -115,7 +115,43 @@ struct AttnArgs {
   int xcd = 0;                 // 1: XCD-aware item order (attention_decode.hip), the launch's grid % 8 == 0
   int plain_partials = 0;      // 1 (ext_combine only): partials stay in the writer's L2 (plain stores)
   int lm = 0;                  // K/V load mode actually launched (LM_*), for the host's record
+  // per-step work plan (attn_plan_kernel; nullptr = derive it in every launch): per item
+  // (sequence, split), PLAN_HDR header ints then the item's block ids, plan_stride ints per item
+  const int* plan = nullptr;
+  int plan_stride = 0;
 };
+
+// The key range of work item (sequence b, split) — shared chunk of its group's prefix, then its
+// private split — from the sequence's length and group record. attn_item derives it in every
+// launch unless a per-step plan holds it (attn_plan_kernel, attention_decode.hip: computed once
+// per decode step, read by every layer's launch in the same round trip as the block ids).
+constexpr int PLAN_HDR = 8;
+struct ItemRange {
+  int b0, n, sh, ctx, sh_b, nsh, pr_b, nv;
+};
+
+RT_DEVICE ItemRange item_range(int ctx, int g0, int g1, int g2, bool grouped, int b, int split, int G, int GM,
+                               int num_splits) {
+  ItemRange it;
+  const bool bad = !grouped | (g1 < 1) | (g1 * G > GM) | (g0 < 0) | (b < g0) | (b - g0 >= g1) | (g2 < 0);
+  it.b0 = bad ? b : g0;   // no / malformed group record: run alone
+  it.n = bad ? 1 : g1;
+  it.sh = bad ? 0 : g2;
+  it.ctx = ctx;
+  const int mi = b - it.b0, nslots = it.n * num_splits, slot = mi * num_splits + split;
+  const int ntiles = (ctx + BS - 1) / BS;
+  // this workgroup's shared chunk (all members' columns) then its private split (own columns)
+  const int sh_per = (it.sh + nslots - 1) / nslots;
+  it.sh_b = min(it.sh, slot * sh_per);
+  const int sh_e = min(it.sh, it.sh_b + sh_per);
+  const int npr = max(0, ntiles - it.sh);
+  const int pr_per = (npr + num_splits - 1) / num_splits;
+  it.pr_b = it.sh + min(npr, split * pr_per);
+  const int pr_e = it.sh + min(npr, split * pr_per + pr_per);
+  it.nsh = sh_e - it.sh_b;
+  it.nv = it.nsh + (pr_e - it.pr_b);
+  return it;
+}
 
 // GM = max query columns the LDS is sized for (n * G <= GM). GM = 4 (Llama-3-8B, Mistral-7B,
 // no groups) keeps the workgroup at ~26 KB so two fit a CU: 16 waves streaming K/V per CU.
@@ -164,41 +200,44 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
 
   const int b = bh / Hkv, hk = bh - (bh / Hkv) * Hkv;
   const int G = Hq / Hkv;
-  // the sequence's length and its group record are requested together, before any test on
-  // either (a short-circuit test made the compiler wait for one load before issuing the next:
-  // two extra dependent trips ahead of the K/V stream)
-  // branch-free: without groups the three record loads read ctx_lens[b] (valid, ignored)
-  const bool grouped = P.groups != nullptr;
-  const int* gp = grouped ? P.groups + 3 * b : ctx_lens + b;
-  const int go = grouped ? 1 : 0;
-  const int ctx = ctx_lens[b];
-  const int g0 = gp[0], g1 = gp[go], g2 = gp[2 * go];
-  const bool bad = !grouped | (g1 < 1) | (g1 * G > GM) | (g0 < 0) | (b < g0) | (b - g0 >= g1) | (g2 < 0);
-  const int b0 = bad ? b : g0;   // no / malformed group record: run alone
-  const int n = bad ? 1 : g1;
-  const int sh = bad ? 0 : g2;
-  const int mi = b - b0, ncol = n * G;
-  const int nslots = n * num_splits, slot = mi * num_splits + split;
-  const int stride = P.slot_stride > 0 ? P.slot_stride : num_splits;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int rseq = r / G, rhead = r - (r / G) * G;  // column r -> (member, head within the kv group)
   // reduction-dim order of the QK^T MFMAs: lane group g holds d = 32c + 8g.. of chunk c (the same
   // permutation of d for Q and K; it matches the chunk-major K block)
   const int kg = 8 * g, kc = 32;
+  const bool grouped = P.groups != nullptr;
+  ItemRange ir;
+  // planned: the item's header and this wave's first 64 block ids are requested together, both
+  // at addresses known at launch — one round trip ahead of the first K/V tile instead of two
+  // (sequence record, then block table)
+  const int* plan_ids = nullptr;
+  const int maxt = P.plan_stride - PLAN_HDR;
+  int blk_lane = 0;
+  if (P.plan != nullptr) {
+    const int* hdr = P.plan + (size_t)(b * num_splits + split) * P.plan_stride;
+    plan_ids = hdr + PLAN_HDR;
+    blk_lane = plan_ids[min(wid + W * lane, maxt - 1)];
+    ir = ItemRange{hdr[0], hdr[1], hdr[2], hdr[3], hdr[4], hdr[5], hdr[6], hdr[7]};
+  } else {
+    // the sequence's length and its group record are requested together, before any test on
+    // either (a short-circuit test made the compiler wait for one load before issuing the next:
+    // two extra dependent trips ahead of the K/V stream)
+    // branch-free: without groups the three record loads read ctx_lens[b] (valid, ignored)
+    const int* gp = grouped ? P.groups + 3 * b : ctx_lens + b;
+    const int go = grouped ? 1 : 0;
+    ir = item_range(ctx_lens[b], gp[0], gp[go], gp[2 * go], grouped, b, split, G, GM, num_splits);
+  }
+  const int b0 = ir.b0, n = ir.n, ctx = ir.ctx;
+  const int mi = b - b0, ncol = n * G;
+  const int nslots = n * num_splits, slot = mi * num_splits + split;
+  const int stride = P.slot_stride > 0 ? P.slot_stride : num_splits;
 
   if (P.probe == 1) {          // launch + metadata round trip only
     if (ctx == -12345) out[0] = 0;
     return false;
   }
-  const int ntiles = (ctx + BS - 1) / BS;
-  // this workgroup's shared chunk (all members' columns) then its private split (own columns)
-  const int sh_per = (sh + nslots - 1) / nslots;
-  const int sh_b = min(sh, slot * sh_per), sh_e = min(sh, sh_b + sh_per);
-  const int npr = max(0, ntiles - sh);
-  const int pr_per = (npr + num_splits - 1) / num_splits;
-  const int pr_b = sh + min(npr, split * pr_per), pr_e = sh + min(npr, split * pr_per + pr_per);
-  const int nsh = sh_e - sh_b, nv = nsh + (pr_e - pr_b);
+  const int sh_b = ir.sh_b, pr_b = ir.pr_b, nsh = ir.nsh, nv = ir.nv;
 
   // Q^T fragments: column r = query head hk*G + rhead of member rseq (zero for r >= ncol)
   short8 qf[D / 32];
@@ -233,12 +272,15 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
   // Block ids of this wave's tiles (v = wid + W*j) are fetched one per lane (at j = 0, in flight
   // with Q, and refilled every 64 tiles, i.e. only past ~164K keys at 10 splits) and read out
   // with readlane: no dependent scalar load inside the loop. B=3, ctx 1500: 12.2 -> 11.2 us.
-  int blk_lane = 0;
+  // With a plan the j = 0 ids were requested with the item header (above).
+  auto blk_of = [&](int tt) -> int {
+    return tt < nv ? (plan_ids != nullptr && tt < maxt ? plan_ids[tt] : bt_entry(tt)) : 0;
+  };
   // tile vn = wid + W*j into t (j: the wave's tile index, uniform)
   auto fetch = [&](Tile<D>& t, int vn, int j) {
-    if ((j & 63) == 0) {
+    if ((j & 63) == 0 && !(j == 0 && plan_ids != nullptr && W * 64 <= maxt)) {
       const int tt = vn + W * lane;
-      blk_lane = tt < nv ? bt_entry(tt) : 0;
+      blk_lane = blk_of(tt);
     }
     const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, j & 63) * blk_stride + (size_t)hk * BS * D;
     load_tile<D, SC1, LM>(t, k_cache + base, v_cache + base, r, g);
@@ -316,7 +358,7 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
       const int jj = past ? j - 1 : j;
       if (!past && (j & 63) == 0) {
         const int tt = vn + W * lane;
-        blk_lane = tt < nv ? bt_entry(tt) : 0;
+        blk_lane = blk_of(tt);
       }
       const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, jj & 63) * blk_stride + (size_t)hk * BS * D;
       load_tile<D, SC1, LM>(t, k_cache + base, v_cache + base, r, g);

@@ -18,7 +18,9 @@ void launch_gelu(void* out, const void* x, int64_t n, hipStream_t stream);
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
-                        hipStream_t stream, int defer_combine, int* deferred);
+                        hipStream_t stream, int defer_combine, int* deferred, const int* plan, int plan_stride);
+int launch_attn_plan(int* plan, int plan_stride, const int* block_tables, const int* ctx_lens, const int* groups,
+                     int B, int Hq, int Hkv, int max_blocks, int num_splits, hipStream_t stream);
 int prefill_rows_per_tile(int G, int D);
 int launch_prefill_split(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                          const int* cu_q, const int* start_pos, const int* items, int n_items, const int* cmap,
@@ -168,7 +170,8 @@ void rope_and_cache(torch::Tensor q_out, torch::Tensor qkv, torch::Tensor positi
 int64_t paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
                                torch::Tensor block_tables, torch::Tensor ctx_lens, double scale, int64_t num_splits,
                                torch::Tensor part_o, torch::Tensor part_ml, torch::Tensor counters,
-                               c10::optional<torch::Tensor> groups, int64_t slot_stride, bool defer_combine) {
+                               c10::optional<torch::Tensor> groups, int64_t slot_stride, bool defer_combine,
+                               c10::optional<torch::Tensor> plan, int64_t plan_stride) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 3, "q must be [B, Hq, D]");
@@ -193,15 +196,41 @@ int64_t paged_attention_decode(torch::Tensor out, torch::Tensor q, torch::Tensor
               "split workspace too small");
   check_type(counters, torch::kInt32, "counters");
   TORCH_CHECK(counters.numel() >= B * k_cache.size(1), "split counters too small");
+  const int* pp = nullptr;
+  if (plan.has_value() && plan->defined()) {
+    check_type(*plan, torch::kInt32, "plan");
+    TORCH_CHECK(plan_stride > 8 && plan->numel() >= B * num_splits * plan_stride, "attention plan too small");
+    pp = plan->data_ptr<int>();
+  }
   int deferred = 0;
   const int rc = launch_paged_decode(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                      block_tables.data_ptr<int>(), ctx_lens.data_ptr<int>(), part_o.data_ptr<float>(),
                                      part_ml.data_ptr<float>(), counters.data_ptr<int>(), (int)B, (int)Hq,
                                      (int)k_cache.size(1), (int)D,
                                      (int)block_tables.size(1), (float)scale, (int)num_splits, gp, (int)stride,
-                                     cur_stream(), defer_combine ? 1 : 0, &deferred);
+                                     cur_stream(), defer_combine ? 1 : 0, &deferred, pp, (int)plan_stride);
   TORCH_CHECK(rc == 0, "paged_attention_decode: unsupported configuration (rc=", rc, ")");
   return deferred;
+}
+
+// per-decode-step attention work plan (attention_decode.hip attn_plan_kernel)
+void attn_plan(torch::Tensor plan, int64_t plan_stride, torch::Tensor block_tables, torch::Tensor ctx_lens,
+               c10::optional<torch::Tensor> groups, int64_t B, int64_t Hq, int64_t Hkv, int64_t num_splits) {
+  check_type(plan, torch::kInt32, "plan");
+  check_type(block_tables, torch::kInt32, "block_tables");
+  check_type(ctx_lens, torch::kInt32, "ctx_lens");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && ctx_lens.numel() >= B, "metadata shape");
+  TORCH_CHECK(plan_stride > 8 && plan.numel() >= B * num_splits * plan_stride, "attention plan too small");
+  const int* gp = nullptr;
+  if (groups.has_value() && groups->defined()) {
+    check_type(*groups, torch::kInt32, "groups");
+    TORCH_CHECK(groups->numel() >= 3 * B, "groups must be [B, 3] int32");
+    gp = groups->data_ptr<int>();
+  }
+  const int rc = launch_attn_plan(plan.data_ptr<int>(), (int)plan_stride, block_tables.data_ptr<int>(),
+                                  ctx_lens.data_ptr<int>(), gp, (int)B, (int)Hq, (int)Hkv, (int)block_tables.size(1),
+                                  (int)num_splits, cur_stream());
+  TORCH_CHECK(rc == 0, "attn_plan: unsupported configuration (rc=", rc, ")");
 }
 
 void prefill_attention(torch::Tensor out, torch::Tensor q, torch::Tensor k_cache, torch::Tensor v_cache,
@@ -694,7 +723,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("paged_attention_decode", &paged_attention_decode, py::arg("out"), py::arg("q"), py::arg("k_cache"),
         py::arg("v_cache"), py::arg("block_tables"), py::arg("ctx_lens"), py::arg("scale"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("counters"), py::arg("groups") = py::none(),
-        py::arg("slot_stride") = 0, py::arg("defer_combine") = false);
+        py::arg("slot_stride") = 0, py::arg("defer_combine") = false, py::arg("plan") = py::none(),
+        py::arg("plan_stride") = 0);
+  m.def("attn_plan", &attn_plan, py::arg("plan"), py::arg("plan_stride"), py::arg("block_tables"),
+        py::arg("ctx_lens"), py::arg("groups"), py::arg("B"), py::arg("Hq"), py::arg("Hkv"), py::arg("num_splits"));
   m.def("prefill_rows_per_tile", &prefill_rows_per_tile, py::arg("G"), py::arg("D") = 128);
   m.def("prefill_attention", &prefill_attention);
   m.def("prefill_attention_split", &prefill_attention_split);

@@ -16,7 +16,8 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
 int launch_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                         const int* ctx_lens, float* part_o, float* part_ml, int* counters, int B, int Hq, int Hkv,
                         int D, int max_blocks, float scale, int num_splits, const int* groups, int slot_stride,
-                        hipStream_t stream, int defer_combine, int* deferred);
+                        hipStream_t stream, int defer_combine, int* deferred, const int* plan = nullptr,
+                        int plan_stride = 0);
 int launch_paging_guard(const int* block_tables, const int* ctx_lens, const int64_t* positions, const int64_t* slots,
                         int* err, int B, int max_blocks, int num_blocks, int BS, hipStream_t stream);
 int launch_decode_advance(int64_t* out, int64_t* ids, int64_t* positions, int* ctx_lens, int64_t* step,

@@ -107,6 +107,16 @@ def test_paged_decode(hq, hkv, d, splits):
     out2 = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws)
     assert torch.equal(out, out2)
     assert int(ws.counters.abs().sum()) == 0
+    _check_planned(out, q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws, hq, hkv)
+
+
+def _check_planned(out, q, kc, vc, bt, cl, scale, splits, ws, hq, hkv, groups=None):
+    """The per-step work plan (ops.attn_plan, csrc/attention_decode.hip attn_plan_kernel) must give
+    the same bits as the launch that derives its own ranges (same partials, same merge order)."""
+    assert ops.attn_plan(bt, cl, splits, ws, hq, hkv, groups, q.shape[0])
+    planned = ops.paged_attention_decode(q, kc, vc, bt, cl, scale, splits, ws, groups=groups, planned=True)
+    assert torch.equal(out, planned)
+    assert int(ws.counters.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64), (4, 1, 128)])
@@ -157,6 +167,7 @@ def test_paged_decode_shared_prefix_groups(hq, hkv, d, splits, layout):
     out2 = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws, groups=groups.to(DEV))
     assert torch.equal(out, out2)
     assert int(ws.counters.abs().sum()) == 0
+    _check_planned(out, q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws, hq, hkv, groups.to(DEV))
 
 
 @pytest.mark.parametrize("splits", [1, 2, 5])
@@ -183,6 +194,8 @@ def test_paged_decode_long_context(splits):
     out = ops.paged_attention_decode(q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws)
     exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, cl, scale)
     close(out, exp.to(DEV), 0.02, 0.02)
+    # planned: items longer than the plan row (512 tiles) read the rest from the block tables
+    _check_planned(out, q, kc, vc, bt.to(DEV), cl.to(DEV), scale, splits, ws, hq, hkv)
 
 
 def test_paged_decode_spike():

@@ -44,6 +44,7 @@ class AttnMeta:
     last_rows: Optional[torch.Tensor] = None    # prefill: rows whose logits are needed
     groups: Optional[torch.Tensor] = None       # decode: [B, 3] shared-prefix groups (ops.decode_groups)
     local_logits: bool = False                  # TP decode: return this rank's vocab shard (C3 greedy argmax)
+    planned: bool = False                       # decode: the workspace holds this step's ops.attn_plan
 
 
 class LlamaModel:
@@ -72,7 +73,8 @@ class LlamaModel:
     def attention(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         if meta.kind == "decode":
             return ops.paged_attention_decode(q, kc, vc, meta.block_tables, meta.ctx_lens, self.scale,
-                                              meta.num_splits, meta.workspace, groups=meta.groups)
+                                              meta.num_splits, meta.workspace, groups=meta.groups,
+                                              planned=meta.planned)
         return ops.prefill_attention(q, kc, vc, meta.block_tables, meta.cu_q, meta.start_pos, self.scale,
                                      meta.tile_map, split=meta.prefill_split)
 
@@ -233,6 +235,10 @@ class LlamaModel:
                 hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Returns logits [rows, vocab] (all rows for decode, ``meta.last_rows`` for prefill).
         ``hidden``: optional pre-gathered embedding rows (used by the fused decode path only)."""
+        if meta.kind == "decode":
+            # one attention work plan per decode step, read by all layers' launches
+            meta.planned = ops.attn_plan(meta.block_tables, meta.ctx_lens, meta.num_splits, meta.workspace,
+                                         self.n_heads, self.n_kv_heads, meta.groups, ids.shape[0])
         if meta.kind == "decode" and self.fused_decode_ok(ids):
             if self.tp.size > 1 or self.force_tp_path:
                 return self.forward_decode_fused_tp(ids, positions, kv, meta, hidden)

@@ -98,6 +98,16 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: Optional
 MAX_GROUP_COLS = 16      # MFMA columns a shared-prefix group's query heads may fill (n * G)
 
 
+# attention plan row: 8 header ints + 512 block ids (the 8 waves x 64 lanes of an item's first
+# block-id fetch; an item with more tiles reads the rest from the block tables)
+PLAN_STRIDE = 8 + 512
+
+
+def plan_enabled() -> bool:
+    """Per-step attention plan (``ROUNDTABLE_ATTN_PLAN=0`` turns it off: A/B)."""
+    return os.environ.get("ROUNDTABLE_ATTN_PLAN", "1") != "0"
+
+
 class DecodeWorkspace:
     """Split-KV scratch for paged decode (static: allocated once, reused inside hipGraphs).
 
@@ -119,6 +129,11 @@ class DecodeWorkspace:
         # (tools/experiments: decode_layer.hip, combine_o.hip)
         self.sync = torch.zeros(8, dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        # per-step attention work plan (attn_plan): per item (sequence, split) a header + the
+        # item's block ids; written once per decode step, read by every layer's launch
+        self.plan_stride = PLAN_STRIDE
+        self.plan = torch.empty(max_batch * max_splits * PLAN_STRIDE, dtype=torch.int32, device=device)
+        self.planned = False
 
 
 _CUS: dict = {}
@@ -189,10 +204,12 @@ def decode_groups(group_of: list, shared_blocks: list, G: int) -> Tuple[torch.Te
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, ctx_lens: torch.Tensor, scale: float,
                            num_splits: int = 1, workspace: Optional[DecodeWorkspace] = None,
-                           out: Optional[torch.Tensor] = None, groups: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None, groups: Optional[torch.Tensor] = None,
+                           planned: bool = False) -> torch.Tensor:
     """``groups`` (optional, device ``[B, 3]`` int32 from :func:`decode_groups`): sequences whose
     block tables share leading blocks decode those keys once for the whole group. The result is
-    identical to decoding every sequence alone (the fp32 oracle ignores ``groups``)."""
+    identical to decoding every sequence alone (the fp32 oracle ignores ``groups``).
+    ``planned``: the workspace holds this step's :func:`attn_plan` for exactly these arguments."""
     if _use_native(q):
         if out is None:
             out = torch.empty_like(q)
@@ -203,12 +220,30 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
         if groups is not None and (workspace.max_group < MAX_GROUP_COLS // G or workspace.max_splits < num_splits):
             raise ValueError(f"decode workspace too small for shared-prefix groups (max_group "
                              f"{workspace.max_group} < {MAX_GROUP_COLS // G})")
+        plan = workspace.plan if planned else None
         native().paged_attention_decode(out, q, k_cache, v_cache, block_tables, ctx_lens, scale,
                                         int(num_splits), workspace.partial_o, workspace.partial_ml,
                                         workspace.counters, groups,
-                                        workspace.slot_stride if groups is not None else 0)
+                                        workspace.slot_stride if groups is not None else 0, False,
+                                        plan, workspace.plan_stride if planned else 0)
         return out
     return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+
+
+def attn_plan(block_tables: torch.Tensor, ctx_lens: torch.Tensor, num_splits: int, workspace: DecodeWorkspace,
+              n_heads: int, n_kv_heads: int, groups: Optional[torch.Tensor] = None, batch: Optional[int] = None) -> bool:
+    """Write the per-step decode-attention work plan into ``workspace`` (csrc/attention_decode.hip
+    attn_plan_kernel): every layer's :func:`paged_attention_decode` of this step (same block tables,
+    lengths, groups, splits) then passes ``planned=True`` and starts its K/V stream one dependent
+    round trip earlier. Returns whether a plan was written (GPU + native + enabled)."""
+    if workspace is None or not block_tables.is_cuda or not native_available() or not plan_enabled():
+        return False
+    B = int(batch if batch is not None else ctx_lens.numel())
+    if B * num_splits * workspace.plan_stride > workspace.plan.numel():
+        return False
+    native().attn_plan(workspace.plan, workspace.plan_stride, block_tables, ctx_lens, groups, B, int(n_heads),
+                       int(n_kv_heads), int(num_splits))
+    return True
 
 
 def prefill_tile_map(cu_q: torch.Tensor, rows_per_tile: int, start_pos=None) -> torch.Tensor:

@@ -185,8 +185,10 @@ def bench_attn(B, ctx, splits_list):
     for splits in splits_list:
         ws = ops.DecodeWorkspace(B, hq, d, splits, DEV)
         out = torch.empty_like(q)
-        fn = lambda i, ws=ws, splits=splits, out=out: ops.paged_attention_decode(
-            q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out)
+        # the per-step work plan (as a decode step computes it once for all layers)
+        pl = ops.attn_plan(bt, cl, splits, ws, hq, hkv, None, B)
+        fn = lambda i, ws=ws, splits=splits, out=out, pl=pl: ops.paged_attention_decode(
+            q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out, planned=pl)
         row(f"decode attn B={B} ctx={ctx} splits={splits}", timed(fn), nbytes)
 
 
@@ -214,8 +216,10 @@ def bench_attn_grouped(B, shared, private, splits_list, hq=32, hkv=8):
             ws = ops.DecodeWorkspace(B, hq, d, splits, DEV, max_group=16 // G if grouped else 1)
             out = torch.empty_like(q)
             gt = groups if grouped else None
-            fn = lambda i, ws=ws, splits=splits, out=out, gt=gt: ops.paged_attention_decode(
-                q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out, groups=gt)
+            pl = ops.attn_plan(bt, cl, splits, ws, hq, hkv, gt, B)
+            fn = lambda i, ws=ws, splits=splits, out=out, gt=gt, pl=pl: ops.paged_attention_decode(
+                q, caches[i % copies][0], caches[i % copies][1], bt, cl, 1 / math.sqrt(d), splits, ws, out, groups=gt,
+                planned=pl)
             row(f"decode attn {'grouped' if grouped else 'private'} hq={hq} hkv={hkv} B={B} shared={shared} "
                 f"own={private} splits={splits}",
                 timed(fn), nbytes if grouped else nbytes + (B - 1) * nsh * 32 * hkv * d * 4)
