@@ -267,3 +267,28 @@ def test_sixty_four_concurrent_clients_all_served(server):
         t.join()
     assert not errs and codes == [200] * n, (errs[:3], len(codes))
     assert server.httpd.request_queue_size >= 128
+
+
+def test_stream_client_disconnect_cancels_the_request(server):
+    """A streaming client that goes away mid-stream must not keep the engine decoding for nobody:
+    the request is cancelled at the next decode chunk and releases its KV."""
+    import http.client
+    from urllib.parse import urlparse
+    u = urlparse(server.url)
+    before = dict(server.sched.stats)
+    conn = http.client.HTTPConnection(u.hostname, u.port, timeout=60)
+    body = {"prompt": "Een lange monoloog:", "max_tokens": 3000, "ignore_eos": True, "temperature": 0, "stream": True}
+    conn.request("POST", "/v1/completions", body=json.dumps(body), headers={"Content-Type": "application/json"})
+    resp = conn.getresponse()
+    assert resp.status == 200
+    line = b""
+    while not line.startswith(b"data: {"):
+        line = resp.fp.readline()
+    conn.sock.shutdown(2)          # the client disappears
+    conn.close()
+    deadline = time.time() + 120
+    while server.sched.stats["requests"] == before["requests"] and time.time() < deadline:
+        time.sleep(0.2)
+    assert server.sched.stats["requests"] == before["requests"] + 1
+    got = server.sched.stats["completion_tokens"] - before["completion_tokens"]
+    assert got < 3000, got

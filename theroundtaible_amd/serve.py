@@ -94,6 +94,7 @@ class _Request:
     # streaming: the scheduler puts the generated ids so far after every host readback (the first
     # token after prefill, then every decode chunk), then None when the request is complete
     stream_q: Optional["queue.Queue"] = None
+    cancelled: bool = False        # the streaming client went away: stop decoding it
 
     def publish(self, gen: List[int]) -> None:
         if self.stream_q is not None:
@@ -166,6 +167,8 @@ class Scheduler:
 
     # ---- completion ---------------------------------------------------------------------------
     def _finished(self, a: _Active) -> bool:
+        if a.req.cancelled:
+            return True
         stops = self.engine.tokenizer.stop_ids
         return len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos
                                                               and not stops.isdisjoint(a.gen))
@@ -438,6 +441,15 @@ class RoundtableServer:
 
                 def emit(obj) -> None:
                     self._chunk((f"data: {json.dumps(obj)}\n\n" if sse else json.dumps(obj) + "\n").encode())
+                try:
+                    self._stream_body(r, emit, first, delta, last, sse)
+                except (BrokenPipeError, ConnectionResetError):
+                    # the client went away mid-stream: its request stops decoding at the next chunk
+                    # (and releases its KV) instead of running to max_tokens for nobody
+                    r.cancelled = True
+                    self.close_connection = True
+
+            def _stream_body(self, r, emit, first, delta, last, sse: bool) -> None:
                 if first is not None:
                     emit(first)
                 sent = ""
