@@ -243,7 +243,7 @@ def test_strong_prediction_matches_cost_model_table():
     """bench.py's per-run prediction (detail.prediction) is the tools/tp_cost.py curve: the
     simulated rank-0 compute of that tp + 2L K9 calls and one gather per step + prefill rings."""
     from theroundtaible_amd.parallel.costmodel import load_simulated, strong_round_ms
-    for n, want in ((2, 1301), (4, 967), (8, 839)):       # profiles/r05/tp_cost_model.md, K9 5 us
+    for n, want in ((2, 1270), (4, 949), (8, 814)):       # profiles/r06/tp_cost_model.md, K9 5 us
         sim = load_simulated(n)
         assert sim is not None and sim["config"]["tp"] == n
         assert abs(strong_round_ms(sim, n, 5.0, 9.5) - want) < 1.0
