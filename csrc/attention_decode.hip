@@ -261,12 +261,10 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
     else RT_PD3(DV, PPV, 3);                        \
   } while (0)
 #define RT_PD(DV) do { if (pp) RT_PD2(DV, true); else RT_PD2(DV, false); } while (0)
-  // A/B knob (round 6): 16-wave workgroups for grouped launches (half the splits give the same
-  // waves; half the partial slots for the combine). RT_ATTN_W16=1; default-path variant only.
-  static const bool w16 = getenv("RT_ATTN_W16") && atoi(getenv("RT_ATTN_W16")) == 1;
-  if (w16 && groups != nullptr && D == 128 && pp && lm == 3)
-    hipLaunchKernelGGL((paged_decode_kernel<128, 16, 16, true, 3>), grid, dim3(16 * 64), 0, stream, args);
-  else if (D == 128) RT_PD(128);
+  // (16-wave grouped workgroups were measured and rejected: __launch_bounds__(1024) caps the item
+  // at 128 VGPRs, it spills, and half the CUs stream — 22K shared keys 25.0 -> 41.6 us at 6 splits,
+  // profiles/r06/attn_kchunk.md)
+  if (D == 128) RT_PD(128);
   else if (D == 64) RT_PD(64);
   else return -2;
 #undef RT_PD
