@@ -2,6 +2,7 @@
 import json
 import threading
 import time
+import urllib.error
 import urllib.request
 
 import pytest
@@ -292,3 +293,32 @@ def test_stream_client_disconnect_cancels_the_request(server):
     assert server.sched.stats["requests"] == before["requests"] + 1
     got = server.sched.stats["completion_tokens"] - before["completion_tokens"]
     assert got < 3000, got
+
+
+def test_stop_strings_cut_the_reply(server):
+    """OpenAI ``stop`` (string or list) / Ollama ``options.stop``: the reply ends before the earliest
+    stop string, finish_reason "stop", decoding ends at the next chunk; streamed pieces never show
+    a stop string and concatenate to the same text."""
+    from theroundtaible_amd.serve import cut_at_stop_strings, stop_prefix_hold
+    assert cut_at_stop_strings("abc STOP def", ["STOP", "de"]) == ("abc ", True)
+    assert cut_at_stop_strings("abc", ["x"]) == ("abc", False)
+    assert stop_prefix_hold("hello ST", ["STOP"]) == 2 and stop_prefix_hold("hello", ["STOP"]) == 0
+    body = {"prompt": "Stop-test:", "max_tokens": 48, "temperature": 0, "ignore_eos": True}
+    full = json.loads(_post(server.url + "/v1/completions", body)[1])["choices"][0]["text"]
+    assert len(full) > 20
+    stop = full[len(full) // 2:len(full) // 2 + 3]
+    want = full[:full.find(stop)]
+    d = json.loads(_post(server.url + "/v1/completions", dict(body, stop=[stop]))[1])
+    assert d["choices"][0]["text"] == want and d["choices"][0]["finish_reason"] == "stop"
+    d = json.loads(_post(server.url + "/v1/completions", dict(body, stop=stop))[1])
+    assert d["choices"][0]["text"] == want
+    events, _ = _stream_events(server.url + "/v1/completions", dict(body, stop=[stop], stream=True))
+    pieces = [e["choices"][0]["text"] for e in events[:-1]]
+    assert "".join(pieces) == want and all(stop not in p for p in pieces)
+    assert events[-2]["choices"][0]["finish_reason"] == "stop"
+    code, msg = 0, ""
+    try:
+        _post(server.url + "/v1/completions", dict(body, stop=[1, 2]))
+    except urllib.error.HTTPError as e:
+        code = e.code
+    assert code == 400

@@ -64,6 +64,39 @@ def render_chat(messages: List[Dict[str, Any]]) -> str:
     return "".join(s.text for s in chat_segments(messages)[0])
 
 
+def cut_at_stop_strings(text: str, stops) -> Tuple[str, bool]:
+    """``text`` up to the earliest occurrence of any stop string (OpenAI ``stop``: the stop string
+    itself is not returned), and whether one occurred."""
+    cut = -1
+    for st in stops:
+        i = text.find(st) if st else -1
+        if i >= 0 and (cut < 0 or i < cut):
+            cut = i
+    return (text[:cut], True) if cut >= 0 else (text, False)
+
+
+def stop_prefix_hold(text: str, stops) -> int:
+    """Characters at the end of ``text`` that may still grow into a stop string (a streamed piece
+    holds them back until the next piece decides)."""
+    hold = 0
+    for st in stops:
+        for k in range(min(len(st) - 1, len(text)), hold, -1):
+            if text.endswith(st[:k]):
+                hold = k
+                break
+    return hold
+
+
+def parse_stops(v) -> Tuple[str, ...]:
+    if v is None:
+        return ()
+    if isinstance(v, str):
+        v = [v]
+    if not isinstance(v, list) or not all(isinstance(x, str) for x in v) or len(v) > 16:
+        raise ValueError("'stop' must be a string or a list of at most 16 strings")
+    return tuple(x for x in v if x)
+
+
 def chat_segments(messages: List[Dict[str, Any]]):
     """The :func:`render_chat` transcript as prompt segments, plus how many leading segments
     are the conversation's system message(s) — the part many clients send identically."""
@@ -95,6 +128,7 @@ class _Request:
     # token after prefill, then every decode chunk), then None when the request is complete
     stream_q: Optional["queue.Queue"] = None
     cancelled: bool = False        # the streaming client went away: stop decoding it
+    stops: Tuple[str, ...] = ()    # OpenAI "stop" / Ollama options.stop strings
 
     def publish(self, gen: List[int]) -> None:
         if self.stream_q is not None:
@@ -170,8 +204,10 @@ class Scheduler:
         if a.req.cancelled:
             return True
         stops = self.engine.tokenizer.stop_ids
-        return len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos
-                                                              and not stops.isdisjoint(a.gen))
+        if len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos and not stops.isdisjoint(a.gen)):
+            return True
+        # stop strings: checked on the decoded text after every decode chunk
+        return bool(a.req.stops) and cut_at_stop_strings(self.engine.tokenizer.decode(a.gen), a.req.stops)[1]
 
     def _complete(self, a: _Active, error: Optional[BaseException] = None) -> None:
         r = a.req
@@ -184,7 +220,11 @@ class Scheduler:
             if not a.req.params.ignore_eos:
                 gen = cut_at_stop(gen, self.engine.tokenizer.stop_ids)
             m = dict(a.metrics, decode_tokens=len(gen), turn_ms=(time.perf_counter() - a.t0) * 1e3)
-            r.result = _Output(self.engine.tokenizer.decode(gen), gen, m)
+            text = self.engine.tokenizer.decode(gen)
+            if r.stops:
+                text, hit = cut_at_stop_strings(text, r.stops)
+                m["stop_string"] = hit
+            r.result = _Output(text, gen, m)
             with self._lock:
                 self.stats["requests"] += 1
                 self.stats["prompt_tokens"] += int(m.get("prompt_tokens", 0))
@@ -462,7 +502,7 @@ class RoundtableServer:
                         break
                     if ids is None:
                         break
-                    text = server.visible_text(ids, r.params)
+                    text = server.visible_text(ids, r.params, r.stops)
                     if text.startswith(sent) and len(text) > len(sent):
                         emit(delta(text[len(sent):]))
                         sent = text
@@ -573,7 +613,7 @@ class RoundtableServer:
                 opts = body.get("options") or {}
                 params = {"temperature": opts.get("temperature"), "top_p": opts.get("top_p"),
                           "top_k": opts.get("top_k"), "seed": opts.get("seed"),
-                          "max_tokens": opts.get("num_predict")}
+                          "max_tokens": opts.get("num_predict"), "stop": opts.get("stop")}
                 if body.get("stream"):
                     # Ollama's NDJSON stream: one message object per line, then a done record
                     # (a request without "stream" keeps the one-object reply of rounds 1-5)
@@ -639,17 +679,24 @@ class RoundtableServer:
     def submit(self, prompt, body: Dict[str, Any], session: Optional[str], stream: bool = False) -> _Request:
         params = self.sampling(body)
         key = f"session:{session}" if session else f"anon:{next(self._anon)}"
+        stops = parse_stops(body.get("stop"))
         return self.sched.submit(_Request(key, prompt, params, persistent=bool(session),
-                                          stream_q=queue.Queue() if stream else None))
+                                          stream_q=queue.Queue() if stream else None, stops=stops))
 
-    def visible_text(self, ids: List[int], params: SamplingParams) -> str:
+    def visible_text(self, ids: List[int], params: SamplingParams, stops=()) -> str:
         """The text of ``ids`` so far as the final result will show it (cut at max_new_tokens and at
-        a stop id, decoded), minus a trailing incomplete UTF-8 character (a byte-level BPE token
-        can end mid-character: held back until the next piece completes it)."""
+        a stop id, decoded, cut at a stop string), minus a trailing incomplete UTF-8 character (a
+        byte-level BPE token can end mid-character) and minus a tail that may still become a stop
+        string: both are held back until the next piece decides."""
         gen = ids[:params.max_new_tokens]
         if not params.ignore_eos:
             gen = cut_at_stop(gen, self.engine.tokenizer.stop_ids)
-        return self.engine.tokenizer.decode(gen).rstrip("\ufffd")
+        text = self.engine.tokenizer.decode(gen).rstrip("\ufffd")
+        if stops:
+            text, hit = cut_at_stop_strings(text, stops)
+            if not hit:
+                text = text[:len(text) - stop_prefix_hold(text, stops)]
+        return text
 
     def generate(self, prompt: str, body: Dict[str, Any], session: Optional[str]) -> Tuple[Any, _Request]:
         r = self.submit(prompt, body, session)
@@ -661,6 +708,8 @@ class RoundtableServer:
 
     @staticmethod
     def finish(out, r: _Request) -> str:
+        if out.metrics.get("stop_string"):
+            return "stop"
         return "length" if len(out.ids) >= r.params.max_new_tokens else "stop"
 
     @staticmethod
