@@ -226,6 +226,10 @@ def test_streaming_emits_chunks_during_decode(server):
     assert "".join(pieces) == want
     assert events[0]["choices"][0]["delta"]["role"] == "assistant"
     assert events[-2]["choices"][0]["finish_reason"] == "length"
+    assert "usage" not in events[-2]
+    ev_u, _ = _stream_events(server.url + "/v1/chat/completions",
+                             dict(body, stream=True, stream_options={"include_usage": True}))
+    assert ev_u[-2]["usage"]["completion_tokens"] == 64
     # the text arrives while decoding: the first content chunk well before the end of the stream
     first = next(i for i, c in enumerate(content) if c)
     assert times[first] < times[-1]

@@ -572,10 +572,17 @@ class RoundtableServer:
 
                     def piece(delta, finish=None):
                         return dict(base, choices=[{"index": 0, "delta": delta, "finish_reason": finish}])
+                    include_usage = bool((body.get("stream_options") or {}).get("include_usage"))
+
+                    def last(out, r):
+                        # OpenAI stream_options.include_usage: the finishing chunk carries the usage
+                        end = piece({}, server.finish(out, r))
+                        if include_usage:
+                            end["usage"] = server.usage(out)
+                        return end
                     self._stream(server.chat_prompt(msgs), body, body.get("user") or body.get("session"),
                                  first=piece({"role": "assistant", "content": ""}),
-                                 delta=lambda t: piece({"content": t}),
-                                 last=lambda out, r: piece({}, server.finish(out, r)))
+                                 delta=lambda t: piece({"content": t}), last=last)
                     return
                 out, r = server.generate(server.chat_prompt(msgs), body, body.get("user") or body.get("session"))
                 usage = server.usage(out)
