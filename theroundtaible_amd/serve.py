@@ -143,6 +143,7 @@ class _Active:
     gen: List[int]
     metrics: Dict[str, Any]
     t0: float
+    checked: int = 0     # tokens of gen already scanned for stop strings
 
 
 class Scheduler:
@@ -206,8 +207,14 @@ class Scheduler:
         stops = self.engine.tokenizer.stop_ids
         if len(a.gen) >= a.req.params.max_new_tokens or (not a.req.params.ignore_eos and not stops.isdisjoint(a.gen)):
             return True
-        # stop strings: checked on the decoded text after every decode chunk
-        return bool(a.req.stops) and cut_at_stop_strings(self.engine.tokenizer.decode(a.gen), a.req.stops)[1]
+        # stop strings: checked after every decode chunk on the decoded TAIL only (the tokens since
+        # the last check plus enough earlier ones to hold the longest stop string), so a long reply
+        # costs O(n) decoding, not O(n^2)
+        if not a.req.stops:
+            return False
+        k = (len(a.gen) - a.checked) + max(len(st) for st in a.req.stops) + 8
+        a.checked = len(a.gen)
+        return cut_at_stop_strings(self.engine.tokenizer.decode(a.gen[-k:]), a.req.stops)[1]
 
     def _complete(self, a: _Active, error: Optional[BaseException] = None) -> None:
         r = a.req
