@@ -37,11 +37,12 @@ def post(url, body, timeout=900):
 
 
 def post_stream(url, body, timeout=900):
-    """Stream a chat completion: (seconds to the first content chunk, usage-like dict)."""
-    req = urllib.request.Request(url, data=json.dumps(dict(body, stream=True)).encode(), method="POST",
-                                 headers={"Content-Type": "application/json"})
+    """Stream a chat completion: (seconds to the first content chunk, content chunks, the usage the
+    server reports with ``stream_options.include_usage``)."""
+    req = urllib.request.Request(url, data=json.dumps(dict(body, stream=True, stream_options={"include_usage": True}))
+                                 .encode(), method="POST", headers={"Content-Type": "application/json"})
     t0 = time.perf_counter()
-    ttfc, n_chunks, done = None, 0, False
+    ttfc, n_chunks, done, usage = None, 0, False, None
     with urllib.request.urlopen(req, timeout=timeout) as r:
         for raw in r:
             line = raw.decode().strip()
@@ -53,13 +54,14 @@ def post_stream(url, body, timeout=900):
             ev = json.loads(line[6:])
             if "error" in ev:
                 raise RuntimeError(ev["error"].get("message"))
+            usage = ev.get("usage") or usage
             if ev["choices"][0]["delta"].get("content"):
                 n_chunks += 1
                 if ttfc is None:
                     ttfc = time.perf_counter() - t0
     if not done:
         raise RuntimeError("stream ended without [DONE]")
-    return ttfc, n_chunks
+    return ttfc, n_chunks, usage
 
 
 def main() -> int:
@@ -88,9 +90,9 @@ def main() -> int:
                 "max_tokens": a.max_tokens, "ignore_eos": True, "temperature": 0.7, "top_p": 0.95}
         t0 = time.perf_counter()
         if a.stream:
-            ttfc, n_chunks = post_stream(url, body)
-            return time.perf_counter() - t0, {"completion_tokens": a.max_tokens, "prompt_tokens": 0,
-                                              "ttfc": ttfc, "chunks": n_chunks}
+            ttfc, n_chunks, u = post_stream(url, body)
+            return time.perf_counter() - t0, dict(u or {"completion_tokens": 0, "prompt_tokens": 0},
+                                                  ttfc=ttfc, chunks=n_chunks)
         d = post(url, body)
         return time.perf_counter() - t0, d["usage"]
 
