@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(1024) decode_combine_kernel(AttnArgs p) {
   const int stride = p.slot_stride > 0 ? p.slot_stride : p.num_splits;
   // the host's sizing: every split of every member of the largest group (slots past the row's
   // own count are inside the row's stride and loaded, never merged)
-  const int nmax = p.comb_slots;   // the host's bound on a row's slots (launch_paged_decode)
+  const int nmax = p.groups != nullptr ? min(stride, (16 / G) * p.num_splits) : p.num_splits;
   const float* __restrict__ po = p.part_o + (size_t)row * stride * D;
   const float* __restrict__ pml = p.part_ml + (size_t)row * stride * 4;
   // the group record and the first chunk's partials are independent: both requests go out
@@ -275,11 +275,7 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
     if (deferred != nullptr) *deferred = 1;
   } else if (args.ext_combine && !skip_combine) {
     // slots per row: every split of every member of the largest group (groups: n * G <= 16)
-    // a group has at most min(B, 16 / G) members (B = 1, sequential rounds: 32 slots, not 128;
-    // the 3-knight table: 30, not 40). RT_COMBINE_FULL_BOUND=1: round 5's (16 / G) bound (A/B)
-    static const bool full_bound = getenv("RT_COMBINE_FULL_BOUND") && atoi(getenv("RT_COMBINE_FULL_BOUND")) == 1;
-    const int nmax = groups != nullptr ? min(slot_stride, min(full_bound ? 16 : B, 16 / G) * num_splits) : num_splits;
-    args.comb_slots = nmax;
+    const int nmax = groups != nullptr ? min(slot_stride, (16 / G) * num_splits) : num_splits;
     // slot-lanes (x 8 dim-lanes) per workgroup, capped at 32 (RT_COMBINE_NSL): fewer, wider lanes
     // (8 slots each for a tp 8 table's 256-slot bound) beat 128 lanes x 2 — 4 waves to dispatch
     // and merge instead of 16; tp 8 grouped attention + combine 12.4 -> 11.6 us

@@ -119,7 +119,6 @@ struct AttnArgs {
   // (sequence, split), PLAN_HDR header ints then the item's block ids, plan_stride ints per item
   const int* plan = nullptr;
   int plan_stride = 0;
-  int comb_slots = 0;          // decode_combine_kernel: slots loaded per row (>= every row's n * num_splits)
 };
 
 // The key range of work item (sequence b, split) — shared chunk of its group's prefix, then its
