@@ -101,12 +101,20 @@ class DistributedPool:
             del self.events[:1024], self.event_ns[:1024]
 
     def _store(self):
-        """The launcher's key-value store, fetched once per pool: torch exposes the default
-        group's store only through ``_get_default_store`` (stable since torch 1.x); the pool
-        keeps the handle instead of asking every turn."""
+        """A key-value store every rank of the launch shares, opened once per pool. Under torchrun
+        (the SPMD commands' launcher) that is a client of the elastic agent's TCP store at
+        MASTER_ADDR:MASTER_PORT — the same store torch's env:// rendezvous joined — under a prefix of
+        our own; a process group initialised any other way falls back to the default group's store
+        (``_get_default_store``, private API)."""
         if getattr(self, "_kv_store", None) is None:
+            import datetime
             import torch.distributed as dist
-            self._kv_store = dist.distributed_c10d._get_default_store()
+            if os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true" and os.environ.get("MASTER_PORT"):
+                client = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
+                                       is_master=False, timeout=datetime.timedelta(seconds=300))
+                self._kv_store = dist.PrefixStore("roundtable/", client)
+            else:
+                self._kv_store = dist.distributed_c10d._get_default_store()
         return self._kv_store
 
     def _rendezvous(self, ranks: tuple, wait_s: float) -> bool:
