@@ -16,9 +16,18 @@ using namespace attn;
 // different placement changes only speed.
 RT_DEVICE int xcd_item(int lin, int nwg) { return (lin & 7) * (nwg >> 3) + (lin >> 3); }
 
+// the LDS-DMA staged form (LM_GLDS) puts each wave's K/V slice over the merge buffers
+template <int D, int GM, int W, int LM>
+union DecodeSmem {
+  AttnSmem<D, GM, W> m;
+  short8 stage[(LM & LM_GLDS) ? W * tile_words<D>() * 64 : 1];
+};
+
 template <int D, int GM, int W = NW, bool PP = true, int LM = 0>
 __global__ void __launch_bounds__(W * 64) paged_decode_kernel(AttnArgs p) {
-  __shared__ AttnSmem<D, GM, W> sm;
+  static_assert(sizeof(DecodeSmem<D, GM, W, LM>) <= 160 * 1024, "LDS of one CU");
+  __shared__ DecodeSmem<D, GM, W, LM> sm_;
+  auto& sm = sm_.m;
   int bh = blockIdx.x, split = blockIdx.y;
   if (p.xcd) {
     const int ns = gridDim.y, nb = gridDim.x / p.Hkv;
@@ -242,9 +251,10 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
   // (profiles/r06/attn_kchunk.md). The one loser: ungrouped rows that read the SAME blocks (3 rows
   // over one 22K prefix without groups, 33.5 -> 35.4: the 2nd / 3rd reads no longer hit L2 / MALL)
   // — the engine decodes shared prefixes as groups, so that case does not arise there.
-  // RT_ATTN_LM pins the mode (0 = default policy, 1 = K nt, 2 = V nt, 3 = both; A/B).
+  // RT_ATTN_LM pins the mode (0 = default policy, 1 = K nt, 2 = V nt, 3 = both; A/B; 7 = both
+  // through the LDS-DMA staged loop, ping-pong form only).
   static const int lm_env = getenv("RT_ATTN_LM") ? atoi(getenv("RT_ATTN_LM")) : (LM_NTK | LM_NTV);
-  const int lm = lm_env & 3;
+  const int lm = (lm_env & LM_GLDS) && pp ? 7 : lm_env & 3;
   args.lm = lm;
 #define RT_PD3(DV, PPV, LMV)                                                                                          \
   do {                                                                                                                \
@@ -258,7 +268,8 @@ int launch_paged_decode(void* out, const void* q, const void* k_cache, const voi
     if (lm == 0) RT_PD3(DV, PPV, 0);                \
     else if (lm == 1) RT_PD3(DV, PPV, 1);           \
     else if (lm == 2) RT_PD3(DV, PPV, 2);           \
-    else RT_PD3(DV, PPV, 3);                        \
+    else if (lm == 3 || !PPV) RT_PD3(DV, PPV, 3);   \
+    else RT_PD3(DV, PPV, 7);                        \
   } while (0)
 #define RT_PD(DV) do { if (pp) RT_PD2(DV, true); else RT_PD2(DV, false); } while (0)
   // (16-wave grouped workgroups were measured and rejected: __launch_bounds__(1024) caps the item

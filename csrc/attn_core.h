@@ -54,6 +54,19 @@ struct Tile {
 // V tiles (LM_NTV). Right where every K/V byte is read once per launch (grouped launches, one row).
 constexpr int LM_NTK = 1;
 constexpr int LM_NTV = 2;
+// LM_GLDS (A/B of VERDICT r5 #1b, RT_ATTN_LM=7): each wave stages its next K/V tile in a private
+// 16-KB LDS slice by LDS-DMA (global_load_lds_dwordx4, lane-linear: lane l's 16 B of load i land
+// at slice[i][l] and the same lane reads them back with ds_read_b128, so no swizzle and no bank
+// conflict), then reads it into ONE register tile: 64 VGPRs less than the ping-pong pair, the
+// same one tile in flight per wave during the math. The slices alias the merge buffers (a drain
+// and a workgroup barrier separate the two uses).
+constexpr int LM_GLDS = 4;
+
+template <int D>
+constexpr int tile_words() { return 2 * (D / 32) + D / 16; }   // 16-B loads per lane per tile
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
 
 template <bool NT>
 RT_DEVICE short8 ld16(const uint16_t* p) {
@@ -345,7 +358,57 @@ RT_DEVICE bool attn_item(const AttnArgs& P, int bh, int split, AttnSmem<D, GM, W
                                                         __builtin_bit_cast(bf16x8, cur.v[e]), o, 0, 0, 0);
     }
   };
-  if constexpr (PP) {
+  if constexpr ((LM & LM_GLDS) != 0 && !SC1) {
+    short8* stg = reinterpret_cast<short8*>(&S) + (size_t)wid * tile_words<D>() * 64;
+    const int krow = 8 * (r >> 2) + (r & 3);
+    // tile vn (or, past the end, the wave's last tile again) -> the wave's LDS slice
+    auto stage = [&](int vn, int j) {
+      const bool past = vn >= nv;
+      const int jj = past ? j - 1 : j;
+      if (!past && (j & 63) == 0 && !(j == 0 && plan_ids != nullptr && W * 64 <= maxt)) blk_lane = blk_of(vn + W * lane);
+      const size_t base = (size_t)__builtin_amdgcn_readlane(blk_lane, jj & 63) * blk_stride + (size_t)hk * BS * D;
+      const uint16_t* kb = k_cache + base;
+      const uint16_t* vb = v_cache + base;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // WAR: the slice's previous ds_reads are done
+      int i = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c, ++i)
+          __builtin_amdgcn_global_load_lds((glb_void*)(kb + c * (BS * 32) + (krow + 4 * h) * 32 + 8 * g),
+                                           (lds_void*)(stg + i * 64), 16, 0, (LM & LM_NTK) ? 2 : 0);
+#pragma unroll
+      for (int e = 0; e < D / 16; ++e, ++i)
+        __builtin_amdgcn_global_load_lds((glb_void*)(vb + (16 * e + r) * BS + 8 * g), (lds_void*)(stg + i * 64), 16, 0,
+                                         (LM & LM_NTV) ? 2 : 0);
+    };
+    auto unstage = [&](Tile<D>& t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the slice's LDS-DMA has landed
+      int i = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c, ++i) t.k[h][c] = stg[i * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < D / 16; ++e, ++i) t.v[e] = stg[i * 64 + lane];
+    };
+    Tile<D> t;
+    if (v < nv) {
+      stage(v, 0);
+      int j = 1;
+      while (true) {
+        unstage(t);
+        stage(v + W, j);        // unconditional (past the end: the same tile again), as PP
+        step(t, v);
+        v += W;
+        ++j;
+        if (v >= nv) break;
+      }
+    }
+    // every wave's LDS-DMA drained before any wave writes the merge buffers over the slices
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else if constexpr (PP) {
     // Ping-pong over two named tiles, no `cur = nxt` copy, and the prefetch UNCONDITIONAL: with
     // the copy (and with a prefetch skipped past the range end) the compiler's wait counts had to
     // hold on every path, so each iteration waited for the NEXT tile's loads (vmcnt 15..0 before
