@@ -7,8 +7,9 @@
 // Grid (n_tiles, Hkv): a workgroup = one tile of query rows (host work list
 // `tile_map` = (sequence, first row)) x one kv head; its 4 waves cover the G query
 // heads of that kv head (GQA: one K/V tile load feeds all G heads):
-//   G<=4: wave w -> head w%G, 16-row group w/G  (tile = 16*4/G rows)
-//   G> 4: every wave 16 rows x G/4 heads        (tile = 16 rows)
+//   G<=4: wave w -> head w%G, 16-row group w/G  (tile = 16*(4/G) rows)
+//   G> 4: every wave 16 rows x HPW = ceil(G/4) heads (tile = 16 rows); a group that is not a
+//         multiple of 4 (Qwen2.5: G = 7) leaves the last wave's surplus head slots idle
 // K/V 32-key tiles are register-staged into LDS, double-buffered with one barrier per
 // tile (async-STAGE split, cdna_hip_programming T14: the next tile's global loads are in
 // flight during this tile's MFMAs). K rows are XOR-swizzled in 16-byte chunks and each
@@ -79,7 +80,9 @@ __global__ void __launch_bounds__(256) prefill_kernel(
   short8 qf[HPW][D / 32];
 #pragma unroll
   for (int hh = 0; hh < HPW; ++hh) {
-    const uint16_t* qr = q + ((size_t)my_row_c * Hq + head0 + hh) * D;
+    // surplus head slot (HPW * 4 > G): read a valid head, never store it
+    const int hq_ = min(head0 + hh, hk * G + G - 1);
+    const uint16_t* qr = q + ((size_t)my_row_c * Hq + hq_) * D;
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) qf[hh][c] = *reinterpret_cast<const short8*>(qr + 8 * (4 * c + g));
   }
@@ -217,7 +220,7 @@ __global__ void __launch_bounds__(256) prefill_kernel(
     for (int i = 0; i < 4; ++i) {
       const float li = __shfl(l, 4 * g + i, 64);
       const int row = wrow0 + 4 * g + i;
-      if (row < q_end && row < row0 + rows_per_tile) {
+      if (row < q_end && row < row0 + rows_per_tile && head0 + hh < hk * G + G) {
         uint16_t* orow = out + ((size_t)row * Hq + head0 + hh) * D;
         const float inv = li > 0.f ? 1.f / li : 0.f;
 #pragma unroll
@@ -253,7 +256,7 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
                    int max_blocks, float scale, hipStream_t stream) {
   if (n_tiles == 0) return 0;
   const int G = Hq / Hkv;
-  if (Hq % Hkv || !(G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) return -1;
+  if (Hq % Hkv || G < 1 || G > 16) return -1;
   if (use_prefill32(G, D))
     return launch_prefill32(out, q, k_cache, v_cache, block_tables, cu_q, start_pos, tile_map, n_tiles, Hq, Hkv,
                             max_blocks, scale, stream, 2, nullptr, 0, nullptr, nullptr);
@@ -264,14 +267,16 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
   hipLaunchKernelGGL((prefill_kernel<DD, HH>), grid, block, 2 * PrefillCfg<DD>::STAGE, stream, (uint16_t*)out,   \
                      (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, \
                      start_pos, tile_map, Hq, Hkv, max_blocks, sl2, rows)
-  const int hpw = G > 4 ? G / 4 : 1;
+  const int hpw = G > 4 ? (G + 3) / 4 : 1;
   if (D == 128) {
     if (hpw == 1) RT_PF(128, 1);
     else if (hpw == 2) RT_PF(128, 2);
+    else if (hpw == 3) RT_PF(128, 3);
     else RT_PF(128, 4);
   } else if (D == 64) {
     if (hpw == 1) RT_PF(64, 1);
     else if (hpw == 2) RT_PF(64, 2);
+    else if (hpw == 3) RT_PF(64, 3);
     else RT_PF(64, 4);
   } else {
     return -2;

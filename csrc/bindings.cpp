@@ -48,7 +48,8 @@ int splitk_parts(int T, int ks, int cus, int64_t ws_ints);
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
-                            hipStream_t stream, int* split_ws, int64_t split_ws_ints, int split_mode);
+                            hipStream_t stream, int* split_ws, int64_t split_ws_ints, int split_mode,
+                            const float* bias);
 int launch_decode_prep(int64_t* slots, int64_t* offsets, void* res, const int64_t* ids, const int64_t* positions,
                        const int* block_tables, const void* embed, int B, int max_blocks, int BS, int H,
                        int64_t vocab, hipStream_t stream);
@@ -433,7 +434,7 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
                       torch::Tensor cos_sin, torch::Tensor k_cache, torch::Tensor v_cache, torch::Tensor slots,
                       int64_t Hq, int64_t Hkv, int64_t D, double eps, c10::optional<torch::Tensor> x2,
                       c10::optional<torch::Tensor> xout, c10::optional<torch::Tensor> split_ws,
-                      int64_t split_mode) {
+                      int64_t split_mode, c10::optional<torch::Tensor> bias) {
   check_bf16(q_out, "q_out");
   check_bf16(x, "x");
   check_bf16(Ws, "Ws");
@@ -448,6 +449,9 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
   TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "positions/slots must cover M rows");
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
   check_caches(k_cache, v_cache, Hkv, D);
+  if (bias.has_value())   // fp32, already in the ROPE epilogue's column order (ops.rope_bias)
+    TORCH_CHECK(bias->scalar_type() == torch::kFloat32 && bias->is_contiguous() && bias->numel() == Ws.size(0) &&
+                    bias->device() == x.device(), "skinny_gemm_rope: bias must be contiguous fp32 [N] on x's device");
   const auto addo = add_operands(x, pro, x2, xout);
   int* sw = nullptr;
   int64_t sw_n = 0;
@@ -461,7 +465,8 @@ void skinny_gemm_rope(torch::Tensor q_out, torch::Tensor x, torch::Tensor Ws, in
                                          (float)eps, positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                          k_cache.data_ptr(), v_cache.data_ptr(), slots.data_ptr<int64_t>(), (int)Hq,
                                          (int)Hkv, (int)D, (int)k_cache.size(2), addo.first, addo.second,
-                                         cur_stream(), sw, sw_n, (int)split_mode);
+                                         cur_stream(), sw, sw_n, (int)split_mode,
+                                         bias.has_value() ? bias->data_ptr<float>() : nullptr);
   TORCH_CHECK(rc == 0, "skinny_gemm_rope: unsupported configuration (rc=", rc, ")");
 }
 
@@ -713,7 +718,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("q_out"), py::arg("x"), py::arg("Ws"), py::arg("pro"), py::arg("positions"), py::arg("cos_sin"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("slots"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
         py::arg("eps"), py::arg("x2") = py::none(), py::arg("xout") = py::none(),
-        py::arg("split_ws") = py::none(), py::arg("split_mode") = 3);
+        py::arg("split_ws") = py::none(), py::arg("split_mode") = 3, py::arg("bias") = py::none());
   m.doc() = "theroundtaible_amd CDNA4 (gfx950) HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);

@@ -584,8 +584,9 @@ int launch_shuffle_weight(void* Ws, const void* W, const void* gamma, int N, int
 int launch_skinny_gemm_rope(void* q_out, const void* x, const void* Ws, int M, int K, int pro, float eps,
                             const int64_t* positions, const float* cos_sin, void* k_cache, void* v_cache,
                             const int64_t* slots, int Hq, int Hkv, int D, int BS, const void* x2, void* xo,
-                            hipStream_t stream, int* split_ws, int64_t split_ws_ints, int split_mode) {
-  const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS};
+                            hipStream_t stream, int* split_ws, int64_t split_ws_ints, int split_mode,
+                            const float* bias) {
+  const RopeEpi re{positions, cos_sin, (uint16_t*)k_cache, (uint16_t*)v_cache, slots, Hq, Hkv, D, BS, bias};
   return launch_skinny_gemm(q_out, x, Ws, nullptr, M, (Hq + 2 * Hkv) * D, K, 0, eps, pro, EPI_ROPE, &re, x2, xo,
                             stream, split_ws, split_ws_ints, split_mode);
 }

@@ -42,6 +42,7 @@ struct RopeEpi {
   uint16_t* v_cache;
   const int64_t* slots;      // [M]
   int Hq, Hkv, D, BS;
+  const float* bias;         // [N] q/k/v bias in the epilogue's column order (Qwen2), or null
 };
 
 // EPI_AR: the K9 comm of csrc/oneshot_ar.hip (receive buffers [2 slots][world][cap] bf16 and
@@ -546,7 +547,7 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
   // K/V slot, position and cos/sin pair (ROPE). Unconditional, rows clamped (no branch for the
   // waitcnt pass to merge); the epilogue thread (em, en) is the one that uses them.
   const int em = min((int)(threadIdx.x >> 4), M - 1), en = threadIdx.x & 15;
-  float e_res = 0.f, e_c = 0.f, e_s = 0.f;
+  float e_res = 0.f, e_c = 0.f, e_s = 0.f, e_b = 0.f, e_bp = 0.f;
   int64_t e_slot = 0;
   if constexpr (EPI == EPI_RESID) e_res = ld16<SC1>(p.res + (size_t)em * N + tile * 16 + en);
   if constexpr (EPI == EPI_ROPE) {
@@ -556,6 +557,10 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
     const float* cs = re.cos_sin + (size_t)re.positions[em] * re.D;
     e_c = cs[pp >> 1];
     e_s = cs[(re.D >> 1) + (pp >> 1)];
+    if (re.bias != nullptr) {   // this column's bias and its rotate-half partner's (column ^ 1)
+      e_b = re.bias[tile * 16 + en];
+      e_bp = re.bias[(tile * 16 + en) ^ 1];
+    }
   }
   int j = 0;
   if constexpr (ALDS) {
@@ -661,8 +666,9 @@ RT_DEVICE void gemm_tile(const GemmArgs& p, int tile, GemmSmem<nacc<EPI>(), NW>&
       const int64_t slot = e_slot;
       const int64_t blk = slot / re.BS;
       const int off = (int)(slot - blk * re.BS);
+      v += e_b;
       if (h < re.Hq + re.Hkv) {
-        const float partner = vpartner * inv;
+        const float partner = fmaf(vpartner, inv, e_bp);
         const int i = pp >> 1, hi = pp & 1;
         const float c = e_c, sn = e_s;
         // pair (x1 = d i, x2 = d i+D/2): y1 = x1 c - x2 s ; y2 = x2 c + x1 s
@@ -806,8 +812,19 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
   // epilogue operands independent of the GEMM, loaded under the k-loop (as gemm_tile); the
   // epilogue thread (em, en) of row block b owns row 16 b + em
   const int em = threadIdx.x >> 4, en = threadIdx.x & 15;
-  float e_res[TN][MB], e_c[TN][MB], e_s[TN][MB];
+  float e_res[TN][MB], e_c[TN][MB], e_s[TN][MB], e_b[TN], e_bp[TN];
   int64_t e_slot[MB];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    e_b[t] = e_bp[t] = 0.f;
+    if constexpr (EPI == EPI_ROPE) {
+      const int c = min(tile0 + t, T - 1) * 16 + en;
+      if (p.re.bias != nullptr) {
+        e_b[t] = p.re.bias[c];
+        e_bp[t] = p.re.bias[c ^ 1];
+      }
+    }
+  }
 #pragma unroll
   for (int b = 0; b < MB; ++b) {
     const int row = min(16 * b + em, M - 1);
@@ -965,8 +982,9 @@ RT_DEVICE void gemm_tiles(const GemmArgs& p, int tile0, GemmSmemN<nacc<EPI>(), N
           const int h = col / D, pp = col - h * D;
           const int64_t blk = e_slot[b] / re.BS;
           const int off = (int)(e_slot[b] - blk * re.BS);
+          v += e_b[t];
           if (h < re.Hq + re.Hkv) {
-            const float partner = vpartner * inv;
+            const float partner = fmaf(vpartner, inv, e_bp[t]);
             const int i = pp >> 1, hi = pp & 1;
             const float y = hi ? fmaf(v, e_c[t][b], partner * e_s[t][b]) : fmaf(v, e_c[t][b], -partner * e_s[t][b]);
             const int d = i + hi * half;

@@ -80,6 +80,26 @@ def test_oom_is_classified_and_recovers():
     assert ok.error is None and len(ok.ids) == 4
 
 
+def test_context_past_max_positions_fails_the_turn_on_the_host():
+    """A context longer than the model's positions (RoPE table, block-table width) must fail the
+    turn before any kernel indexes past those tables (Qwen2.5-7B: 32768 positions; a 40K-token
+    discussion faulted the GPU before this guard) — as prefill and as decode growth."""
+    from dataclasses import replace as dc_replace
+    e = cpu_engine(num_blocks=256)
+    assert e.kv.max_tokens == e.cfg.max_pos
+    e.kv.max_tokens = 128                    # a short-context model without building one
+    out = e.run_turns([Turn("K", "woord " * 200, GREEDY)])[0]
+    assert isinstance(out.error, AdapterError) and out.error.kind == "oom" and "positions" in str(out.error)
+    # a prompt that fits but whose reply would cross the limit fails the same way
+    n = len(e.encode_prompt("woord " * 40))
+    assert n + 2 < 128
+    sp = dc_replace(GREEDY, max_new_tokens=128 - n + 8)
+    out = e.run_turns([Turn("K2", "woord " * 40, sp)])[0]
+    assert out.error is not None and out.error.kind == "oom"
+    ok = e.run_turns([Turn("K3", "kort", GREEDY)])[0]
+    assert ok.error is None and len(ok.ids) == 10
+
+
 def test_timeout():
     e = cpu_engine(sync_every=1)
     out = e.run_turns([Turn("K", "hallo", SamplingParams(temperature=0, max_new_tokens=50, ignore_eos=True,

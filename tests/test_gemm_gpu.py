@@ -238,6 +238,35 @@ def test_skinny_gemm_rope_epilogue(M, hq, hkv, d):
     close(q_r, q2, 0.05, 0.02)
 
 
+@pytest.mark.parametrize("M", [1, 3, 20])
+@pytest.mark.parametrize("hq,hkv,K,d", [(28, 4, 3584, 128), (4, 1, 3584, 128), (14, 2, 896, 64)])
+def test_skinny_gemm_rope_qkv_bias(M, hq, hkv, K, d):
+    """Qwen2 q/k/v bias in the RoPE epilogue (after the norm scale, before the rotation; the
+    rotate-half partner gets its own column's bias) on every launch form the shapes select —
+    whole tiles, CU-balanced halves (Qwen2.5-7B: 288 tiles), split-K (a 48-tile tp shard), the
+    20-row serving form — against the natural-order path: fp32 GEMM + bias -> K2 reference."""
+    N = (hq + 2 * hkv) * d
+    x = bf(M, K, seed=161)
+    W = bf(N, K, scale=0.05, seed=162)
+    gam = bf(K, seed=163)
+    b = bf(N, scale=0.5, seed=164)
+    cos_sin = ref.rope_cos_sin(4096, d, 1e6, DEV)
+    positions = torch.randint(0, 4000, (M,), device=DEV, dtype=torch.int64)
+    nb = 8
+    slots = torch.randperm(nb * 32, device=DEV)[:M].to(torch.int64)
+    kc = torch.zeros(nb, hkv, 32, d, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros(nb, hkv, d, 32, dtype=torch.bfloat16, device=DEV)
+    Ws = ops.shuffle_weight(W, gam, rope_heads=hq + hkv, head_dim=d)
+    q = ops.skinny_gemm_rope(x, Ws, ops.PRO_NORM, positions, cos_sin, kc, vc, slots, hq, hkv, d, 1e-6,
+                             split_ws=ops.split_workspace(DEV), bias=ops.rope_bias(b, hq, hkv, d))
+    kc_r, vc_r = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    qkv = ref.skinny_gemm(x.cpu(), ref.fold_gamma(W.cpu(), gam.cpu()), 1, 3, None, 1e-6) + b.cpu().float()[None, :]
+    q_r = ref.rope_and_cache(qkv, positions.cpu(), cos_sin.cpu(), kc_r, vc_r, slots.cpu(), hq, hkv, d)
+    close(q, q_r.to(DEV), 0.05, 0.02)
+    close(kc, kc_r.to(DEV), 0.05, 0.02)
+    close(vc, vc_r.to(DEV), 0.05, 0.02)
+
+
 @pytest.mark.parametrize("M", [1, 3, 16])
 @pytest.mark.parametrize("hq,hkv,K", [(32, 8, 4096), (40, 8, 1024)])
 def test_skinny_gemm_rope_balanced_split(M, hq, hkv, K):

@@ -14,6 +14,7 @@ import torch
 transformers = pytest.importorskip("transformers")
 
 from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn  # noqa: E402
+from theroundtaible_amd.models.config import get_config  # noqa: E402
 
 
 def _save_llama(path, mistral=False, big=False, seed=0):
@@ -28,6 +29,23 @@ def _save_llama(path, mistral=False, big=False, seed=0):
     else:
         cfg = transformers.LlamaConfig(rope_theta=500000.0 if big else 10000.0, **kw)
         m = transformers.LlamaForCausalLM(cfg)
+    m.eval().save_pretrained(str(path), safe_serialization=True)
+    return m
+
+
+def _save_qwen2(path, big=False, seed=0):
+    """Qwen2 (Qwen2.5 / Qwen2.5-Coder): the Llama block with q/k/v biases; the small config ties
+    the embeddings (as Qwen2.5-0.5B does) and uses head_dim 64 with 2 KV heads."""
+    kw = dict(hidden_size=512 if big else 256, intermediate_size=1024 if big else 512, num_hidden_layers=2,
+              num_attention_heads=4, num_key_value_heads=1 if big else 2, vocab_size=32000,
+              max_position_embeddings=8192 if big else 4096, rms_norm_eps=1e-6, rope_theta=1e6,
+              tie_word_embeddings=not big, initializer_range=0.08, use_sliding_window=False)
+    torch.manual_seed(seed)
+    m = transformers.Qwen2ForCausalLM(transformers.Qwen2Config(**kw))
+    with torch.no_grad():   # HF initialises the biases to zero: make them matter
+        for layer in m.model.layers:
+            for lin in (layer.self_attn.q_proj, layer.self_attn.k_proj, layer.self_attn.v_proj):
+                lin.bias.normal_(0.0, 0.5)
     m.eval().save_pretrained(str(path), safe_serialization=True)
     return m
 
@@ -79,15 +97,22 @@ def test_mistral_matches_transformers(tmp_path):
     _check_cpu("tiny-llama", _save_llama(tmp_path, mistral=True), tmp_path, {"rope_theta": 1e6})
 
 
+def test_qwen2_matches_transformers(tmp_path):
+    """q/k/v biases before RoPE, tied embeddings (the lm_head is the embedding), theta 1e6."""
+    from theroundtaible_amd.utils.local_detect import checkpoint_model
+    hf = _save_qwen2(tmp_path)
+    preset, ov = checkpoint_model(str(tmp_path))      # config.json alone maps it to the Qwen family
+    assert preset is not None and get_config(preset, **ov).qkv_bias
+    _check_cpu("tiny-qwen", hf, tmp_path)
+
+
 def test_gpt2_matches_transformers(tmp_path):
     _check_cpu("tiny-gpt2", _save_gpt2(tmp_path), tmp_path)
 
 
-@pytest.mark.gpu
-def test_llama_gpu_kernels_match_transformers(tmp_path):
-    """bf16 HIP path (prefill kernels, fused decode GEMMs + paged decode attention in hipGraphs)."""
-    hf = _save_llama(tmp_path, big=True).float()
-    e = Engine(EngineConfig(model="tiny-llama-128", weights=str(tmp_path), device="cuda", num_blocks=256))
+def _check_gpu(engine_model, hf, path):
+    hf = hf.float()
+    e = Engine(EngineConfig(model=engine_model, weights=str(path), device="cuda", num_blocks=256))
     ids = _ids(300, seed=3)
     with torch.no_grad():
         ref = hf(torch.tensor([ids])).logits[0, -1].float()
@@ -105,3 +130,15 @@ def test_llama_gpu_kernels_match_transformers(tmp_path):
                            pad_token_id=0)[0, len(prompt_ids):].tolist()
     assert out.ids[:3] == gen2[:3], (out.ids, gen2)
     assert gen[:1] == [int(torch.argmax(got))]
+
+
+@pytest.mark.gpu
+def test_llama_gpu_kernels_match_transformers(tmp_path):
+    """bf16 HIP path (prefill kernels, fused decode GEMMs + paged decode attention in hipGraphs)."""
+    _check_gpu("tiny-llama-128", _save_llama(tmp_path, big=True), tmp_path)
+
+
+@pytest.mark.gpu
+def test_qwen2_gpu_kernels_match_transformers(tmp_path):
+    """Qwen2 on the HIP path: the q/k/v bias rides in the fused qkv GEMM's RoPE epilogue."""
+    _check_gpu("tiny-qwen-128", _save_qwen2(tmp_path, big=True), tmp_path)

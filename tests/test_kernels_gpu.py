@@ -80,7 +80,7 @@ def test_rope_and_cache(hq, hkv, d, rope):
 
 
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 2, 128), (4, 1, 128),
-                                      (8, 1, 128)])
+                                      (8, 1, 128), (28, 4, 128), (14, 2, 64)])
 @pytest.mark.parametrize("splits", [1, 3, 8, 64])
 def test_paged_decode(hq, hkv, d, splits):
     lens = [1, 31, 32, 33, 257, 1500]
@@ -119,7 +119,8 @@ def _check_planned(out, q, kc, vc, bt, cl, scale, splits, ws, hq, hkv, groups=No
     assert int(ws.counters.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64), (4, 1, 128)])
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64), (4, 1, 128),
+                                      (28, 4, 128)])
 @pytest.mark.parametrize("splits", [1, 3, 10, 64])
 @pytest.mark.parametrize("layout", ["table3", "mixed"])
 def test_paged_decode_shared_prefix_groups(hq, hkv, d, splits, layout):
@@ -215,8 +216,11 @@ def test_paged_decode_spike():
         close(out, exp.to(DEV), 0.03, 0.02)
 
 
-@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 128), (16, 1, 128)])
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 128), (16, 1, 128),
+                                      (28, 4, 128), (14, 2, 64), (12, 4, 128), (12, 1, 64)])
 def test_prefill_varlen(hq, hkv, d):
+    """Includes GQA groups that are not powers of two (Qwen2.5: G = 7; G = 3, 12): the 16x16
+    kernel's surplus head slots stay idle."""
     # (start_pos, new tokens): prefix already cached + delta chunk
     specs = [(0, 1), (0, 45), (100, 70), (31, 33), (500, 17)]
     S = len(specs)

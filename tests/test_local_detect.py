@@ -41,6 +41,25 @@ def test_detect_and_match(tmp_path):
     assert mis.adapter_slug() == "mistral-7b-v0-3"
 
 
+def test_detect_qwen2_family(tmp_path):
+    """Qwen2.5 checkpoints (model_type qwen2) map to the Qwen presets with q/k/v biases; a Llama
+    variant with biased o / MLP projections is not offered (the engine's block has none)."""
+    qwen7b = {"model_type": "qwen2", "hidden_size": 3584, "num_hidden_layers": 28, "num_attention_heads": 28,
+              "num_key_value_heads": 4, "intermediate_size": 18944, "vocab_size": 152064,
+              "max_position_embeddings": 32768, "rope_theta": 1000000.0, "rms_norm_eps": 1e-6,
+              "tie_word_embeddings": False}
+    _ckpt(str(tmp_path / "Qwen2.5-7B-Instruct"), qwen7b)
+    _ckpt(str(tmp_path / "Qwen2.5-Coder-0.5B"), dict(qwen7b, hidden_size=896, num_hidden_layers=24,
+                                                     num_attention_heads=14, num_key_value_heads=2,
+                                                     intermediate_size=4864, vocab_size=151936,
+                                                     tie_word_embeddings=True))
+    _ckpt(str(tmp_path / "llama-attn-bias"), dict(LLAMA8B_HF, attention_bias=True))
+    found = {m.model_id: m for m in detect_local_models([str(tmp_path)])}
+    assert set(found) == {"Qwen2.5-7B-Instruct", "Qwen2.5-Coder-0.5B"}
+    assert found["Qwen2.5-7B-Instruct"].preset == "qwen2.5-7b" and found["Qwen2.5-7B-Instruct"].overrides == {}
+    assert found["Qwen2.5-Coder-0.5B"].preset == "qwen2.5-0.5b" and found["Qwen2.5-Coder-0.5B"].overrides == {}
+
+
 def test_match_gpt2():
     preset, diff = match_preset({"arch": "gpt2", "n_layers": 12, "hidden": 768, "n_heads": 12, "n_kv_heads": 12,
                                  "head_dim": 64, "ffn": 3072, "vocab": 50257, "max_pos": 1024, "rope_theta": 0.0,

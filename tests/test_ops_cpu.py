@@ -39,6 +39,36 @@ def test_skinny_gemm_rope_reference_matches_unfused():
     assert torch.equal(vc, vc2)
 
 
+def test_skinny_gemm_rope_bias_reference_matches_unfused():
+    """Qwen2 q/k/v bias: permuted into the shuffled weight's column order (ops.rope_bias) and
+    added before RoPE, it equals the natural-order GEMM + bias -> K2 path."""
+    torch.manual_seed(2)
+    M, hq, hkv, d, K = 3, 8, 2, 64, 128
+    N = (hq + 2 * hkv) * d
+    x = torch.randn(M, K).bfloat16()
+    W = (torch.randn(N, K) * 0.05).bfloat16()
+    g = torch.randn(K).bfloat16()
+    b = (torch.randn(N) * 0.5).bfloat16()
+    cs = ref.rope_cos_sin(256, d, 1e6)
+    pos = torch.tensor([5, 100, 200])
+    slots = torch.tensor([3, 40, 77])
+    kc = torch.zeros(4, hkv, 32, d).bfloat16()
+    vc = torch.zeros(4, hkv, d, 32).bfloat16()
+    Wp = ops.shuffle_weight(W, g, rope_heads=hq + hkv, head_dim=d)
+    q = ops.skinny_gemm_rope(x, Wp, ops.PRO_NORM, pos, cs, kc, vc, slots, hq, hkv, d,
+                             bias=ops.rope_bias(b, hq, hkv, d))
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    qkv = ref.skinny_gemm(x, ref.fold_gamma(W, g), ops.PRO_NORM, 3) + b.float()[None, :]
+    q2 = ref.rope_and_cache(qkv, pos, cs, kc2, vc2, slots, hq, hkv, d)
+    assert (q.float() - q2.float()).abs().max() < 0.02
+    assert (kc.float() - kc2.float()).abs().max() < 0.02
+    assert (vc.float() - vc2.float()).abs().max() < 0.02
+    # without the bias the result differs (the test would not see a dropped bias otherwise)
+    kc3, vc3 = torch.zeros_like(kc), torch.zeros_like(vc)
+    q3 = ops.skinny_gemm_rope(x, Wp, ops.PRO_NORM, pos, cs, kc3, vc3, slots, hq, hkv, d)
+    assert (q3.float() - q2.float()).abs().max() > 0.1
+
+
 def test_skinny_gemm_norm_prologue_equals_rmsnorm_then_linear():
     torch.manual_seed(1)
     x = torch.randn(4, 256).bfloat16()

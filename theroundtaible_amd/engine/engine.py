@@ -194,8 +194,10 @@ class Engine:
             # them or none (a pool sized from one rank's free memory, e.g. a second rehearsal rank
             # on a shared GPU, could run out alone and skip collectives its peers enter)
             nb = self.tp.group_min(int(nb))
-        return PagedKVCache(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, int(nb), bs,
-                            self.device, self.dtype)
+        kv = PagedKVCache(self.cfg.n_layers, m.kv_heads_local, self.cfg.head_dim, int(nb), bs,
+                          self.device, self.dtype)
+        kv.max_tokens = self.cfg.max_pos   # RoPE table / block-table width (_max_blocks)
+        return kv
 
     def allocate_kv(self, budget_bytes: Optional[int] = None) -> None:
         """Deferred KV pool (``defer_kv``): sized by ``budget_bytes`` — EnginePool.finalize splits a

@@ -99,8 +99,15 @@ class PagedKVCache:
     def blocks_needed(self, n_tokens: int) -> int:
         return (n_tokens + self.block_size - 1) // self.block_size
 
+    # positions a sequence may reach (the model's RoPE table / position embeddings and the block
+    # tables are sized by it); None = unbounded. Past it a kernel would index beyond those tables,
+    # so the turn fails here, on the host, like any other KV exhaustion (kind "oom").
+    max_tokens: Optional[int] = None
+
     def ensure_capacity(self, s: SeqState, n_tokens: int) -> None:
         """Grow ``s.blocks`` to hold ``n_tokens`` (copy-on-write if the tail block is shared)."""
+        if self.max_tokens is not None and n_tokens > self.max_tokens:
+            raise KVCacheOOM(f"context of {n_tokens} tokens exceeds the model's {self.max_tokens} positions")
         need = self.blocks_needed(n_tokens)
         if s.blocks and self.alloc.ref[s.blocks[-1]] > 1 and s.length % self.block_size:
             self._cow_tail(s)

@@ -8,7 +8,7 @@ from typing import Dict
 @dataclass(frozen=True)
 class ModelConfig:
     name: str
-    arch: str                 # "llama" (Llama-3 / Mistral) | "gpt2"
+    arch: str                 # "llama" (Llama-3 / Mistral / Qwen2) | "gpt2"
     n_layers: int
     hidden: int
     n_heads: int
@@ -20,6 +20,7 @@ class ModelConfig:
     rope_theta: float = 500000.0
     norm_eps: float = 1e-5
     tie_embeddings: bool = False
+    qkv_bias: bool = False    # Qwen2 / Qwen2.5: biased q/k/v projections (added before RoPE)
 
     @property
     def q_size(self) -> int:
@@ -39,6 +40,8 @@ class ModelConfig:
             per = 4 * h * h + 2 * h * f + 9 * h + f
             return L * per + v * h + self.max_pos * h + 2 * h
         per = h * (self.q_size + 2 * self.kv_size) + self.q_size * h + 3 * h * f + 2 * h
+        if self.qkv_bias:
+            per += self.q_size + 2 * self.kv_size
         emb = v * h * (1 if self.tie_embeddings else 2)
         return L * per + emb + h
 
@@ -50,11 +53,20 @@ PRESETS: Dict[str, ModelConfig] = {
     "llama3-8b": ModelConfig("llama3-8b", "llama", 32, 4096, 32, 8, 128, 14336, 128256, 131072, 500000.0, 1e-5),
     "llama3-70b": ModelConfig("llama3-70b", "llama", 80, 8192, 64, 8, 128, 28672, 128256, 131072, 500000.0, 1e-5),
     "mistral-7b": ModelConfig("mistral-7b", "llama", 32, 4096, 32, 8, 128, 14336, 32000, 32768, 1000000.0, 1e-5),
+    # Qwen2.5 (HF model_type "qwen2"): the Llama block with q/k/v biases; 7B: GQA 28 / 4 heads,
+    # 0.5B: head_dim 64, tied embeddings (the family most local coding setups run)
+    "qwen2.5-7b": ModelConfig("qwen2.5-7b", "llama", 28, 3584, 28, 4, 128, 18944, 152064, 32768, 1000000.0, 1e-6,
+                              False, True),
+    "qwen2.5-0.5b": ModelConfig("qwen2.5-0.5b", "llama", 24, 896, 14, 2, 64, 4864, 151936, 32768, 1000000.0, 1e-6,
+                                True, True),
     # GPT-2-small: random init allows n_positions beyond 1024 (SURVEY §7.3 hard part 3).
     "gpt2-small": ModelConfig("gpt2-small", "gpt2", 12, 768, 12, 12, 64, 3072, 50257, 8192, 0.0, 1e-5, True),
     # test-sized models (CPU unit tests, GPU smoke)
     "tiny-llama": ModelConfig("tiny-llama", "llama", 2, 256, 4, 2, 64, 512, 32000, 4096, 10000.0, 1e-5),
     "tiny-llama-128": ModelConfig("tiny-llama-128", "llama", 2, 512, 4, 1, 128, 1024, 32000, 8192, 500000.0, 1e-5),
+    "tiny-qwen": ModelConfig("tiny-qwen", "llama", 2, 256, 4, 2, 64, 512, 32000, 4096, 1000000.0, 1e-6, True, True),
+    "tiny-qwen-128": ModelConfig("tiny-qwen-128", "llama", 2, 512, 4, 1, 128, 1024, 32000, 8192, 1000000.0, 1e-6,
+                                 False, True),
     "tiny-gpt2": ModelConfig("tiny-gpt2", "gpt2", 2, 128, 2, 2, 64, 512, 32000, 2048, 0.0, 1e-5, True),
 }
 

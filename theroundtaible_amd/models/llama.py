@@ -1,4 +1,4 @@
-"""Llama-3 / Mistral decoder (dense, GQA, RoPE, SwiGLU, RMSNorm), TP-aware.
+"""Llama-3 / Mistral / Qwen2 decoder (dense, GQA, RoPE, SwiGLU, RMSNorm; Qwen2: q/k/v bias), TP-aware.
 
 Per layer (decode and prefill share the code; only the attention op differs):
 
@@ -122,6 +122,8 @@ class LlamaModel:
                             # stays one weight copy + one tensor
                             lw[name] = None
                             self.w[f"layers.{i}.{name}"] = None
+                    if lw.get("bqkv") is not None:   # Qwen2: the bias the qkv epilogue adds before RoPE
+                        d["bqkv"] = ops.rope_bias(lw["bqkv"], self.n_heads, self.n_kv_heads, self.head_dim)
                     layers.append(d)
                 lm = ops.shuffle_weight(self.w["lm_head"], self.w["final_norm"])
                 if drop_originals:
@@ -186,7 +188,7 @@ class LlamaModel:
         for l, lw in enumerate(dec["layers"]):
             q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kv.k_layer(l),
                                      kv.v_layer(l), meta.slot_mapping, self.n_heads, self.n_kv_heads,
-                                     self.head_dim, eps, split_ws=sw, split_mode=SK)
+                                     self.head_dim, eps, split_ws=sw, split_mode=SK, bias=lw.get("bqkv"))
             a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)
             ops.skinny_gemm(a.reshape(B, -1), lw["wo"], ops.PRO_PLAIN, ops.EPI_RESID, res=res, split_ws=sw,
                             split_mode=SK)
@@ -220,7 +222,7 @@ class LlamaModel:
             kc, vc = kv.k_layer(l), kv.v_layer(l)
             q = ops.skinny_gemm_rope(res, lw["wqkv"], ops.PRO_NORM, positions, self.cos_sin, kc, vc,
                                      meta.slot_mapping, self.n_heads, self.n_kv_heads, self.head_dim, eps,
-                                     split_ws=dec["split_ws"], split_mode=0)
+                                     split_ws=dec["split_ws"], split_mode=0, bias=lw.get("bqkv"))
             a = self.attention(q, kc, vc, meta)
             tp.row_parallel(a.reshape(B, -1), lw["wo"], res=res, **sk)
             g = ops.skinny_gemm(res, lw["w_gate_up"], ops.PRO_NORM, ops.EPI_SWIGLU, eps=eps, **sk)
@@ -253,7 +255,7 @@ class LlamaModel:
                 x = ops.rms_norm(h, self._norm_w(l, "attn_norm"), cfg.norm_eps)
             else:
                 x, res = ops.fused_add_rms_norm(h, res, self._norm_w(l, "attn_norm"), cfg.norm_eps)
-            qkv = F.linear(x, self._row_major(l, "wqkv"))
+            qkv = F.linear(x, self._row_major(l, "wqkv"), lw.get("bqkv"))
             q = ops.rope_and_cache(qkv, positions, self.cos_sin, kv.k_layer(l), kv.v_layer(l), meta.slot_mapping,
                                    self.n_heads, self.n_kv_heads, self.head_dim)
             a = self.attention(q, kv.k_layer(l), kv.v_layer(l), meta)

@@ -7,7 +7,7 @@ first and then shards them, so TP=1 and TP=N see identical math (TP equivalence
 tests). ``random-dev:<seed>`` does the same with the full tensors generated on the target
 device, one tensor at a time (GPU TP checks at 8B / 70B shapes, where CPU generation of the
 unsharded model would take minutes and tens of GB of host memory per rank).
-A path loads HF-named safetensors (Llama/Mistral/GPT-2 naming) and shards it.
+A path loads HF-named safetensors (Llama/Mistral/Qwen2/GPT-2 naming) and shards it.
 """
 from __future__ import annotations
 
@@ -39,6 +39,8 @@ def llama_layout(cfg: ModelConfig) -> Dict[str, Tuple[Tuple[int, ...], str, Opti
         p = f"layers.{i}."
         lay[p + "attn_norm"] = ((H,), "ones", None)
         lay[p + "wqkv"] = (((cfg.n_heads + 2 * cfg.n_kv_heads) * D, H), "normal", "qkv")
+        if cfg.qkv_bias:
+            lay[p + "bqkv"] = (((cfg.n_heads + 2 * cfg.n_kv_heads) * D,), "normal", "qkv")
         lay[p + "wo"] = ((H, cfg.n_heads * D), "normal", "col")
         lay[p + "ffn_norm"] = ((H,), "ones", None)
         lay[p + "w_gate_up"] = ((2 * cfg.ffn, H), "normal", "gateup")
@@ -135,7 +137,9 @@ def materialize(cfg: ModelConfig, spec: str, device, dtype=torch.bfloat16, tp: O
                 if init == "normal" and name in ("embed", "wte"):
                     w.mul_(10)
                 out[name] = w
-        if cfg.tie_embeddings and "lm_head" in out:
+        # GPT-2 reads its tied head from wte; a tied Llama-family model (random init) keeps an
+        # independent vocab-parallel lm_head (checkpoints copy the embedding, load_safetensors)
+        if cfg.tie_embeddings and cfg.arch == "gpt2" and "lm_head" in out:
             out.pop("lm_head")
         return out
     if os.path.isdir(spec) or spec.endswith(".safetensors"):
@@ -168,6 +172,10 @@ def _hf_llama_name_map(cfg: ModelConfig) -> Dict[str, Callable[[Dict[str, torch.
         m[f"layers.{i}.wqkv"] = lambda t, p=p: torch.cat([t[p + "self_attn.q_proj.weight"],
                                                            t[p + "self_attn.k_proj.weight"],
                                                            t[p + "self_attn.v_proj.weight"]])
+        if cfg.qkv_bias:
+            m[f"layers.{i}.bqkv"] = lambda t, p=p: torch.cat([t[p + "self_attn.q_proj.bias"],
+                                                               t[p + "self_attn.k_proj.bias"],
+                                                               t[p + "self_attn.v_proj.bias"]])
         m[f"layers.{i}.wo"] = lambda t, p=p: t[p + "self_attn.o_proj.weight"]
         m[f"layers.{i}.w_gate_up"] = lambda t, p=p: torch.cat([t[p + "mlp.gate_proj.weight"],
                                                                t[p + "mlp.up_proj.weight"]])
@@ -212,8 +220,8 @@ def load_safetensors(cfg: ModelConfig, path: str, device, dtype, tp: TPInfo) -> 
     lay = layout_for(cfg)
     out = {}
     for name, fn in name_map.items():
-        if name == "lm_head" and cfg.tie_embeddings:
-            continue
+        if name == "lm_head" and cfg.tie_embeddings and cfg.arch == "gpt2":
+            continue   # GPT-2 reads the tied head from wte; Llama-family models get a (sharded) copy
         w = fn(tensors)
         kind = lay[name][2]
         out[name] = shard_tensor(name, w.float(), kind, cfg, tp).to(device=device, dtype=dtype).contiguous()

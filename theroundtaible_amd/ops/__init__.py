@@ -422,18 +422,25 @@ def skinny_gemm_rope(x: torch.Tensor, Ws: torch.Tensor, pro: int, positions: tor
                      k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor, n_heads: int,
                      n_kv_heads: int, head_dim: int, eps: float = 1e-5, x2: Optional[torch.Tensor] = None,
                      xout: Optional[torch.Tensor] = None, split_ws: Optional[torch.Tensor] = None,
-                     split_mode: int = SPLIT_K | SPLIT_BALANCE) -> torch.Tensor:
+                     split_mode: int = SPLIT_K | SPLIT_BALANCE, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Decode qkv projection (+ optional RMSNorm prologue) with RoPE and the paged K/V cache
     write fused into the epilogue; returns q [M, n_heads, head_dim]. ``Ws`` must come from
     ``shuffle_weight(Wqkv, gamma, rope_heads=n_heads + n_kv_heads, head_dim=head_dim)``.
-    ``split_ws`` / ``split_mode``: as in :func:`skinny_gemm` (no balanced launch with ``PRO_NORM_ADD``)."""
+    ``split_ws`` / ``split_mode``: as in :func:`skinny_gemm` (no balanced launch with ``PRO_NORM_ADD``).
+    ``bias`` (Qwen2 q/k/v bias, added after the norm scale and before RoPE) must come from
+    :func:`rope_bias` (fp32, the shuffled weight's column order)."""
     if _use_native(x):
         q = torch.empty(x.shape[0], n_heads, head_dim, dtype=x.dtype, device=x.device)
         native().skinny_gemm_rope(q, x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
-                                  head_dim, eps, x2, xout, split_ws, int(split_mode))
+                                  head_dim, eps, x2, xout, split_ws, int(split_mode), bias)
         return q
     return ref.skinny_gemm_rope(x, Ws, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads,
-                                head_dim, eps, x2, xout)
+                                head_dim, eps, x2, xout, bias)
+
+
+def rope_bias(b: torch.Tensor, n_heads: int, n_kv_heads: int, head_dim: int) -> torch.Tensor:
+    """A q/k/v bias [(n_heads + 2 n_kv_heads) * head_dim] in the form :func:`skinny_gemm_rope` adds it."""
+    return ref.rope_bias(b, n_heads + n_kv_heads, head_dim)
 
 
 def decode_prep(slots: torch.Tensor, offsets: torch.Tensor, res: torch.Tensor, ids: torch.Tensor,

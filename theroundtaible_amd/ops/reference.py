@@ -168,6 +168,12 @@ def rope_row_perm(n_rows: int, rope_heads: int, head_dim: int) -> torch.Tensor:
     return idx
 
 
+def rope_bias(b: torch.Tensor, rope_heads: int, head_dim: int) -> torch.Tensor:
+    """A q/k/v bias (natural order) as the ROPE epilogue adds it: fp32, in the pair-interleaved
+    column order of the shuffled weight (:func:`rope_row_perm`)."""
+    return b.float()[rope_row_perm(b.numel(), rope_heads, head_dim).to(b.device)].contiguous()
+
+
 def fold_gamma(W, gamma=None, rope_heads: int = 0, head_dim: int = 0):
     """W * gamma[None, :] rounded to W's dtype (the RMSNorm weight folded into the next linear),
     rows optionally permuted for the ROPE epilogue (``rope_heads`` leading heads)."""
@@ -202,10 +208,13 @@ def skinny_gemm(x, Wf, pro=0, epi=0, res=None, eps=1e-5, x2=None, xout=None):
 
 
 def skinny_gemm_rope(x, Wp, pro, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv_heads, head_dim,
-                     eps=1e-5, x2=None, xout=None):
-    """ROPE-epilogue semantics: fp32 projection on the pair-permuted weight, columns restored
-    to natural order, then RoPE + paged K/V scatter with no bf16 rounding in between."""
+                     eps=1e-5, x2=None, xout=None, bias=None):
+    """ROPE-epilogue semantics: fp32 projection on the pair-permuted weight (+ the fp32 bias in
+    the same column order, :func:`rope_bias`), columns restored to natural order, then RoPE +
+    paged K/V scatter with no bf16 rounding in between."""
     y = skinny_gemm(x, Wp, pro, 3, None, eps, x2, xout)
+    if bias is not None:
+        y = y + bias.float()[None, :]
     perm = rope_row_perm(Wp.shape[0], n_heads + n_kv_heads, head_dim)
     qkv = torch.empty_like(y)
     qkv[:, perm] = y

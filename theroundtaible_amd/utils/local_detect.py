@@ -11,7 +11,7 @@ knights, so discovery looks for *weights*: directories holding ``config.json`` p
 * the Hugging Face hub cache (``$HF_HOME``/``~/.cache/huggingface/hub/models--*/snapshots/*``).
 
 Each hit is read (JSON only — nothing from a checkpoint is executed) and matched to a preset
-(Llama-3-8B/70B, Mistral-7B, GPT-2) or described as a preset plus shape overrides; embedding /
+(Llama-3-8B/70B, Mistral-7B, Qwen2.5-7B/0.5B, GPT-2) or described as a preset plus shape overrides; embedding /
 reranker / speech models are skipped, as the reference's ``isNonChatModel`` does.
 Running servers are still supported from the other side: ``roundtable serve`` speaks the
 LM Studio / Ollama dialects.
@@ -62,7 +62,9 @@ def is_non_chat_model(model_id: str) -> bool:
 
 def _shape_from_hf(hf: Dict[str, Any]) -> Optional[Dict[str, Any]]:
     mt = str(hf.get("model_type", "")).lower()
-    if mt in ("llama", "mistral"):
+    if mt in ("llama", "mistral", "qwen2"):
+        if hf.get("attention_bias") or hf.get("mlp_bias"):
+            return None   # biased o / MLP projections (Llama variants): not in the engine's layer
         h = int(hf["hidden_size"])
         nh = int(hf["num_attention_heads"])
         return {"arch": "llama", "n_layers": int(hf["num_hidden_layers"]), "hidden": h, "n_heads": nh,
@@ -70,7 +72,8 @@ def _shape_from_hf(hf: Dict[str, Any]) -> Optional[Dict[str, Any]]:
                 "ffn": int(hf["intermediate_size"]), "vocab": int(hf["vocab_size"]),
                 "max_pos": int(hf.get("max_position_embeddings", 8192)),
                 "rope_theta": float(hf.get("rope_theta", 10000.0)), "norm_eps": float(hf.get("rms_norm_eps", 1e-5)),
-                "tie_embeddings": bool(hf.get("tie_word_embeddings", False))}
+                "tie_embeddings": bool(hf.get("tie_word_embeddings", False)),
+                "qkv_bias": mt == "qwen2"}
     if mt == "gpt2":
         h = int(hf["n_embd"])
         nh = int(hf["n_head"])
@@ -95,7 +98,7 @@ def match_preset(shape: Dict[str, Any]) -> (Optional[str], Dict[str, Any]):
 
 def checkpoint_model(path: str) -> Optional[tuple]:
     """(engine preset, ModelConfig overrides) for an HF checkpoint directory, from its
-    ``config.json`` alone; None if it is not a recognised Llama / Mistral / GPT-2 checkpoint."""
+    ``config.json`` alone; None if it is not a recognised Llama / Mistral / Qwen2 / GPT-2 checkpoint."""
     try:
         with open(os.path.join(path, "config.json"), encoding="utf-8") as f:
             shape = _shape_from_hf(json.load(f))
