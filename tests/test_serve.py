@@ -326,3 +326,31 @@ def test_stop_strings_cut_the_reply(server):
     except urllib.error.HTTPError as e:
         code = e.code
     assert code == 400
+
+
+def test_context_length_exceeded_and_reply_clamped(server):
+    """A prompt past the model's positions (tiny-llama: 4096) is the client's error — HTTP 400 with
+    OpenAI's code, streamed or not; a prompt that fits gets its reply cut to the room left."""
+    long = "woord " * 6000
+    for stream in (False, True):
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            _post(server.url + "/v1/chat/completions",
+                  {"messages": [{"role": "user", "content": long}], "max_tokens": 4, "stream": stream})
+        assert ei.value.code == 400
+        err = json.loads(ei.value.read().decode())["error"]
+        assert err["code"] == "context_length_exceeded" and "4096" in err["message"]
+    eng = server.engine
+    lo, hi = 1, 6000                         # the longest prompt of repeated words below the limit
+    while lo < hi:
+        mid = (lo + hi + 1) // 2
+        if len(eng.encode_prompt("woord " * mid)) < 4096:
+            lo = mid
+        else:
+            hi = mid - 1
+    words = lo
+    n = len(eng.encode_prompt("woord " * words))
+    assert 4096 - 50 < n < 4096
+    code, body = _post(server.url + "/v1/completions", {"prompt": "woord " * words, "max_tokens": 50,
+                                                       "temperature": 0})
+    d = json.loads(body)
+    assert code == 200 and d["usage"]["completion_tokens"] == 4096 - n

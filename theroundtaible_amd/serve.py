@@ -115,6 +115,11 @@ def chat_segments(messages: List[Dict[str, Any]]):
     return parts, n_sys
 
 
+class ContextLengthError(ValueError):
+    """A prompt longer than the model's positions (HTTP 400, OpenAI's error code)."""
+    code = "context_length_exceeded"
+
+
 @dataclass
 class _Request:
     key: str
@@ -564,7 +569,8 @@ class RoundtableServer:
                     else:
                         self._send(404, {"error": {"message": f"no route {self.path}"}})
                 except ValueError as e:
-                    self._send(400, {"error": {"message": str(e), "type": "invalid_request_error"}})
+                    self._send(400, {"error": {"message": str(e), "type": "invalid_request_error",
+                                               "code": getattr(e, "code", None)}})
                 except Exception as e:  # noqa: BLE001
                     self._send(500, {"error": {"message": str(e), "type": "server_error"}})
 
@@ -692,6 +698,16 @@ class RoundtableServer:
 
     def submit(self, prompt, body: Dict[str, Any], session: Optional[str], stream: bool = False) -> _Request:
         params = self.sampling(body)
+        # the model's positions bound prompt + reply (the engine would fail the turn past them):
+        # a prompt that alone reaches them is the client's error (OpenAI's 400
+        # context_length_exceeded); otherwise the reply is cut to the room left (finish "length")
+        limit = int(self.engine.cfg.max_pos)
+        n = len(self.engine.encode_prompt(prompt))
+        if n >= limit:
+            raise ContextLengthError(f"This model's maximum context length is {limit} tokens, "
+                                     f"but the prompt has {n} tokens.")
+        if n + params.max_new_tokens > limit:
+            params = SamplingParams(**{**params.__dict__, "max_new_tokens": limit - n})
         key = f"session:{session}" if session else f"anon:{next(self._anon)}"
         stops = parse_stops(body.get("stop"))
         return self.sched.submit(_Request(key, prompt, params, persistent=bool(session),
