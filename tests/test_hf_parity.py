@@ -17,7 +17,16 @@ from theroundtaible_amd.engine import Engine, EngineConfig, SamplingParams, Turn
 from theroundtaible_amd.models.config import get_config  # noqa: E402
 
 
-def _save_llama(path, mistral=False, big=False, seed=0):
+def _sharpen(m, gain=4.0):
+    """Scale q / k projections so attention is peaked: with the default init the scores are
+    nearly uniform and a wrong RoPE (theta, scaling) would still match to 2e-4."""
+    with torch.no_grad():
+        for layer in m.model.layers:
+            layer.self_attn.q_proj.weight.mul_(gain)
+            layer.self_attn.k_proj.weight.mul_(gain)
+
+
+def _save_llama(path, mistral=False, big=False, seed=0, rope_scaling=None, sharp=True):
     kw = dict(hidden_size=512 if big else 256, intermediate_size=1024 if big else 512, num_hidden_layers=2,
               num_attention_heads=4, num_key_value_heads=1 if big else 2, vocab_size=32000,
               max_position_embeddings=8192 if big else 4096, rms_norm_eps=1e-5, tie_word_embeddings=False,
@@ -27,21 +36,26 @@ def _save_llama(path, mistral=False, big=False, seed=0):
         cfg = transformers.MistralConfig(rope_theta=1e6, sliding_window=None, **kw)
         m = transformers.MistralForCausalLM(cfg)
     else:
-        cfg = transformers.LlamaConfig(rope_theta=500000.0 if big else 10000.0, **kw)
+        cfg = transformers.LlamaConfig(rope_theta=500000.0 if big else 10000.0, rope_scaling=rope_scaling, **kw)
         m = transformers.LlamaForCausalLM(cfg)
+    if sharp and not big:
+        _sharpen(m)
     m.eval().save_pretrained(str(path), safe_serialization=True)
     return m
 
 
-def _save_qwen2(path, big=False, seed=0):
+def _save_qwen2(path, big=False, seed=0, rope_scaling=None):
     """Qwen2 (Qwen2.5 / Qwen2.5-Coder): the Llama block with q/k/v biases; the small config ties
     the embeddings (as Qwen2.5-0.5B does) and uses head_dim 64 with 2 KV heads."""
     kw = dict(hidden_size=512 if big else 256, intermediate_size=1024 if big else 512, num_hidden_layers=2,
               num_attention_heads=4, num_key_value_heads=1 if big else 2, vocab_size=32000,
               max_position_embeddings=8192 if big else 4096, rms_norm_eps=1e-6, rope_theta=1e6,
-              tie_word_embeddings=not big, initializer_range=0.08, use_sliding_window=False)
+              tie_word_embeddings=not big, initializer_range=0.08, use_sliding_window=False,
+              rope_scaling=rope_scaling)
     torch.manual_seed(seed)
     m = transformers.Qwen2ForCausalLM(transformers.Qwen2Config(**kw))
+    if not big:
+        _sharpen(m)
     with torch.no_grad():   # HF initialises the biases to zero: make them matter
         for layer in m.model.layers:
             for lin in (layer.self_attn.q_proj, layer.self_attn.k_proj, layer.self_attn.v_proj):
@@ -66,8 +80,11 @@ def _ids(n, seed=1):
 
 
 def _check_cpu(engine_model, hf, path, overrides=None):
+    if overrides is None:   # the architecture from config.json, as the knights / serve resolve it
+        from theroundtaible_amd.utils.local_detect import resolve_model
+        engine_model, overrides = resolve_model(engine_model, str(path))
     e = Engine(EngineConfig(model=engine_model, weights=str(path), device="cpu", dtype="fp32", num_blocks=64,
-                            model_overrides=dict(overrides or {})))
+                            model_overrides=dict(overrides)))
     ids = _ids(97)
     with torch.no_grad():
         ref = hf(torch.tensor([ids])).logits[0].float()
@@ -94,7 +111,28 @@ def test_llama_matches_transformers(tmp_path):
 
 
 def test_mistral_matches_transformers(tmp_path):
-    _check_cpu("tiny-llama", _save_llama(tmp_path, mistral=True), tmp_path, {"rope_theta": 1e6})
+    _check_cpu("tiny-llama", _save_llama(tmp_path, mistral=True), tmp_path)
+
+
+def test_llama31_rope_scaling_matches_transformers(tmp_path):
+    """Llama 3.1 / 3.2 checkpoints carry rope_type "llama3" (long wavelengths divided by the
+    factor, a smooth band between): read from config.json and folded into the RoPE table."""
+    rs = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+          "original_max_position_embeddings": 64}
+    _check_cpu("tiny-llama", _save_llama(tmp_path, rope_scaling=rs), tmp_path)
+
+
+def test_qwen2_yarn_rope_scaling_matches_transformers(tmp_path):
+    """Qwen2.5's long-context YaRN setting: blended frequencies and scaled cos / sin."""
+    rs = {"rope_type": "yarn", "factor": 4.0, "original_max_position_embeddings": 64}
+    _check_cpu("tiny-qwen", _save_qwen2(tmp_path, rope_scaling=rs), tmp_path)
+
+
+def test_wrong_rope_is_detected(tmp_path):
+    """The parity check is sensitive to RoPE: the same checkpoint with a different theta fails."""
+    hf = _save_llama(tmp_path, mistral=True)
+    with pytest.raises(AssertionError):
+        _check_cpu("tiny-llama", hf, tmp_path, {"rope_theta": 10000.0})
 
 
 def test_qwen2_matches_transformers(tmp_path):

@@ -60,6 +60,23 @@ def test_detect_qwen2_family(tmp_path):
     assert found["Qwen2.5-Coder-0.5B"].preset == "qwen2.5-0.5b" and found["Qwen2.5-Coder-0.5B"].overrides == {}
 
 
+def test_rope_scaling_and_theta_formats(tmp_path):
+    """Llama 3.1 (rope_scaling llama3, old file format), a transformers-5 file (rope_parameters
+    with rope_theta inside) and an unsupported scaling type (not offered)."""
+    from theroundtaible_amd.utils.local_detect import checkpoint_model
+    l31 = dict(LLAMA8B_HF, rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                         "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    _ckpt(str(tmp_path / "Llama-3.1-8B"), l31)
+    preset, ov = checkpoint_model(str(tmp_path / "Llama-3.1-8B"))
+    assert preset == "llama3-8b" and ov == {"rope_scaling": ("llama3", 8.0, 1.0, 4.0, 8192)}
+    v5 = {k: v for k, v in LLAMA8B_HF.items() if k != "rope_theta"}
+    v5["rope_parameters"] = {"rope_theta": 500000.0, "rope_type": "default"}
+    _ckpt(str(tmp_path / "v5"), v5)
+    assert checkpoint_model(str(tmp_path / "v5")) == ("llama3-8b", {})
+    _ckpt(str(tmp_path / "longrope"), dict(LLAMA8B_HF, rope_scaling={"rope_type": "longrope", "factor": 4.0}))
+    assert checkpoint_model(str(tmp_path / "longrope")) is None
+
+
 def test_match_gpt2():
     preset, diff = match_preset({"arch": "gpt2", "n_layers": 12, "hidden": 768, "n_heads": 12, "n_kv_heads": 12,
                                  "head_dim": 64, "ffn": 3072, "vocab": 50257, "max_pos": 1024, "rope_theta": 0.0,

@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 from dataclasses import dataclass, replace
-from typing import Dict
+from typing import Dict, Optional
 
 
 @dataclass(frozen=True)
@@ -21,6 +21,9 @@ class ModelConfig:
     norm_eps: float = 1e-5
     tie_embeddings: bool = False
     qkv_bias: bool = False    # Qwen2 / Qwen2.5: biased q/k/v projections (added before RoPE)
+    # checkpoint RoPE scaling (ops/reference.py rope_inv_freq): ("linear", f) | ("llama3", f, low,
+    # high, original_max_pos) | ("yarn", f, original_max_pos, beta_fast, beta_slow, attention_factor)
+    rope_scaling: Optional[tuple] = None
 
     @property
     def q_size(self) -> int:
@@ -75,4 +78,6 @@ def get_config(name: str, **overrides) -> ModelConfig:
     if name not in PRESETS:
         raise KeyError(f"unknown model preset '{name}' (known: {', '.join(PRESETS)})")
     cfg = PRESETS[name]
+    if isinstance(overrides.get("rope_scaling"), list):   # from a JSON config
+        overrides = dict(overrides, rope_scaling=tuple(overrides["rope_scaling"]))
     return replace(cfg, **overrides) if overrides else cfg

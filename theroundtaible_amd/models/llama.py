@@ -61,7 +61,7 @@ class LlamaModel:
         self.n_kv_heads = self.tp.kv_heads(cfg.n_kv_heads)   # replicated when tp > KV heads
         self.head_dim = cfg.head_dim
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
-        self.cos_sin = rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device)
+        self.cos_sin = rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device, cfg.rope_scaling)
         self.layers = [{k.split(".", 2)[2]: v for k, v in weights.items() if k.startswith(f"layers.{i}.")}
                        for i in range(cfg.n_layers)]
         self.lm_rows = weights["lm_head"].shape[0]   # (vocab shard) rows of the lm_head

@@ -44,11 +44,56 @@ def fused_add_layer_norm(x, residual, w, b, eps):
     return layer_norm(r, w, b, eps), r
 
 
-def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+def rope_inv_freq(head_dim: int, theta: float, scaling: Optional[tuple] = None) -> Tuple[torch.Tensor, float]:
+    """RoPE inverse frequencies (fp64) and the cos / sin magnitude, for the checkpoint's
+    ``rope_scaling`` (``models/config.py`` ``ModelConfig.rope_scaling``):
+
+    * ``("linear", factor)``: positions / factor;
+    * ``("llama3", factor, low_freq_factor, high_freq_factor, original_max_pos)`` (Llama 3.1 / 3.2):
+      wavelengths past ``original / low`` divided by ``factor``, shorter than ``original / high``
+      kept, the band between interpolated smoothly;
+    * ``("yarn", factor, original_max_pos, beta_fast, beta_slow, attention_factor)`` (YaRN,
+      Qwen2.5 long context): per-dimension blend of interpolated / extrapolated frequencies over
+      the correction range, cos and sin scaled by ``attention_factor`` (the parser's default:
+      0.1 ln(factor) + 1).
+    The kernels read the resulting table; nothing else changes."""
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    mag = 1.0
+    if not scaling:
+        return inv, mag
+    kind = scaling[0]
+    if kind == "linear":
+        return inv / float(scaling[1]), mag
+    if kind == "llama3":
+        factor, low_ff, high_ff, orig = (float(v) for v in scaling[1:5])
+        wavelen = 2 * math.pi / inv
+        low_wl, high_wl = orig / low_ff, orig / high_ff
+        out = torch.where(wavelen > low_wl, inv / factor, inv)
+        smooth = (orig / wavelen - low_ff) / (high_ff - low_ff)
+        mid = (wavelen >= high_wl) & (wavelen <= low_wl)
+        return torch.where(mid, (1 - smooth) * out / factor + smooth * out, out), mag
+    if kind == "yarn":
+        factor, orig, beta_fast, beta_slow, att = (float(v) for v in scaling[1:6])
+
+        def corr_dim(rot):
+            return (head_dim * math.log(orig / (rot * 2 * math.pi))) / (2 * math.log(theta))
+        low = max(math.floor(corr_dim(beta_fast)), 0)
+        high = min(math.ceil(corr_dim(beta_slow)), head_dim - 1)
+        if low == high:
+            high += 0.001
+        ramp = ((torch.arange(head_dim // 2, dtype=torch.float64) - low) / (high - low)).clamp(0, 1)
+        extra = 1 - ramp                     # 1: keep the original frequency, 0: interpolate
+        out = (inv / factor) * (1 - extra) + inv * extra
+        return out, att
+    raise ValueError(f"unsupported rope_scaling {scaling!r}")
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None,
+                 scaling: Optional[tuple] = None) -> torch.Tensor:
+    inv, mag = rope_inv_freq(head_dim, theta, scaling)
     t = torch.arange(max_pos, dtype=torch.float64)
     f = torch.outer(t, inv)
-    return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)
+    return torch.cat([f.cos() * mag, f.sin() * mag], dim=-1).float().to(device)
 
 
 def _rotate(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import glob
 import json
+import math
 import os
 import re
 from dataclasses import dataclass, field
@@ -60,20 +61,57 @@ def is_non_chat_model(model_id: str) -> bool:
     return bool(NON_CHAT.search(model_id))
 
 
+def _rope_scaling(hf: Dict[str, Any]):
+    """config.json ``rope_scaling`` -> ModelConfig.rope_scaling; False when the type is unknown
+    (the checkpoint is then not offered: a silently different RoPE would be wrong text)."""
+    # transformers >= 5 writes "rope_parameters" (rope_theta inside), older files "rope_scaling"
+    rs = hf.get("rope_scaling") or hf.get("rope_parameters")
+    if not isinstance(rs, dict):
+        return None
+    kind = str(rs.get("rope_type", rs.get("type", "default"))).lower()
+    orig = int(rs.get("original_max_position_embeddings") or hf.get("max_position_embeddings", 8192))
+    if kind == "default":
+        return None
+    if kind == "linear":
+        return ("linear", float(rs["factor"]))
+    if kind == "llama3":
+        return ("llama3", float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)),
+                float(rs.get("high_freq_factor", 4.0)), orig)
+    if kind == "yarn":
+        factor = float(rs.get("factor") or hf.get("max_position_embeddings", orig) / orig)
+
+        def mscale(scale, m=1.0):
+            return 1.0 if scale <= 1 else 0.1 * m * math.log(scale) + 1.0
+        att = rs.get("attention_factor")
+        if att is None:
+            att = (mscale(factor, rs["mscale"]) / mscale(factor, rs["mscale_all_dim"])
+                   if rs.get("mscale") and rs.get("mscale_all_dim") else mscale(factor))
+        return ("yarn", factor, orig, float(rs.get("beta_fast") or 32.0), float(rs.get("beta_slow") or 1.0), float(att))
+    return False
+
+
+def _rope_theta(hf: Dict[str, Any], default: float = 10000.0) -> float:
+    rp = hf.get("rope_parameters") if isinstance(hf.get("rope_parameters"), dict) else {}
+    return float(hf.get("rope_theta") or rp.get("rope_theta") or default)
+
+
 def _shape_from_hf(hf: Dict[str, Any]) -> Optional[Dict[str, Any]]:
     mt = str(hf.get("model_type", "")).lower()
     if mt in ("llama", "mistral", "qwen2"):
         if hf.get("attention_bias") or hf.get("mlp_bias"):
             return None   # biased o / MLP projections (Llama variants): not in the engine's layer
+        scaling = _rope_scaling(hf)
+        if scaling is False:
+            return None   # a RoPE scaling the engine does not implement
         h = int(hf["hidden_size"])
         nh = int(hf["num_attention_heads"])
         return {"arch": "llama", "n_layers": int(hf["num_hidden_layers"]), "hidden": h, "n_heads": nh,
                 "n_kv_heads": int(hf.get("num_key_value_heads", nh)), "head_dim": int(hf.get("head_dim", h // nh)),
                 "ffn": int(hf["intermediate_size"]), "vocab": int(hf["vocab_size"]),
                 "max_pos": int(hf.get("max_position_embeddings", 8192)),
-                "rope_theta": float(hf.get("rope_theta", 10000.0)), "norm_eps": float(hf.get("rms_norm_eps", 1e-5)),
+                "rope_theta": _rope_theta(hf), "norm_eps": float(hf.get("rms_norm_eps", 1e-5)),
                 "tie_embeddings": bool(hf.get("tie_word_embeddings", False)),
-                "qkv_bias": mt == "qwen2"}
+                "qkv_bias": mt == "qwen2", "rope_scaling": scaling}
     if mt == "gpt2":
         h = int(hf["n_embd"])
         nh = int(hf["n_head"])
