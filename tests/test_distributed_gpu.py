@@ -251,7 +251,10 @@ def test_fused_ar_correct_at_tp4_tp8_with_cu_split_on_shared_gpu(tp):
     launch shapes that follow the CU count): prefill and decode logits cosine > 0.999."""
     cus = 256 // tp
     ref = _tp_check(1, "llama3-8b", 2, env_extra={"ROC_GLOBAL_CU_MASK": hex((1 << cus) - 1)}, tag=f"_cu{cus}")
-    got = _tp_check(tp, "llama3-8b", 2, extra=("--graphs", "--poll-limit", "262144"), fused_ar=True,
+    # poll bound 2^22 (~4 s): four processes time-share one card's queues, and at 2^18 one
+    # scheduling gap in 6 round-6 suites read as an expired wait (profiles/r06/final_z/README.md);
+    # a lost peer still fails within seconds
+    got = _tp_check(tp, "llama3-8b", 2, extra=("--graphs", "--poll-limit", str(1 << 22)), fused_ar=True,
                     env_extra={"ROUNDTABLE_REHEARSAL_CU_SPLIT": "1"}, tag="_cusplit")
     assert got["fused_ar"] and got["fused_ar_calls"] > 0 and all(got["graphs_per_rank"]), got
     assert all(e is None for e in got["errors"]) and not got["flag_errors"], got["errors"]
