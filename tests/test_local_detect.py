@@ -58,6 +58,11 @@ def test_detect_qwen2_family(tmp_path):
     assert set(found) == {"Qwen2.5-7B-Instruct", "Qwen2.5-Coder-0.5B"}
     assert found["Qwen2.5-7B-Instruct"].preset == "qwen2.5-7b" and found["Qwen2.5-7B-Instruct"].overrides == {}
     assert found["Qwen2.5-Coder-0.5B"].preset == "qwen2.5-0.5b" and found["Qwen2.5-Coder-0.5B"].overrides == {}
+    from theroundtaible_amd.models.config import get_config
+    # preset shapes = the published parameter counts (0.49 / 7.6 / 14.7 / 32.8 / 72.7 B)
+    for name, b in (("qwen2.5-0.5b", 0.49), ("qwen2.5-7b", 7.62), ("qwen2.5-14b", 14.77), ("qwen2.5-32b", 32.76),
+                    ("qwen2.5-72b", 72.71)):
+        assert abs(get_config(name).n_params() / 1e9 - b) < 0.01, name
 
 
 def test_rope_scaling_and_theta_formats(tmp_path):

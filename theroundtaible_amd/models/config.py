@@ -60,6 +60,12 @@ PRESETS: Dict[str, ModelConfig] = {
     # 0.5B: head_dim 64, tied embeddings (the family most local coding setups run)
     "qwen2.5-7b": ModelConfig("qwen2.5-7b", "llama", 28, 3584, 28, 4, 128, 18944, 152064, 32768, 1000000.0, 1e-6,
                               False, True),
+    "qwen2.5-14b": ModelConfig("qwen2.5-14b", "llama", 48, 5120, 40, 8, 128, 13824, 152064, 32768, 1000000.0, 1e-6,
+                               False, True),
+    "qwen2.5-32b": ModelConfig("qwen2.5-32b", "llama", 64, 5120, 40, 8, 128, 27648, 152064, 32768, 1000000.0, 1e-6,
+                               False, True),
+    "qwen2.5-72b": ModelConfig("qwen2.5-72b", "llama", 80, 8192, 64, 8, 128, 29568, 152064, 32768, 1000000.0, 1e-6,
+                               False, True),
     "qwen2.5-0.5b": ModelConfig("qwen2.5-0.5b", "llama", 24, 896, 14, 2, 64, 4864, 151936, 32768, 1000000.0, 1e-6,
                                 True, True),
     # GPT-2-small: random init allows n_positions beyond 1024 (SURVEY §7.3 hard part 3).
