@@ -121,3 +121,53 @@ def test_knight_on_checkpoint_dir_without_overrides(tmp_path):
     assert b.engine.cfg.vocab == V and b.engine.cfg.hidden == 256
     res = b.execute("De koning spreekt.", 60.0, seq_key="Local")
     assert isinstance(res.text, str) and len(res.ids) == 3
+
+
+QWEN_SPECIAL = ["<|endoftext|>", "<|im_start|>", "<|im_end|>"]
+CHATML_TEMPLATE = (   # Qwen2.5's ChatML with its default system turn (trimmed to the parts a turn uses)
+    "{%- if messages[0]['role'] != 'system' %}{{- '<|im_start|>system\\nYou are Qwen, created by Alibaba Cloud. "
+    "You are a helpful assistant.<|im_end|>\\n' }}{%- endif %}{%- for message in messages %}"
+    "{{- '<|im_start|>' + message['role'] + '\\n' + message['content'] + '<|im_end|>' + '\\n' }}{%- endfor %}"
+    "{%- if add_generation_prompt %}{{- '<|im_start|>assistant\\n' }}{%- endif %}")
+
+
+def test_qwen_chatml_checkpoint(tmp_path):
+    """A Qwen2.5-style checkpoint: ChatML template with its default system turn, no BOS, stops at
+    <|im_end|> and <|endoftext|>; the architecture (q/k/v biases, tied head) comes from config.json."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    from theroundtaible_amd.utils.local_detect import resolve_model
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    corpus = ["You are Qwen, created by Alibaba Cloud. You are a helpful assistant.",
+              "De ridders van de ronde tafel bespreken de kernel en de cache."] * 20
+    tok.train_from_iterator(corpus, trainers.BpeTrainer(vocab_size=400, special_tokens=QWEN_SPECIAL,
+                                                        initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    tok.save(str(tmp_path / "tokenizer.json"))
+    V = tok.get_vocab_size()
+    end, ims, ime = (tok.token_to_id(s) for s in QWEN_SPECIAL)
+    torch.manual_seed(0)
+    m = transformers.Qwen2ForCausalLM(transformers.Qwen2Config(
+        hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
+        vocab_size=V, max_position_embeddings=4096, rope_theta=1e6, rms_norm_eps=1e-6, tie_word_embeddings=True,
+        bos_token_id=end, eos_token_id=ime, use_sliding_window=False))
+    m.save_pretrained(str(tmp_path), safe_serialization=True)
+    (tmp_path / "tokenizer_config.json").write_text(json.dumps({"bos_token": None, "eos_token": "<|im_end|>",
+                                                                "chat_template": CHATML_TEMPLATE}))
+    (tmp_path / "generation_config.json").write_text(json.dumps({"bos_token_id": end, "eos_token_id": [ime, end]}))
+    model, ov = resolve_model("tiny-llama", str(tmp_path))
+    assert ov.get("qkv_bias", True) and ov.get("vocab") == V
+    e = Engine(EngineConfig(model=model, weights=str(tmp_path), device="cpu", dtype="fp32", num_blocks=64,
+                            model_overrides=ov))
+    assert e.cfg.qkv_bias and e.cfg.tie_embeddings and e.tokenizer.stop_ids == {ime, end}
+    text = "De ridders bespreken de cache."
+    want = tok.encode("<|im_start|>system\nYou are Qwen, created by Alibaba Cloud. You are a helpful assistant."
+                      "<|im_end|>\n<|im_start|>user\n" + text + "<|im_end|>\n<|im_start|>assistant\n").ids
+    assert e.encode_prompt(text) == want
+    sp = SamplingParams(temperature=0.0, max_new_tokens=4, ignore_eos=True, stop_on_consensus=False)
+    r = e.run_turns([Turn("K", text, sp)])[0]
+    assert r.error is None and len(r.ids) == 4
+    with torch.no_grad():    # the engine's greedy tokens are transformers' on the same prompt
+        gen = m.generate(torch.tensor([want]), max_new_tokens=4, do_sample=False, pad_token_id=end,
+                         eos_token_id=None)[0, len(want):].tolist()
+    assert r.ids == gen
