@@ -44,7 +44,8 @@ def _tp_worker(rank, world, port, model, q, overrides=None):
 
 @pytest.mark.parametrize("model,tp,overrides", [("tiny-llama", 2, None), ("tiny-gpt2", 2, None),
                                                  ("tiny-llama", 4, {"n_kv_heads": 4}),
-                                                 ("tiny-llama", 4, None)])     # 2 KV heads: replicated
+                                                 ("tiny-llama", 4, None),      # 2 KV heads: replicated
+                                                 ("tiny-qwen", 2, None)])      # q/k/v bias sharded with the heads
 def test_tp_matches_tp1(model, tp, overrides):
     """TP=2/4 forward + greedy decode equal TP=1; the TP decode samples
     greedily with the per-rank argmax + (value, id) all-gather (C3), so identical tokens show the
