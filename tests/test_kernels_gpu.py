@@ -80,7 +80,7 @@ def test_rope_and_cache(hq, hkv, d, rope):
 
 
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 2, 128), (4, 1, 128),
-                                      (8, 1, 128), (28, 4, 128), (14, 2, 64)])
+                                      (8, 1, 128), (28, 4, 128), (14, 2, 64), (24, 8, 128)])
 @pytest.mark.parametrize("splits", [1, 3, 8, 64])
 def test_paged_decode(hq, hkv, d, splits):
     lens = [1, 31, 32, 33, 257, 1500]
@@ -120,7 +120,7 @@ def _check_planned(out, q, kc, vc, bt, cl, scale, splits, ws, hq, hkv, groups=No
 
 
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (8, 2, 128), (12, 12, 64), (4, 1, 128),
-                                      (28, 4, 128)])
+                                      (28, 4, 128), (24, 8, 128)])
 @pytest.mark.parametrize("splits", [1, 3, 10, 64])
 @pytest.mark.parametrize("layout", ["table3", "mixed"])
 def test_paged_decode_shared_prefix_groups(hq, hkv, d, splits, layout):

@@ -59,9 +59,9 @@ def test_detect_qwen2_family(tmp_path):
     assert found["Qwen2.5-7B-Instruct"].preset == "qwen2.5-7b" and found["Qwen2.5-7B-Instruct"].overrides == {}
     assert found["Qwen2.5-Coder-0.5B"].preset == "qwen2.5-0.5b" and found["Qwen2.5-Coder-0.5B"].overrides == {}
     from theroundtaible_amd.models.config import get_config
-    # preset shapes = the published parameter counts (0.49 / 7.6 / 14.7 / 32.8 / 72.7 B)
+    # preset shapes = the published parameter counts (Qwen2.5 0.5-72B, Llama 3.1-8B, 3.2-1B / 3B)
     for name, b in (("qwen2.5-0.5b", 0.49), ("qwen2.5-7b", 7.62), ("qwen2.5-14b", 14.77), ("qwen2.5-32b", 32.76),
-                    ("qwen2.5-72b", 72.71)):
+                    ("qwen2.5-72b", 72.71), ("llama3.1-8b", 8.03), ("llama3.2-1b", 1.24), ("llama3.2-3b", 3.21)):
         assert abs(get_config(name).n_params() / 1e9 - b) < 0.01, name
 
 
@@ -73,7 +73,7 @@ def test_rope_scaling_and_theta_formats(tmp_path):
                                          "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
     _ckpt(str(tmp_path / "Llama-3.1-8B"), l31)
     preset, ov = checkpoint_model(str(tmp_path / "Llama-3.1-8B"))
-    assert preset == "llama3-8b" and ov == {"rope_scaling": ("llama3", 8.0, 1.0, 4.0, 8192)}
+    assert preset == "llama3.1-8b" and ov == {}
     v5 = {k: v for k, v in LLAMA8B_HF.items() if k != "rope_theta"}
     v5["rope_parameters"] = {"rope_theta": 500000.0, "rope_type": "default"}
     _ckpt(str(tmp_path / "v5"), v5)

@@ -54,6 +54,14 @@ class ModelConfig:
 
 PRESETS: Dict[str, ModelConfig] = {
     "llama3-8b": ModelConfig("llama3-8b", "llama", 32, 4096, 32, 8, 128, 14336, 128256, 131072, 500000.0, 1e-5),
+    # Llama 3.1 / 3.2: the same blocks with rope_type "llama3" scaling (3.2: tied embeddings;
+    # 3.2-3B has GQA group 3)
+    "llama3.1-8b": ModelConfig("llama3.1-8b", "llama", 32, 4096, 32, 8, 128, 14336, 128256, 131072, 500000.0, 1e-5,
+                               False, False, ("llama3", 8.0, 1.0, 4.0, 8192)),
+    "llama3.2-1b": ModelConfig("llama3.2-1b", "llama", 16, 2048, 32, 8, 64, 8192, 128256, 131072, 500000.0, 1e-5,
+                               True, False, ("llama3", 32.0, 1.0, 4.0, 8192)),
+    "llama3.2-3b": ModelConfig("llama3.2-3b", "llama", 28, 3072, 24, 8, 128, 8192, 128256, 131072, 500000.0, 1e-5,
+                               True, False, ("llama3", 32.0, 1.0, 4.0, 8192)),
     "llama3-70b": ModelConfig("llama3-70b", "llama", 80, 8192, 64, 8, 128, 28672, 128256, 131072, 500000.0, 1e-5),
     "mistral-7b": ModelConfig("mistral-7b", "llama", 32, 4096, 32, 8, 128, 14336, 32000, 32768, 1000000.0, 1e-5),
     # Qwen2.5 (HF model_type "qwen2"): the Llama block with q/k/v biases; 7B: GQA 28 / 4 heads,
