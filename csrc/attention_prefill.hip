@@ -237,7 +237,8 @@ int launch_prefill32(void* out, const void* q, const void* k_cache, const void* 
                      int max_blocks, float scale, hipStream_t stream, int map_stride, const int* cmap, int n_split,
                      float* part_o, float* part_ml);
 
-// D = 128 with G in {1, 2, 4, 8} runs the 32x32-MFMA kernel (attention_prefill32.hip) unless
+// D = 128 with G <= 8 (a non-power-of-two group in the next power of two of head slots) runs the
+// 32x32-MFMA kernel (attention_prefill32.hip) unless
 // ROUNDTABLE_PREFILL16=1; everything else this file's 16x16 kernel. The host tile map must use
 // the rows of the kernel that will run, hence one function for both.
 static bool use_prefill32(int G, int D) {
@@ -285,7 +286,7 @@ int launch_prefill(void* out, const void* q, const void* k_cache, const void* v_
   return 0;
 }
 
-// Key-split prefill (32x32 kernel only: D = 128, G in {1, 2, 4, 8}): items [n_items, 5] (sequence,
+// Key-split prefill (32x32 kernel only: D = 128, G <= 8): items [n_items, 5] (sequence,
 // first row, first / end key tile, partial slot or -1), cmap [n_split, 4] (sequence, first row,
 // first slot, parts). For launches with fewer tiles than CUs (tensor-parallel shards: one or two
 // KV heads per rank), where whole tiles would leave most CUs idle.

@@ -6,7 +6,8 @@
 // reads from LDS feeds a full 32x32x16 MFMA (four times the work per LDS byte of the 16x16
 // kernel).
 //
-// Workgroup = 8 waves: wave w -> head hk*G + w%G, rows row0 + 32*(w/G) .. +31 (256/G rows
+// Workgroup = 8 waves over G head slots (G a power of two >= the GQA group; surplus slots idle):
+// wave w -> head slot w%G, rows row0 + 32*(w/G) .. +31 (256/G rows
 // per workgroup: two waves per SIMD, each K/V tile feeds 8 x 32 query rows). Per 64-key
 // tile (two cache blocks):
 //   S^T[64 keys x 32 q] = K . Q^T      2 key blocks x 8 d-chunks   (A = K rows from LDS, B = Q^T regs)
@@ -123,7 +124,12 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
   const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 31, h = lane >> 5;   // MFMA column (query) and k-half
 
-  const int head = hk * G + (wid % G);
+  // G = head slots per kv head (a power of two); the real group Gr <= G (Qwen2.5: 7 in 8 slots,
+  // Llama-3.2-3B: 3 in 4): a surplus slot's wave loads and barriers with the others, skips the
+  // math and stores nothing
+  const int Gr = Hq / Hkv, slot_h = wid % G;
+  const bool head_ok = slot_h < Gr;
+  const int head = hk * Gr + min(slot_h, Gr - 1);
   const int wrow0 = row0 + 32 * (wid / G);
   const int tile_rows_end = min(row0 + rows_per_tile, q_end);
   const int kmax = sp + (tile_rows_end - q_begin);  // keys [0, kmax) for the whole workgroup
@@ -141,7 +147,7 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
   const int my_pos = sp + (my_row - q_begin);
   // keys this wave can ever see (tiles past it are still loaded cooperatively, math skipped)
   const int wave_rows_end = min(wrow0 + 32, q_end);
-  const int wave_kmax = sp + (wave_rows_end - q_begin);
+  const int wave_kmax = head_ok ? sp + (wave_rows_end - q_begin) : 0;
   const int wave_min_pos = sp + (min(wrow0, q_end - 1) - q_begin);   // first row of the wave
 
   // Q^T B-fragments: lane (q = c, h) holds Q[q][16 dk + 8 h + j]
@@ -330,7 +336,7 @@ __global__ void __launch_bounds__(NW * 64) prefill32_kernel(
     if (h == 0) *reinterpret_cast<float2*>(part_ml + 2 * slot) = make_float2(m, lsum);
     return;
   }
-  if (row < q_end && row < row0 + rows_per_tile) {
+  if (head_ok && row < q_end && row < row0 + rows_per_tile) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     uint16_t* orow = out + ((size_t)row * Hq + head) * D;
 #pragma unroll
@@ -358,8 +364,9 @@ __global__ void __launch_bounds__(NW * 32) prefill32_combine_kernel(uint16_t* __
   const int w = threadIdx.x >> 5, c = threadIdx.x & 31;
   const int s = cmap[4 * st], row0 = cmap[4 * st + 1], p0 = cmap[4 * st + 2], np = cmap[4 * st + 3];
   const int row = row0 + 32 * (w / G) + c;
-  if (row >= cu_q[s + 1] || row >= row0 + rows_per_tile) return;
-  const int head = hk * G + (w % G);
+  const int Gr = Hq / Hkv;   // real group in G slots (prefill32_kernel)
+  if (row >= cu_q[s + 1] || row >= row0 + rows_per_tile || w % G >= Gr) return;
+  const int head = hk * Gr + (w % G);
   const int d0 = 16 * blockIdx.y;
   constexpr int PC = 4;   // parts per chunk of loads
   float M = -INFINITY, L = 0.f;
@@ -402,10 +409,15 @@ __global__ void __launch_bounds__(NW * 32) prefill32_combine_kernel(uint16_t* __
 }
 }  // namespace
 
+// head slots for group size G: the next power of two (surplus slots idle); 0 = unsupported
+static int prefill32_slots(int G) {
+  return G == 1 ? 1 : G == 2 ? 2 : G <= 4 ? 4 : G <= 8 ? 8 : 0;
+}
+
 // rows of one work tile for group size G (D = 128); 0 = unsupported (use attention_prefill.hip)
 int prefill32_rows(int G) {
-  if (G == 1 || G == 2 || G == 4 || G == 8) return 32 * 8 / G;   // 8 waves x 32 rows over G heads
-  return 0;
+  const int slots = prefill32_slots(G);
+  return slots ? 32 * 8 / slots : 0;   // 8 waves x 32 rows over the G heads' slots
 }
 
 // tile_map [n_tiles, map_stride]: map_stride 2 = (sequence, first row), every tile whole;
@@ -437,7 +449,7 @@ int launch_prefill32(void* out, const void* q, const void* k_cache, const void* 
   if (map_stride == 5 && n_split > 0)                                                                            \
     hipLaunchKernelGGL((prefill32_combine_kernel<GG, NWV>), dim3(n_split * Hkv, D / 16), dim3(32 * NWV), 0, stream, \
                        (uint16_t*)out, cmap, cu_q, (const float*)part_o, (const float*)part_ml, Hq, Hkv, rows)
-  switch (G) {
+  switch (prefill32_slots(G)) {
     case 1: RT_P32(1, 8); break;
     case 2: RT_P32(2, 8); break;
     case 4: RT_P32(4, 8); break;

@@ -219,8 +219,9 @@ def test_paged_decode_spike():
 @pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (64, 8, 128), (12, 12, 64), (8, 4, 128), (16, 1, 128),
                                       (28, 4, 128), (14, 2, 64), (12, 4, 128), (12, 1, 64)])
 def test_prefill_varlen(hq, hkv, d):
-    """Includes GQA groups that are not powers of two (Qwen2.5: G = 7; G = 3, 12): the 16x16
-    kernel's surplus head slots stay idle."""
+    """Includes GQA groups that are not powers of two (Qwen2.5: G = 7; Llama-3.2-3B: G = 3; 12):
+    D = 128 groups up to 8 run the 32x32 kernel in the next power of two of head slots, the others
+    the 16x16 kernel; surplus head slots stay idle in both."""
     # (start_pos, new tokens): prefix already cached + delta chunk
     specs = [(0, 1), (0, 45), (100, 70), (31, 33), (500, 17)]
     S = len(specs)
@@ -272,7 +273,7 @@ def test_prefill_long_prefix():
     close(out, exp.to(DEV), 0.02, 0.02)
 
 
-@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (32, 8)])
+@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (32, 8), (28, 4), (12, 4)])
 @pytest.mark.parametrize("min_chunk", [1, 3, 8])
 def test_prefill_key_split(hq, hkv, min_chunk):
     """Key-split prefill (tensor-parallel shard head counts: few tiles x KV heads): work items
