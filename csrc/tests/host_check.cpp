@@ -91,7 +91,10 @@ int main() {
   EXPECT(launch_paging_guard(nullptr, nullptr, nullptr, nullptr, nullptr, 0, 4, 16, 32, nullptr) == 0);
   EXPECT(launch_decode_advance(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 8, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, nullptr) == 0);
   // prefill tile geometry
-  EXPECT(prefill32_rows(4) == 64 && prefill32_rows(8) == 32 && prefill32_rows(1) == 256 && prefill32_rows(3) == 0);
+  // (a group that is not a power of two takes the next power of two of head slots: G = 3 -> 4,
+  // G = 7 -> 8; past 8 the 16x16 kernel runs)
+  EXPECT(prefill32_rows(4) == 64 && prefill32_rows(8) == 32 && prefill32_rows(1) == 256 && prefill32_rows(3) == 64 &&
+         prefill32_rows(7) == 32 && prefill32_rows(5) == 32 && prefill32_rows(12) == 0 && prefill32_rows(16) == 0);
   std::printf("host_check: %d failure(s)\n", failures);
   return failures ? 1 : 0;
 }
